@@ -1,0 +1,145 @@
+/*
+ * visreps_hip.h — C ABI of libvisreps_hip.so, the MI355X (gfx950) implementation of
+ * the visreps RSA eval hot path: N×N Pearson RDM → upper-triangle midrank Spearman →
+ * bootstrapped Spearman RSA.
+ *
+ * The reference (yashsmehta/visreps) has no FFI: its boundary is the Python module API
+ * (visreps/analysis/rsa.py). Each entry point below names the reference function or
+ * loop it replaces; the Python mirror in visreps_amd/analysis/rsa.py binds them with
+ * ctypes.
+ *
+ * Conventions
+ *  - Every function returns int status: VR_OK (0) or a negative VR_E* code; the
+ *    message of the last failure on the calling thread is vr_last_error().
+ *  - Array pointers marked [dev] are caller-owned device pointers (hipMalloc /
+ *    torch.Tensor.data_ptr()); [host] pointers are host memory.
+ *  - Scratch memory comes from a caller-provided workspace whose size is given by the
+ *    matching *_workspace() query. The library never allocates caller-visible memory.
+ *  - `stream` is a hipStream_t passed as void*; device work is asynchronous on it.
+ *    Functions are reentrant across distinct streams and workspaces.
+ *  - A statistic that is undefined (constant input, NaN input, fewer than two pairs)
+ *    is returned as NaN in the output value, never as an error status — the same
+ *    contract as compute_rdm_correlation (rsa.py:106-109,123-129).
+ */
+#ifndef VISREPS_HIP_H
+#define VISREPS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VR_OK 0
+#define VR_EINVAL (-1)    /* invalid argument (shape, pointer, size) */
+#define VR_EHIP (-2)      /* HIP runtime error */
+#define VR_EWORKSPACE (-3) /* workspace smaller than the *_workspace() query */
+
+/* Library version (major*10000 + minor*100 + patch). */
+int vr_version(void);
+/* Message of the last failing call on this thread ("" if none). */
+const char* vr_last_error(void);
+
+/* ------------------------------------------------------------------------------
+ * RDM: replaces compute_rdm(X, correlation="Pearson", correction)
+ *      visreps/analysis/rsa.py:59-93 (x.float(); x -= mean; std = sqrt(mean(x^2)+c);
+ *      zero-variance guard; cov = x@x.T/D; corr = cov/(std_i std_j + c); clamp; diag=1;
+ *      rdm = 1 - corr).
+ * X [dev] fp32 row-major (n, d) with leading dimension ldx >= d.
+ * rdm [dev] fp32 row-major (n, n) with leading dimension ldr >= n. Exactly symmetric,
+ * diagonal exactly 0.
+ * -------------------------------------------------------------------------- */
+size_t vr_rdm_pearson_workspace(int64_t n, int64_t d);
+int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
+                       int64_t ldr, float correction, void* ws, size_t ws_bytes,
+                       void* stream);
+
+/* Row statistics of the same RDM (rsa.py:80-87): mean[i] (fp32) and
+ * std[i] = sqrt(mean((x-mean)^2) + correction) with std < 10*correction -> 1.
+ * Exposed so extraction can emit them alongside the feature rows. */
+int vr_row_stats_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* mean,
+                     float* stdv, float correction, void* stream);
+
+/* ------------------------------------------------------------------------------
+ * Rank plans: the one-time per-RDM precompute behind every Spearman on that RDM.
+ * The strict upper triangle (torch.triu_indices(n, n, 1) order, rsa.py:111) is
+ * sorted by value once (LSD radix sort, -0.0 == +0.0), tie groups (equal fp32 values)
+ * are marked, and the positions are cut into chunks aligned to group boundaries.
+ * Replaces the per-call scipy.stats.rankdata(.., 'average') inside
+ * scipy.stats.spearmanr (rsa.py:43-47,121-122).
+ * plan [dev]: vr_rank_plan_bytes(n) bytes, owned by the caller, reused across calls.
+ * -------------------------------------------------------------------------- */
+size_t vr_rank_plan_bytes(int64_t n);
+size_t vr_rank_plan_workspace(int64_t n);
+int vr_rank_plan_build_f32(const float* rdm, int64_t n, int64_t ld, void* plan,
+                           size_t plan_bytes, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------
+ * Spearman of two RDMs' upper triangles: replaces
+ * compute_rdm_correlation(rdm1, rdm2, correlation="Spearman") (rsa.py:96-129).
+ * out [dev] one double. NaN if n<=1, any NaN value, or a constant triangle.
+ * -------------------------------------------------------------------------- */
+size_t vr_spearman_triu_workspace(int64_t n);
+int vr_spearman_triu_f32(const float* A, const float* B, int64_t n, int64_t ld,
+                         double* out, void* ws, size_t ws_bytes, void* stream);
+
+/* Pearson of the two upper triangles (fp64), replacing
+ * compute_rdm_correlation(.., correlation="Pearson") -> scipy.stats.pearsonr. */
+size_t vr_pearson_triu_workspace(int64_t n);
+int vr_pearson_triu_f32(const float* A, const float* B, int64_t n, int64_t ld,
+                        double* out, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------
+ * Bootstrapped Spearman RSA: replaces the loop
+ *   for i in range(n_bootstrap):
+ *       idx = rng.choice(n, int(0.9n), replace=False)
+ *       scores[i] = compute_rdm_correlation(A[idx][:, idx], B[idx][:, idx], "Spearman")
+ * visreps/evals.py:355-373 (identical copies evals.py:506-522, rsa.py:233-261).
+ *
+ * The engine evaluates 64 subsets per pass (one bit per subset in a per-stimulus
+ * 64-bit inclusion mask); every score is exact integer midrank arithmetic on the
+ * pre-sorted plans, so results do not depend on pass grouping or GPU count.
+ *
+ * idx [dev] int32 (n_sets, k): stimulus indices of each subset (distinct, in [0,n)).
+ *   If full_first != 0 an extra first subset = all n stimuli is evaluated and its
+ *   score written to scores[0] (the point estimate, evals.py:347-349), followed by the
+ *   n_sets subset scores. scores [dev] double (n_sets + (full_first?1:0)).
+ * -------------------------------------------------------------------------- */
+size_t vr_bootstrap_workspace(int64_t n);
+int vr_bootstrap_spearman_plans(const void* planA, const void* planB, int64_t n,
+                                const int32_t* idx, int64_t k, int64_t n_sets,
+                                int full_first, double* scores, void* ws,
+                                size_t ws_bytes, void* stream);
+
+/* One-shot form: builds both plans in the workspace, then runs the engine. */
+size_t vr_bootstrap_spearman_workspace(int64_t n);
+int vr_bootstrap_spearman_f32(const float* A, const float* B, int64_t n, int64_t ld,
+                              const int32_t* idx, int64_t k, int64_t n_sets,
+                              int full_first, double* scores, void* ws, size_t ws_bytes,
+                              void* stream);
+
+/* ------------------------------------------------------------------------------
+ * Host: legacy numpy RandomState (MT19937) index streams, bit-exact.
+ * Replaces np.random.RandomState(seed) + .choice(n, k, replace=False) / .permutation(n)
+ * (evals.py:260-261,356,362-364; rsa.py:169,176,248-250; evals.py:111-113).
+ * -------------------------------------------------------------------------- */
+/* Opaque generator state (caller-allocated, vr_rng_state_bytes() bytes). */
+size_t vr_rng_state_bytes(void);
+int vr_rng_seed(void* state, uint32_t seed);                /* RandomState(seed) */
+int vr_rng_permutation(void* state, int64_t n, int32_t* out); /* .permutation(n) */
+int vr_rng_choice(void* state, int64_t n, int64_t k, int32_t* out); /* .choice(n,k,replace=False) */
+int vr_rng_random_u32(void* state, int64_t count, uint32_t* out);   /* raw MT19937 draws */
+/* Convenience: fresh RandomState(seed), then n_draws successive choice(n, k) calls
+ * into out (n_draws, k) [host]. */
+int vr_legacy_choice(uint32_t seed, int64_t n, int64_t k, int64_t n_draws, int32_t* out);
+
+/* numpy.percentile(x, q) with the default 'linear' method (evals.py:371-372),
+ * NaN-propagating. x [host] double (n). Returns the percentile (NaN if n == 0). */
+double vr_percentile_linear(const double* x, int64_t n, double q);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VISREPS_HIP_H */

@@ -1,0 +1,239 @@
+"""HIP path vs the CPU oracle (oracle/rsa_oracle.py) on seeded inputs.
+
+Tolerances
+  * RDM entries: |delta| <= 2e-5 (fp32 Gram, different summation order; the reference's
+    own torch-CPU sgemm differs from any other fp32 order at this level).
+  * Spearman on identical RDM inputs: |delta| <= 1e-12 (both exact midrank arithmetic;
+    scipy's float64 corrcoef rounding is ~1e-15).
+  * Spearman / RSA scores where each side builds its own RDM: |delta| < 1e-5
+    (BASELINE.json north_star tolerance).
+  * Bootstrap index sets: bit-exact (legacy MT19937 stream).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import rsa_oracle as O
+from visreps_amd.analysis import rsa as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(n, d, seed=0, scale=1.0):
+    return np.random.RandomState(seed).randn(n, d).astype(np.float32) * scale
+
+
+# --------------------------------------------------------------------------- RDM
+@pytest.mark.parametrize("n,d", [(1, 5), (2, 3), (3, 7), (17, 33), (130, 257), (300, 1000),
+                                 (129, 4100), (64, 1), (200, 6)])
+def test_rdm_matches_oracle(dev, n, d):
+    x = _rand(n, d, seed=n * 7 + d)
+    got = R.compute_rdm(torch.from_numpy(x).to(dev)).cpu().numpy()
+    ref = O.compute_rdm(x)
+    assert got.dtype == np.float32 and got.shape == (n, n)
+    assert np.array_equal(got, got.T), "RDM must be exactly symmetric"
+    assert np.all(np.diag(got) == 0.0)
+    assert np.max(np.abs(got - ref)) <= 2e-5
+
+
+def test_rdm_split_k_conv5_shape(dev):
+    # cfg1 shape: N=256 stimuli x conv5 D=43264 -> split-K path
+    x = np.maximum(_rand(256, 43264, seed=5), 0)
+    got = R.compute_rdm(torch.from_numpy(x).to(dev)).cpu().numpy()
+    ref = O.compute_rdm(x)
+    assert np.array_equal(got, got.T)
+    assert np.max(np.abs(got - ref)) <= 2e-5
+
+
+def test_rdm_cpu_input_returns_cpu(dev):
+    x = torch.from_numpy(_rand(20, 10))
+    rdm = R.compute_rdm(x)
+    assert rdm.device.type == "cpu" and rdm.dtype == torch.float32
+
+
+def test_rdm_known_values(dev):
+    # tests/test_rsa_bootstrap.py:214-225 and 1017-1033
+    x = torch.tensor([[1.0, 2.0, 3.0, 4.0, 5.0], [2.0, 4.0, 6.0, 8.0, 10.0],
+                      [5.0, 3.0, 1.0, -1.0, -3.0]])
+    rdm = R.compute_rdm(x)
+    assert rdm[0, 1].item() == pytest.approx(0.0, abs=1e-4)
+    assert rdm[0, 2].item() == pytest.approx(2.0, abs=1e-4)
+    assert R.compute_rdm(torch.tensor([[1.0, 2.0, 3.0], [1.0, 2.0, 3.0]]))[0, 1].item() == pytest.approx(0.0, abs=1e-5)
+    assert R.compute_rdm(torch.tensor([[1.0, 2.0, 3.0], [-1.0, -2.0, -3.0]]))[0, 1].item() == pytest.approx(2.0, abs=1e-4)
+
+
+def test_rdm_zero_variance_rows_finite(dev):
+    x = torch.randn(10, 5)
+    x[3] = 5.0
+    x[7] = -2.0
+    rdm = R.compute_rdm(x)
+    assert torch.isfinite(rdm).all()
+    assert torch.all(rdm.diag() == 0.0)
+    ref = O.compute_rdm(x.numpy())
+    assert np.max(np.abs(rdm.numpy() - ref)) <= 2e-5
+
+
+def test_rdm_spearman_is_pearson_on_ranks(dev):
+    x = torch.from_numpy(_rand(12, 20, seed=3))
+    a = R.compute_rdm(x, correlation="Spearman")
+    b = R.compute_rdm(R._rank(x), correlation="Pearson")
+    assert torch.equal(a, b)
+    ref = O.compute_rdm(x.numpy(), correlation="Spearman")
+    assert np.max(np.abs(a.numpy() - ref)) <= 2e-5
+
+
+def test_rdm_invalid_method():
+    with pytest.raises(ValueError):
+        R.compute_rdm(torch.randn(5, 3), correlation="cosine")
+
+
+def test_rdm_does_not_mutate(dev):
+    x = torch.randn(10, 5, device=dev)
+    x0 = x.clone()
+    R.compute_rdm(x)
+    R.compute_rdm(x, correlation="Spearman")
+    assert torch.equal(x, x0)
+
+
+# --------------------------------------------------------------------------- Spearman
+def _tied_rdm(n, seed, levels=None):
+    rng = np.random.RandomState(seed)
+    m = rng.rand(n, n).astype(np.float32)
+    if levels:
+        m = np.floor(m * levels).astype(np.float32) / levels
+    m = np.triu(m, 1)
+    return (m + m.T).astype(np.float32)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 16, 63, 64, 65, 257, 1000])
+@pytest.mark.parametrize("levels", [None, 7, 1000])
+def test_spearman_exact_vs_oracle(dev, n, levels):
+    a = _tied_rdm(n, 1 + n, levels)
+    b = _tied_rdm(n, 2 + n, levels)
+    got = R.compute_rdm_correlation(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev),
+                                    correlation="Spearman")
+    iu = np.triu_indices(n, 1)
+    exact = O.midrank_spearman(a[iu], b[iu])
+    ref = O.compute_rdm_correlation(a, b, "Spearman")
+    if math.isnan(exact):
+        assert math.isnan(got) and math.isnan(ref)
+    else:
+        assert abs(got - exact) <= 1e-12
+        assert abs(got - ref) <= 1e-9
+
+
+def test_spearman_nan_and_constant(dev):
+    a = _tied_rdm(10, 1)
+    b = a.copy()
+    b[2, 5] = b[5, 2] = np.nan
+    assert math.isnan(R.compute_rdm_correlation(torch.from_numpy(a), torch.from_numpy(b), correlation="Spearman"))
+    c = np.ones((10, 10), np.float32)
+    np.fill_diagonal(c, 0)
+    assert math.isnan(R.compute_rdm_correlation(torch.from_numpy(a), torch.from_numpy(c), correlation="Spearman"))
+    assert math.isnan(R.compute_rdm_correlation(torch.zeros(1, 1), torch.zeros(1, 1), correlation="Spearman"))
+    # n=2 -> one pair -> undefined
+    assert math.isnan(R.compute_rdm_correlation(torch.from_numpy(a[:2, :2]), torch.from_numpy(a[:2, :2]),
+                                                correlation="Spearman"))
+
+
+def test_spearman_negative_zero_ties(dev):
+    a = _tied_rdm(30, 4, levels=5) - 0.4  # negative values and exact zeros
+    a[np.abs(a) < 1e-7] = -0.0
+    b = _tied_rdm(30, 5, levels=5)
+    iu = np.triu_indices(30, 1)
+    got = R.compute_rdm_correlation(torch.from_numpy(a), torch.from_numpy(b), correlation="Spearman")
+    assert abs(got - O.midrank_spearman(a[iu], b[iu])) <= 1e-12
+
+
+@pytest.mark.parametrize("n", [3, 15, 200])
+def test_pearson_vs_scipy(dev, n):
+    a, b = _tied_rdm(n, 7), _tied_rdm(n, 8)
+    got = R.compute_rdm_correlation(torch.from_numpy(a), torch.from_numpy(b), correlation="Pearson")
+    ref = O.compute_rdm_correlation(a, b, "Pearson")
+    assert abs(got - ref) <= 1e-6
+
+
+def test_correlation_errors():
+    with pytest.raises(ValueError):
+        R.compute_rdm_correlation(torch.zeros(5, 5), torch.zeros(6, 6))
+    with pytest.raises(ValueError):
+        R.compute_rdm_correlation(torch.zeros(5, 5), torch.zeros(5, 5), correlation="cosine")
+
+
+# --------------------------------------------------------------------------- bootstrap
+@pytest.mark.parametrize("n,nb", [(10, 20), (64, 50), (130, 70), (256, 130)])
+def test_bootstrap_matches_oracle_same_rdms(dev, n, nb):
+    x = O.synthetic_features(n, [300, 200], seed=n)
+    m_rdm = O.compute_rdm(x[0])
+    n_rdm = O.compute_rdm(x[1])
+    point, scores, lo, hi = R.bootstrap_rsa(torch.from_numpy(m_rdm).to(dev),
+                                            torch.from_numpy(n_rdm).to(dev), n_bootstrap=nb, seed=42)
+    rp, rs, rlo, rhi = O.bootstrap_rsa(m_rdm, n_rdm, n_bootstrap=nb, seed=42)
+    assert abs(point - rp) <= 1e-12
+    assert np.max(np.abs(scores - rs)) <= 1e-12
+    assert abs(lo - rlo) <= 1e-12 and abs(hi - rhi) <= 1e-12
+
+
+def test_bootstrap_end_to_end_tolerance(dev):
+    # each side computes its own RDMs from the same features: |dSpearman| < 1e-5
+    n = 256
+    feats = O.synthetic_features(n, [43264, 2000], seed=11, relu=[True, False], noise=3.0)
+    gm = R.compute_rdm(torch.from_numpy(feats[0]).to(dev))
+    gn = R.compute_rdm(torch.from_numpy(feats[1]).to(dev))
+    point, scores, lo, hi = R.bootstrap_rsa(gm, gn, n_bootstrap=100, seed=42)
+    rp, rs, rlo, rhi = O.bootstrap_rsa(O.compute_rdm(feats[0]), O.compute_rdm(feats[1]),
+                                       n_bootstrap=100, seed=42)
+    assert abs(point - rp) < 1e-5
+    assert np.max(np.abs(scores - rs)) < 1e-5
+    assert abs(lo - rlo) < 1e-5 and abs(hi - rhi) < 1e-5
+
+
+def test_bootstrap_masks_large_n_global_path(dev):
+    # n > 20k stimuli -> inclusion masks read from global memory instead of LDS
+    n = 20500
+    rng = np.random.RandomState(0)
+    a = torch.rand(n, n, device=dev)
+    a = torch.triu(a, 1)
+    a = a + a.T
+    b = (a * 3).floor() / 3 + 0.01 * torch.rand(n, n, device=dev)
+    b = torch.triu(b, 1)
+    b = b + b.T
+    idx = np.stack([rng.choice(n, 50, replace=False) for _ in range(3)]).astype(np.int32)
+    pa, pb = R.RankPlan(a), R.RankPlan(b)
+    scores = R.bootstrap_spearman(pa, pb, idx).cpu().numpy()
+    an, bn = a.cpu().numpy(), b.cpu().numpy()
+    for i in range(3):
+        s = idx[i]
+        sa, sb = an[np.ix_(s, s)], bn[np.ix_(s, s)]
+        iu = np.triu_indices(len(s), 1)
+        assert abs(scores[i + 1] - O.midrank_spearman(sa[iu], sb[iu])) <= 1e-12
+
+
+# --------------------------------------------------------------------------- compute_rsa
+def test_compute_rsa_matches_oracle(dev):
+    from visreps_amd.analysis.alignment import AlignmentData
+
+    rng = np.random.RandomState(42)
+    n_train, n_test, v = 200, 50, 100
+    neural_train = rng.randn(n_train, v).astype(np.float32)
+    neural_test = rng.randn(n_test, v).astype(np.float32)
+    good_train = neural_train + 0.5 * rng.randn(n_train, v).astype(np.float32)
+    good_test = neural_test + 0.5 * rng.randn(n_test, v).astype(np.float32)
+    bad_train = rng.randn(n_train, v).astype(np.float32)
+    bad_test = rng.randn(n_test, v).astype(np.float32)
+    cfg = {"compare_method": "spearman"}
+    sel = AlignmentData({"good": torch.from_numpy(good_train), "bad": torch.from_numpy(bad_train)},
+                        torch.from_numpy(neural_train))
+    ev = AlignmentData({"good": torch.from_numpy(good_test), "bad": torch.from_numpy(bad_test)},
+                       torch.from_numpy(neural_test))
+    got = R.compute_rsa(cfg, sel, ev, n_select=100, bootstrap=True, n_bootstrap=60, seed=42)[0]
+    ref = O.compute_rsa(cfg, {"good": good_train, "bad": bad_train}, neural_train,
+                        {"good": good_test, "bad": bad_test}, neural_test,
+                        n_select=100, bootstrap=True, n_bootstrap=60, seed=42)[0]
+    assert got["layer"] == ref["layer"] == "good"
+    assert abs(got["score"] - ref["score"]) < 1e-5
+    assert np.max(np.abs(np.array(got["bootstrap_scores"]) - np.array(ref["bootstrap_scores"]))) < 1e-5
+    for g, r in zip(got["layer_selection_scores"], ref["layer_selection_scores"]):
+        assert g["layer"] == r["layer"] and abs(g["score"] - r["score"]) < 1e-5

@@ -1,0 +1,152 @@
+"""ctypes binding of libvisreps_hip.so (the C ABI declared in include/visreps_hip.h).
+
+torch is imported first on purpose: its bundled libamdhip64.so.7 is then the HIP runtime
+the library binds to (same SONAME), so device pointers and streams are shared with
+torch. There is no CPU fallback anywhere in the product path: if the library is missing
+the import of this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede loading the HIP library, see module doc)
+
+__all__ = [
+    "LIB_PATH",
+    "VisrepsHipError",
+    "lib",
+    "check",
+    "stream_of",
+    "workspace",
+    "EXPORTED_SYMBOLS",
+]
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvisreps_hip.so")
+
+
+class VisrepsHipError(RuntimeError):
+    """A libvisreps_hip call returned a non-zero status."""
+
+
+_c_i64 = ctypes.c_int64
+_c_sz = ctypes.c_size_t
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/visreps_hip.h
+_PROTOTYPES = {
+    "vr_version": (ctypes.c_int, []),
+    "vr_last_error": (ctypes.c_char_p, []),
+    "vr_rdm_pearson_workspace": (_c_sz, [_c_i64, _c_i64]),
+    "vr_rdm_pearson_f32": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _vp, _c_sz, _vp],
+    ),
+    "vr_row_stats_f32": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, ctypes.c_float, _vp],
+    ),
+    "vr_rank_plan_bytes": (_c_sz, [_c_i64]),
+    "vr_rank_plan_workspace": (_c_sz, [_c_i64]),
+    "vr_rank_plan_build_f32": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _vp, _c_sz, _vp, _c_sz, _vp],
+    ),
+    "vr_spearman_triu_workspace": (_c_sz, [_c_i64]),
+    "vr_spearman_triu_f32": (
+        ctypes.c_int,
+        [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp],
+    ),
+    "vr_pearson_triu_workspace": (_c_sz, [_c_i64]),
+    "vr_pearson_triu_f32": (
+        ctypes.c_int,
+        [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp],
+    ),
+    "vr_bootstrap_workspace": (_c_sz, [_c_i64]),
+    "vr_bootstrap_spearman_plans": (
+        ctypes.c_int,
+        [_vp, _vp, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _vp, _c_sz, _vp],
+    ),
+    "vr_bootstrap_spearman_workspace": (_c_sz, [_c_i64]),
+    "vr_bootstrap_spearman_f32": (
+        ctypes.c_int,
+        [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _vp, _c_sz, _vp],
+    ),
+    "vr_rng_state_bytes": (_c_sz, []),
+    "vr_rng_seed": (ctypes.c_int, [_vp, ctypes.c_uint32]),
+    "vr_rng_permutation": (ctypes.c_int, [_vp, _c_i64, _vp]),
+    "vr_rng_choice": (ctypes.c_int, [_vp, _c_i64, _c_i64, _vp]),
+    "vr_rng_random_u32": (ctypes.c_int, [_vp, _c_i64, _vp]),
+    "vr_legacy_choice": (ctypes.c_int, [ctypes.c_uint32, _c_i64, _c_i64, _c_i64, _vp]),
+    "vr_percentile_linear": (ctypes.c_double, [_vp, _c_i64, ctypes.c_double]),
+}
+
+EXPORTED_SYMBOLS = tuple(_PROTOTYPES)
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} not found: build the MI355X kernels first "
+                    "(python -c 'import __graft_entry__ as g; g.build()' or "
+                    "make -C visreps_amd/csrc). There is no CPU fallback."
+                )
+            handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            for name, (res, args) in _PROTOTYPES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+    return _lib
+
+
+def check(rc: int, fn: str) -> None:
+    if rc != 0:
+        msg = lib().vr_last_error().decode(errors="replace")
+        raise VisrepsHipError(f"{fn} failed (status {rc}): {msg}")
+
+
+def stream_of(device: torch.device) -> int:
+    """hipStream_t of torch's current stream on `device`, as an integer."""
+    return int(torch.cuda.current_stream(device).cuda_stream)
+
+
+class _WorkspacePool:
+    """Per-(device, tag) grow-only scratch buffers handed to the library.
+
+    The library never allocates; every call gets its scratch from here. Buffers are
+    reused across calls on the same stream (torch's caching allocator keeps stream
+    order), so a tag must not be shared by two calls that are live at once.
+    """
+
+    def __init__(self):
+        self._bufs: dict[tuple, torch.Tensor] = {}
+
+    def get(self, device: torch.device, nbytes: int, tag: str = "ws") -> torch.Tensor:
+        key = (str(device), tag)
+        buf = self._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            self._bufs.pop(key, None)
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            self._bufs[key] = buf
+        return buf
+
+    def release(self, tag: str | None = None) -> None:
+        if tag is None:
+            self._bufs.clear()
+        else:
+            for k in [k for k in self._bufs if k[1] == tag]:
+                del self._bufs[k]
+
+
+workspace = _WorkspacePool()

@@ -1,0 +1,434 @@
+"""MI355X implementation of visreps.analysis.rsa (reference: visreps/analysis/rsa.py).
+
+Same public names, argument meaning and error behaviour as the reference; the
+arithmetic runs in the HIP kernels of libvisreps_hip.so:
+
+  compute_rdm             rsa.py:59-93    fp32 MFMA Gram + fused 1-clamp(corr) epilogue
+  compute_rdm_correlation rsa.py:96-129   Spearman: sorted-triangle midrank engine
+                                          Pearson: fp64 two-pass triangle reduction
+  compute_rsa             rsa.py:132-281  layer selection + point + bootstrap on device
+  bootstrap_rsa           evals.py:355-373 the inline NSD/TVSD bootstrap, batched
+
+Tensors on a HIP device stay there; CPU tensors are copied to the current device and
+results come back on the CPU (the reference's own return device). There is no CPU
+fallback: without a HIP device these functions raise.
+"""
+from __future__ import annotations
+
+import logging
+import math
+from typing import TYPE_CHECKING, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .._lib import check, lib, stream_of, workspace
+from ..utils import rprint
+from ._random import LegacyRandomState, bootstrap_indices
+
+if TYPE_CHECKING:  # pragma: no cover
+    from .alignment import AlignmentData
+
+logger = logging.getLogger(__name__)
+
+__all__ = [
+    "compute_rdm",
+    "compute_rdm_correlation",
+    "compute_rsa",
+    "bootstrap_rsa",
+    "RankPlan",
+    "bootstrap_spearman",
+    "percentile",
+    "_rank",
+    "_concept_average_exact",
+]
+
+_VALID_RDM = {"pearson", "spearman"}
+_VALID_CMP = {"pearson", "spearman", "kendall"}
+
+
+# -----------------------------------------------------------------------------
+# device helpers
+# -----------------------------------------------------------------------------
+def _device_for(*tensors: torch.Tensor) -> torch.device:
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            return t.device
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            "visreps_amd needs a HIP (MI355X) device: the RSA kernels have no CPU path"
+        )
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _as_device_f32(x: torch.Tensor, dev: torch.device) -> torch.Tensor:
+    if not isinstance(x, torch.Tensor):
+        x = torch.as_tensor(np.asarray(x))
+    x = x.to(device=dev, dtype=torch.float32)
+    if x.ndim == 2 and x.stride(1) != 1:
+        x = x.contiguous()
+    if x.ndim == 2 and x.size(0) > 0 and x.stride(0) < max(x.size(1), 1):
+        x = x.contiguous()
+    return x
+
+
+def _ptr(t: torch.Tensor) -> int:
+    return int(t.data_ptr())
+
+
+def _rank(x: torch.Tensor) -> torch.Tensor:
+    """Row-wise ordinal rank via double argsort (rsa.py:50-52); ties are broken by
+    position (stable sort), as the reference's CPU argsort does for tie-free data."""
+    return torch.argsort(torch.argsort(x, dim=1, stable=True), dim=1, stable=True).float()
+
+
+# -----------------------------------------------------------------------------
+# RDM
+# -----------------------------------------------------------------------------
+def compute_rdm(
+    representations: torch.Tensor, *, correlation: str = "Pearson", correction: float = 1e-12
+) -> torch.Tensor:
+    """(n, n) float32 RDM = 1 - Pearson correlation of the rows (rsa.py:59-93).
+
+    Diagonal exactly 0; the matrix is exactly symmetric. correlation="Spearman" ranks
+    each row first (ordinal ranks, rsa.py:77-78)."""
+    corr = correlation.lower()
+    if corr not in _VALID_RDM:
+        raise ValueError("correlation must be 'Pearson' or 'Spearman'")
+    if not isinstance(representations, torch.Tensor):
+        representations = torch.as_tensor(np.asarray(representations))
+    if representations.ndim != 2:
+        raise ValueError("representations must be a 2-D (n_samples, n_features) tensor")
+    dev = _device_for(representations)
+    x = _as_device_f32(representations, dev)
+    if corr == "spearman":
+        x = _rank(x)
+    n, d = x.shape
+    out = torch.empty((n, n), dtype=torch.float32, device=dev)
+    if n > 0:
+        if d == 0:  # mean of nothing: NaN off the diagonal, as the reference's torch path
+            out.fill_(float("nan"))
+            out.fill_diagonal_(0.0)
+        else:
+            L = lib()
+            nbytes = L.vr_rdm_pearson_workspace(n, d)
+            ws = workspace.get(dev, nbytes, "rdm")
+            with torch.cuda.device(dev):
+                check(
+                    L.vr_rdm_pearson_f32(
+                        _ptr(x), n, d, x.stride(0), _ptr(out), n, float(correction),
+                        _ptr(ws), ws.numel(), stream_of(dev),
+                    ),
+                    "vr_rdm_pearson_f32",
+                )
+    return out if representations.is_cuda else out.cpu()
+
+
+# -----------------------------------------------------------------------------
+# Rank plans and the Spearman engine
+# -----------------------------------------------------------------------------
+class RankPlan:
+    """Device-resident sorted upper triangle of one RDM (values, tie groups, chunks).
+
+    Built once per RDM and reused by every Spearman against it: the model RDM of a
+    layer serves all ROIs, a neural RDM all layers."""
+
+    def __init__(self, rdm: torch.Tensor):
+        if rdm.ndim != 2 or rdm.size(0) != rdm.size(1):
+            raise ValueError("RankPlan needs a square 2-D RDM")
+        self.device = _device_for(rdm)
+        r = _as_device_f32(rdm, self.device)
+        self.n = int(r.size(0))
+        if self.n > 65535:
+            raise ValueError("rank plans support n <= 65535 stimuli")
+        L = lib()
+        self.buf = torch.empty(L.vr_rank_plan_bytes(self.n), dtype=torch.uint8, device=self.device)
+        ws = workspace.get(self.device, L.vr_rank_plan_workspace(self.n), "plan_build")
+        with torch.cuda.device(self.device):
+            check(
+                L.vr_rank_plan_build_f32(
+                    _ptr(r), self.n, r.stride(0), _ptr(self.buf), self.buf.numel(),
+                    _ptr(ws), ws.numel(), stream_of(self.device),
+                ),
+                "vr_rank_plan_build_f32",
+            )
+
+
+def bootstrap_spearman(
+    plan_a: RankPlan,
+    plan_b: RankPlan,
+    idx: Optional[np.ndarray | torch.Tensor],
+    *,
+    full_first: bool = True,
+) -> torch.Tensor:
+    """Spearman of triu(A[s][:, s]) vs triu(B[s][:, s]) for every subset s (row of idx),
+    preceded by the full set when full_first. Returns float64 scores on the device."""
+    if plan_a.n != plan_b.n or plan_a.device != plan_b.device:
+        raise ValueError("rank plans must describe RDMs of the same size and device")
+    dev, n = plan_a.device, plan_a.n
+    if idx is None:
+        idx_t = torch.empty((0, 0), dtype=torch.int32, device=dev)
+    else:
+        idx_t = torch.as_tensor(idx).to(device=dev, dtype=torch.int32).contiguous()
+        if idx_t.ndim != 2:
+            raise ValueError("idx must be (n_sets, k)")
+    n_sets, k = (int(idx_t.size(0)), int(idx_t.size(1))) if idx_t.numel() else (0, 0)
+    total = n_sets + (1 if full_first else 0)
+    scores = torch.empty(total, dtype=torch.float64, device=dev)
+    if total == 0:
+        return scores
+    L = lib()
+    ws = workspace.get(dev, L.vr_bootstrap_workspace(n), "engine")
+    with torch.cuda.device(dev):
+        check(
+            L.vr_bootstrap_spearman_plans(
+                _ptr(plan_a.buf), _ptr(plan_b.buf), n,
+                _ptr(idx_t) if idx_t.numel() else None, k, n_sets, int(full_first),
+                _ptr(scores), _ptr(ws), ws.numel(), stream_of(dev),
+            ),
+            "vr_bootstrap_spearman_plans",
+        )
+    return scores
+
+
+def percentile(scores: np.ndarray, q: float) -> float:
+    """numpy.percentile(scores, q), linear method (evals.py:371-372)."""
+    a = np.ascontiguousarray(scores, dtype=np.float64)
+    return float(lib().vr_percentile_linear(a.ctypes.data, a.size, float(q)))
+
+
+# -----------------------------------------------------------------------------
+# RDM comparison
+# -----------------------------------------------------------------------------
+def compute_rdm_correlation(
+    rdm1: torch.Tensor, rdm2: torch.Tensor, *, correlation: str = "Kendall"
+) -> float:
+    """Correlation of the strict upper triangles of two RDMs (rsa.py:96-129).
+
+    NaN when undefined (n <= 1, NaN input, constant triangle); ValueError on a shape
+    mismatch or an unknown method — checked in the reference's order."""
+    if not isinstance(rdm1, torch.Tensor):
+        rdm1 = torch.as_tensor(np.asarray(rdm1))
+    if not isinstance(rdm2, torch.Tensor):
+        rdm2 = torch.as_tensor(np.asarray(rdm2))
+    if rdm1.shape != rdm2.shape or rdm1.ndim != 2:
+        raise ValueError("RDMs must share the same 2-D shape")
+    n = rdm1.size(0)
+    if n <= 1:
+        logger.warning("RDM dimension <= 1; correlation undefined")
+        return float("nan")
+    if rdm1.size(1) < n:
+        raise ValueError("RDMs must be square")
+    corr = correlation.lower()
+    if corr not in _VALID_CMP:
+        raise ValueError("correlation must be 'Pearson', 'Spearman', or 'Kendall'")
+    if corr == "kendall":
+        raise NotImplementedError(
+            "Kendall tau-a RDM comparison is not on the MI355X path yet "
+            "(SURVEY.md §8(f) rank 1); use compare_method='spearman'"
+        )
+    dev = _device_for(rdm1, rdm2)
+    a = _as_device_f32(rdm1, dev)
+    b = _as_device_f32(rdm2, dev)
+    if a.stride(0) != b.stride(0):
+        a, b = a.contiguous(), b.contiguous()
+    out = torch.empty(1, dtype=torch.float64, device=dev)
+    L = lib()
+    with torch.cuda.device(dev):
+        if corr == "spearman":
+            ws = workspace.get(dev, L.vr_spearman_triu_workspace(n), "triu")
+            check(
+                L.vr_spearman_triu_f32(_ptr(a), _ptr(b), n, a.stride(0), _ptr(out),
+                                       _ptr(ws), ws.numel(), stream_of(dev)),
+                "vr_spearman_triu_f32",
+            )
+        else:
+            ws = workspace.get(dev, L.vr_pearson_triu_workspace(n), "pearson")
+            check(
+                L.vr_pearson_triu_f32(_ptr(a), _ptr(b), n, a.stride(0), _ptr(out),
+                                      _ptr(ws), ws.numel(), stream_of(dev)),
+                "vr_pearson_triu_f32",
+            )
+    val = float(out.item())
+    if math.isnan(val):
+        logger.warning("NaN returned for %s correlation", correlation)
+        return float("nan")
+    return val
+
+
+# -----------------------------------------------------------------------------
+# Bootstrap (evals.py:355-373) and train/test RSA (rsa.py:132-281)
+# -----------------------------------------------------------------------------
+def bootstrap_rsa(
+    model_rdm: torch.Tensor | RankPlan,
+    neural_rdm: torch.Tensor | RankPlan,
+    *,
+    n_bootstrap: int = 1000,
+    seed: int = 42,
+    idx: Optional[np.ndarray] = None,
+) -> Tuple[float, np.ndarray, float, float]:
+    """Point Spearman plus the reference's inline bootstrap: a fresh RandomState(seed),
+    n_bootstrap draws of choice(n, int(0.9 n), replace=False), Spearman of the two
+    sub-RDMs per draw, 2.5/97.5 linear percentiles. Returns
+    (point, scores[n_bootstrap], ci_low, ci_high)."""
+    pa = model_rdm if isinstance(model_rdm, RankPlan) else RankPlan(model_rdm)
+    pb = neural_rdm if isinstance(neural_rdm, RankPlan) else RankPlan(neural_rdm)
+    n = pa.n
+    if idx is None:
+        idx = bootstrap_indices(seed, n, int(n * 0.9), int(n_bootstrap)) if n_bootstrap else None
+    scores = bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    point, boot = float(scores[0]), scores[1:].copy()
+    if boot.size == 0:
+        return point, boot, float("nan"), float("nan")
+    return point, boot, percentile(boot, 2.5), percentile(boot, 97.5)
+
+
+def _flatten(a: torch.Tensor) -> torch.Tensor:
+    return a.flatten(start_dim=1) if a.ndim > 2 else a
+
+
+def _index_rows(a: torch.Tensor, idx: np.ndarray) -> torch.Tensor:
+    return a[torch.as_tensor(idx, dtype=torch.long, device=a.device)]
+
+
+def compute_rsa(
+    cfg: Dict,
+    selection: "AlignmentData",
+    evaluation: "AlignmentData",
+    n_select: int | None = None,
+    bootstrap: bool = True,
+    n_bootstrap: int = 1000,
+    seed: int = 42,
+    verbose: bool = False,
+    re_extract_fn=None,
+) -> List[Dict]:
+    """Train/test RSA (rsa.py:132-281): best layer on the selection split by Spearman
+    of Pearson RDMs (first strict maximum), point estimate on the evaluation split,
+    optional 90 % subsample bootstrap. One RandomState(seed) feeds the n_select draw and
+    then the bootstrap draws, as in the reference."""
+    method = cfg.get("compare_method", "spearman").lower()
+    rng = LegacyRandomState(seed)
+
+    n_train = selection.neural.size(0)
+    n_test = evaluation.neural.size(0)
+
+    if n_select is not None and n_select < n_train:
+        n_sel = n_select
+        sel_idx = rng.choice(n_train, size=n_sel, replace=False)
+        sel_label = f"subsampling {n_sel}"
+    else:
+        n_sel = n_train
+        sel_idx = np.arange(n_train)
+        sel_label = f"using all {n_sel}"
+
+    if verbose:
+        rprint(f"Train/test RSA: {n_train} train, {n_test} test, {sel_label} for layer selection",
+               style="info")
+        rprint(f"Building RDMs with Pearson, comparing with {method.capitalize()}", style="info")
+
+    neural_rdm_sel = compute_rdm(_index_rows(selection.neural, sel_idx))
+    sel_plan = RankPlan(neural_rdm_sel) if method == "spearman" and n_sel > 1 else None
+
+    selection_scores = []
+    best_layer, best_score = None, -float("inf")
+    for layer, acts in selection.activations.items():
+        flat = _flatten(_index_rows(acts, sel_idx))
+        layer_rdm = compute_rdm(flat)
+        if sel_plan is not None:
+            score = float(bootstrap_spearman(RankPlan(layer_rdm), sel_plan, None)[0].item())
+            if math.isnan(score):
+                logger.warning("NaN returned for %s correlation", method.capitalize())
+        else:
+            score = compute_rdm_correlation(layer_rdm, neural_rdm_sel,
+                                            correlation=method.capitalize())
+        selection_scores.append({"layer": layer, "score": score})
+        if verbose:
+            rprint(f"  [select] {layer:<15} RSA = {score:.4f}", style="info")
+        if score > best_score:
+            best_score = score
+            best_layer = layer
+
+    if verbose:
+        rprint(f"  Best layer: {best_layer} (score={best_score:.4f})", style="highlight")
+
+    if re_extract_fn is not None:
+        rprint(f"  Re-extracting {best_layer} without SRP for exact test RDMs...", style="info")
+        exact_acts, _ = re_extract_fn(best_layer, evaluation.stimulus_ids)
+        test_acts_flat = _flatten(exact_acts)
+    else:
+        test_acts_flat = _flatten(evaluation.activations[best_layer])
+
+    test_neural_rdm = compute_rdm(evaluation.neural)
+    test_model_rdm = compute_rdm(test_acts_flat)
+
+    ci_low, ci_high = None, None
+    bootstrap_scores_list = None
+    if method == "spearman" and n_test > 1:
+        plan_m, plan_n = RankPlan(test_model_rdm), RankPlan(test_neural_rdm)
+        boot_idx = None
+        if bootstrap and n_bootstrap > 0:
+            k = int(n_test * 0.9)
+            boot_idx = np.stack([rng.choice(n_test, size=k, replace=False)
+                                 for _ in range(n_bootstrap)]).astype(np.int32)
+        scores = bootstrap_spearman(plan_m, plan_n, boot_idx, full_first=True).cpu().numpy()
+        point_estimate = float(scores[0])
+        if math.isnan(point_estimate):
+            logger.warning("NaN returned for %s correlation", method.capitalize())
+        if bootstrap:
+            boot = scores[1:].astype(np.float64)
+            if boot.size:
+                ci_low, ci_high = percentile(boot, 2.5), percentile(boot, 97.5)
+            else:  # np.percentile of an empty array raises in the reference
+                raise IndexError("cannot compute percentiles of zero bootstrap scores")
+            bootstrap_scores_list = boot.tolist()
+    else:
+        point_estimate = compute_rdm_correlation(test_model_rdm, test_neural_rdm,
+                                                 correlation=method.capitalize())
+        if bootstrap:
+            k = int(n_test * 0.9)
+            boot = np.empty(n_bootstrap, dtype=np.float64)
+            for i in range(n_bootstrap):
+                bi = torch.as_tensor(rng.choice(n_test, size=k, replace=False),
+                                     device=test_model_rdm.device)
+                boot[i] = compute_rdm_correlation(test_model_rdm[bi][:, bi],
+                                                  test_neural_rdm[bi][:, bi],
+                                                  correlation=method.capitalize())
+            ci_low, ci_high = percentile(boot, 2.5), percentile(boot, 97.5)
+            bootstrap_scores_list = boot.tolist()
+
+    if verbose:
+        rprint(f"  Test RSA = {point_estimate:.4f}", style="highlight")
+    rprint("")
+    msg = f"  {method.capitalize():<10}| {best_layer} = {point_estimate:.4f}"
+    if bootstrap:
+        msg += f"  [95% CI: {ci_low:.4f}, {ci_high:.4f}]"
+    rprint(msg, style="highlight")
+
+    result = {
+        "layer": best_layer,
+        "compare_method": method,
+        "score": point_estimate,
+        "ci_low": ci_low,
+        "ci_high": ci_high,
+        "analysis": "rsa",
+        "layer_selection_scores": selection_scores,
+    }
+    if bootstrap_scores_list is not None:
+        result["bootstrap_scores"] = bootstrap_scores_list
+    return [result]
+
+
+def _concept_average_exact(raw_acts, raw_ids, data):
+    """Concept means of exact per-image activations in data.stimulus_ids order
+    (rsa.py:284-305); a concept with no images gets a zero row."""
+    id_to_idx = {str(k): i for i, k in enumerate(raw_ids)}
+    rows = []
+    for concept in data.stimulus_ids:
+        img_ids = data.concept_image_ids[concept]
+        indices = [id_to_idx[sid] for sid in img_ids if sid in id_to_idx]
+        if indices:
+            sel = raw_acts[torch.as_tensor(indices, dtype=torch.long, device=raw_acts.device)]
+            rows.append(sel.float().mean(0))
+        else:
+            rows.append(torch.zeros(raw_acts.size(1), device=raw_acts.device))
+    return torch.stack(rows).to(raw_acts.dtype)

@@ -1,0 +1,194 @@
+// Host-side pieces of libvisreps_hip.so:
+//  - error reporting and device queries,
+//  - the legacy numpy RandomState (MT19937) index stream, bit-exact, which draws the
+//    bootstrap / selection subsets (visreps/evals.py:260-261,356,362-364;
+//    visreps/analysis/rsa.py:169,176,248-250; evals.py:111-113),
+//  - numpy.percentile(.., method='linear') for the bootstrap CI (evals.py:371-372).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+namespace vr {
+
+static thread_local char g_err[1024] = {0};
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+void clear_error() { g_err[0] = 0; }
+
+int num_cus() {
+  static std::mutex mu;
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  std::lock_guard<std::mutex> lk(mu);
+  if (cache[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+            hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cache[dev] = cus;
+  }
+  return cache[dev];
+}
+
+// ---------------------------------------------------------------------------------
+// MT19937 as numpy's legacy RandomState uses it: integer seeds go through
+// init_genrand (mt19937_seed), 32-bit draws are the standard tempered outputs, and
+// bounded integers use masked rejection (legacy random_interval). permutation(n)
+// shuffles arange(n) with i running n-1 .. 1, j = interval(i), swap(x[i], x[j]);
+// choice(n, k, replace=False) is permutation(n)[:k].
+// ---------------------------------------------------------------------------------
+struct MTState {
+  uint32_t mt[624];
+  int pos;
+};
+
+static void mt_seed(MTState* s, uint32_t seed) {
+  s->mt[0] = seed;
+  for (int i = 1; i < 624; ++i)
+    s->mt[i] = 1812433253u * (s->mt[i - 1] ^ (s->mt[i - 1] >> 30)) + (uint32_t)i;
+  s->pos = 624;
+}
+
+static void mt_regen(MTState* s) {
+  uint32_t* mt = s->mt;
+  for (int i = 0; i < 624; ++i) {
+    uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
+    mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  }
+  s->pos = 0;
+}
+
+static inline uint32_t mt_next(MTState* s) {
+  if (s->pos >= 624) mt_regen(s);
+  uint32_t y = s->mt[s->pos++];
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+// Bounded draw in [0, mx] for mx < 2^32 (every caller here bounds n by INT32_MAX).
+static inline uint32_t mt_interval(MTState* s, uint32_t mx) {
+  if (mx == 0) return 0;
+  uint32_t mask = mx;
+  mask |= mask >> 1;
+  mask |= mask >> 2;
+  mask |= mask >> 4;
+  mask |= mask >> 8;
+  mask |= mask >> 16;
+  uint32_t v;
+  while ((v = (mt_next(s) & mask)) > mx) {
+  }
+  return v;
+}
+
+static void mt_permutation(MTState* s, int64_t n, int32_t* out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = (int32_t)i;
+  for (int64_t i = n - 1; i >= 1; --i) {
+    int64_t j = (int64_t)mt_interval(s, (uint32_t)i);
+    std::swap(out[i], out[j]);
+  }
+}
+
+}  // namespace vr
+
+using namespace vr;
+
+extern "C" {
+
+int vr_version(void) { return 100; }
+
+const char* vr_last_error(void) { return g_err; }
+
+size_t vr_rng_state_bytes(void) { return sizeof(MTState); }
+
+int vr_rng_seed(void* state, uint32_t seed) {
+  VR_REQUIRE(state != nullptr, "vr_rng_seed: null state");
+  mt_seed(static_cast<MTState*>(state), seed);
+  return VR_OK;
+}
+
+int vr_rng_permutation(void* state, int64_t n, int32_t* out) {
+  VR_REQUIRE(state != nullptr && (out != nullptr || n == 0), "vr_rng_permutation: null pointer");
+  VR_REQUIRE(n >= 0 && n <= INT32_MAX, "vr_rng_permutation: n=%lld out of range", (long long)n);
+  mt_permutation(static_cast<MTState*>(state), n, out);
+  return VR_OK;
+}
+
+int vr_rng_choice(void* state, int64_t n, int64_t k, int32_t* out) {
+  VR_REQUIRE(state != nullptr, "vr_rng_choice: null state");
+  VR_REQUIRE(n >= 0 && n <= INT32_MAX, "vr_rng_choice: n=%lld out of range", (long long)n);
+  // numpy: "Cannot take a larger sample than population when 'replace=False'"
+  VR_REQUIRE(k >= 0 && k <= n, "vr_rng_choice: sample size %lld > population %lld",
+             (long long)k, (long long)n);
+  std::vector<int32_t> perm((size_t)n);
+  mt_permutation(static_cast<MTState*>(state), n, perm.data());
+  if (k > 0) std::memcpy(out, perm.data(), (size_t)k * sizeof(int32_t));
+  return VR_OK;
+}
+
+int vr_rng_random_u32(void* state, int64_t count, uint32_t* out) {
+  VR_REQUIRE(state != nullptr && (out != nullptr || count == 0), "vr_rng_random_u32: null pointer");
+  MTState* s = static_cast<MTState*>(state);
+  for (int64_t i = 0; i < count; ++i) out[i] = mt_next(s);
+  return VR_OK;
+}
+
+int vr_legacy_choice(uint32_t seed, int64_t n, int64_t k, int64_t n_draws, int32_t* out) {
+  VR_REQUIRE(n >= 0 && n <= INT32_MAX && k >= 0 && k <= n && n_draws >= 0,
+             "vr_legacy_choice: bad sizes n=%lld k=%lld draws=%lld", (long long)n,
+             (long long)k, (long long)n_draws);
+  VR_REQUIRE(out != nullptr || n_draws == 0 || k == 0, "vr_legacy_choice: null out");
+  MTState s;
+  mt_seed(&s, seed);
+  std::vector<int32_t> perm((size_t)n);
+  for (int64_t d = 0; d < n_draws; ++d) {
+    mt_permutation(&s, n, perm.data());
+    if (k > 0) std::memcpy(out + d * k, perm.data(), (size_t)k * sizeof(int32_t));
+  }
+  return VR_OK;
+}
+
+// numpy.percentile(x, q), method='linear' (numpy/lib/_function_base_impl.py: q/100,
+// virtual index (n-1)*q, neighbours floor/floor+1 clipped, gamma = frac, _lerp with
+// the b - diff*(1-gamma) branch for gamma >= 0.5). NaN anywhere -> NaN.
+double vr_percentile_linear(const double* x, int64_t n, double q) {
+  if (n <= 0 || x == nullptr) return std::nan("");
+  std::vector<double> v(x, x + n);
+  for (double e : v)
+    if (std::isnan(e)) return std::nan("");
+  std::sort(v.begin(), v.end());
+  const double qq = q / 100.0;
+  const double vi = (double)(n - 1) * qq;
+  int64_t prev, next;
+  if (vi >= (double)(n - 1)) {
+    prev = next = n - 1;
+  } else if (vi < 0) {
+    prev = next = 0;
+  } else {
+    prev = (int64_t)std::floor(vi);
+    next = prev + 1;
+  }
+  const double gamma = vi - std::floor(vi);
+  const double a = v[(size_t)prev], b = v[(size_t)next];
+  const double diff = b - a;
+  if (gamma >= 0.5) return b - diff * (1.0 - gamma);
+  return a + diff * gamma;
+}
+
+}  // extern "C"

@@ -1,0 +1,69 @@
+// Internal (non-ABI) declarations shared between the .hip translation units.
+#pragma once
+
+#include "common.h"
+
+namespace vr {
+
+// ---- device-wide exclusive scan of uint32 (scan.hip) -------------------------------
+constexpr int SCAN_BS = 256;
+constexpr int SCAN_IPT = 16;
+constexpr int SCAN_TILE = SCAN_BS * SCAN_IPT;
+size_t scan_ws_elems(int64_t n);  // uint32 elements of scratch
+// out[i] = sum(in[0:i]); *total_dev (if non-null) = sum(in). in may alias out.
+int scan_exclusive_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* total_dev,
+                       uint32_t* ws, hipStream_t st);
+
+// ---- LSD radix sort of (uint32 key, uint32 value) pairs (sort.hip) -----------------
+constexpr int RS_BS = 256;
+constexpr int RS_IPT = 16;
+constexpr int RS_TILE = RS_BS * RS_IPT;
+size_t radix_ws_elems(int64_t n);  // uint32 elements of scratch (histograms + scan)
+// Sorts ascending by key, stable. keys/vals hold the result; *_alt are ping-pong
+// buffers of the same length.
+int radix_sort_kv(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                  int64_t n, uint32_t* ws, hipStream_t st);
+
+// ---- block-level helpers -----------------------------------------------------------
+// Exclusive scan across a block of BS threads (BS multiple of 64, <= 1024).
+// lds must hold BS/64 + 1 uint32. Returns this thread's exclusive prefix; total = sum.
+template <int BS>
+__device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint32_t& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int w = 0; w < BS / 64; ++w) {
+      uint32_t t = lds[w];
+      lds[w] = s;
+      s += t;
+    }
+    lds[BS / 64] = s;
+  }
+  __syncthreads();
+  uint32_t r = x - v + lds[wid];
+  total = lds[BS / 64];
+  __syncthreads();
+  return r;
+}
+
+// Padded LDS index for tiles read both striped (lane-contiguous) and blocked (16
+// consecutive per thread): one pad dword per 32 keeps both patterns conflict-free.
+__device__ inline int lds_pad(int p) { return p + (p >> 5); }
+
+// Sortable transform of an fp32 value: ascending uint32 order == ascending float order,
+// -0.0 canonicalised to +0.0 so the two tie (scipy.stats.rankdata semantics).
+__device__ inline uint32_t f32_sort_key(float f) {
+  uint32_t u = __float_as_uint(f);
+  if (u == 0x80000000u) u = 0u;
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+}  // namespace vr

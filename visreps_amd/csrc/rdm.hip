@@ -1,0 +1,435 @@
+// RDM = 1 - Pearson correlation of the rows of X (n x d), the MI355X replacement of
+// compute_rdm(.., correlation="Pearson") in visreps/analysis/rsa.py:59-93:
+//   x = X.float(); x -= x.mean(1); std = sqrt(mean(x^2, 1) + c); std[std < 10c] = 1
+//   cov = x @ x.T / D; corr = cov / (std_i std_j + c); clamp(-1, 1); diag = 1; 1 - corr
+//
+// Kernels
+//  k_row_stats   one block per row, two passes (mean, then centred sum of squares),
+//                fp64 accumulation of fp32 terms -> fp32 mean / std.     [HBM-bound]
+//  k_gram        symmetric Gram of the centred rows on the fp32 matrix cores
+//                (v_mfma_f32_32x32x2_f32, exact fp32 fma chains). Only tiles with
+//                bi <= bj are computed; centring is fused into the register staging
+//                of each 128x32 panel; the epilogue writes the tile and its mirror.
+//                Split-K over d when the tile count cannot fill 256 CUs, with fp32
+//                partial tiles reduced in fixed order by k_gram_reduce.  [MFMA-bound]
+#include "internal.h"
+
+namespace vr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------------------------
+// Row statistics
+// ------------------------------------------------------------------------------------
+constexpr int RSTAT_BS = 256;
+
+__device__ inline double block_sum_f64(double v, double* lds) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  double s = 0;
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < RSTAT_BS / 64; ++w) s += lds[w];
+    lds[RSTAT_BS / 64] = s;
+  }
+  __syncthreads();
+  s = lds[RSTAT_BS / 64];
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(RSTAT_BS) void k_row_stats(const float* __restrict__ X, int64_t d,
+                                                        int64_t ldx, float* __restrict__ mean,
+                                                        float* __restrict__ stdv,
+                                                        float correction, int vec) {
+  __shared__ double lds[RSTAT_BS / 64 + 1];
+  const float* row = X + (int64_t)blockIdx.x * ldx;
+  double s = 0;
+  if (vec) {
+    const f32x4* r4 = reinterpret_cast<const f32x4*>(row);
+    const int64_t d4 = d / 4;
+    for (int64_t i = threadIdx.x; i < d4; i += RSTAT_BS) {
+      f32x4 v = r4[i];
+      s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+    }
+    for (int64_t i = d4 * 4 + threadIdx.x; i < d; i += RSTAT_BS) s += (double)row[i];
+  } else {
+    for (int64_t i = threadIdx.x; i < d; i += RSTAT_BS) s += (double)row[i];
+  }
+  s = block_sum_f64(s, lds);
+  const float m = (float)(s / (double)d);
+  double q = 0;
+  if (vec) {
+    const f32x4* r4 = reinterpret_cast<const f32x4*>(row);
+    const int64_t d4 = d / 4;
+    for (int64_t i = threadIdx.x; i < d4; i += RSTAT_BS) {
+      f32x4 v = r4[i];
+      float a = v.x - m, b = v.y - m, c = v.z - m, e = v.w - m;
+      q += (double)(a * a) + (double)(b * b) + (double)(c * c) + (double)(e * e);
+    }
+    for (int64_t i = d4 * 4 + threadIdx.x; i < d; i += RSTAT_BS) {
+      float a = row[i] - m;
+      q += (double)(a * a);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < d; i += RSTAT_BS) {
+      float a = row[i] - m;
+      q += (double)(a * a);
+    }
+  }
+  q = block_sum_f64(q, lds);
+  if (threadIdx.x == 0) {
+    float var = (float)(q / (double)d);
+    float sd = sqrtf(var + correction);
+    if (sd < correction * 10.0f) sd = 1.0f;  // rsa.py:84-87 zero-variance guard
+    mean[blockIdx.x] = m;
+    stdv[blockIdx.x] = sd;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Symmetric Gram on fp32 MFMA
+// ------------------------------------------------------------------------------------
+constexpr int GT = 128;            // tile edge (rows of the i and j panels)
+constexpr int GK = 32;             // k per LDS stage
+constexpr int GLD = GK + 4;        // padded LDS row: conflict-free ds_read_b128
+constexpr int G_THREADS = 256;     // 4 waves as 2x2, each wave 64x64 = 2x2 MFMA tiles
+constexpr int G_STAGE = GT * GLD;  // floats per panel per stage
+
+struct GramParams {
+  const float* X;
+  const float* mean;
+  const float* stdv;
+  float* rdm;
+  float* partial;   // split-K fp32 partial tiles (null when splits == 1)
+  int64_t n, d, ldx, ldr;
+  int64_t kslice;   // k extent of one split (multiple of GK)
+  int T;            // tiles per dimension
+  int ntiles;       // T*(T+1)/2
+  int splits;
+  float correction;
+  int vec;          // 16-B aligned rows: float4 staging
+};
+
+__device__ inline void tile_coords(int p, int T, int& bi, int& bj) {
+  // row-major enumeration of the upper triangle: row bi holds T - bi tiles
+  float tf = (float)T;
+  int r = (int)((2.f * tf + 1.f - sqrtf((2.f * tf + 1.f) * (2.f * tf + 1.f) - 8.f * (float)p)) * 0.5f);
+  if (r < 0) r = 0;
+  if (r > T - 1) r = T - 1;
+  auto off = [&](int b) { return b * T - b * (b - 1) / 2; };
+  while (r > 0 && off(r) > p) --r;
+  while (r + 1 < T && off(r + 1) <= p) ++r;
+  bi = r;
+  bj = r + (p - off(r));
+}
+
+// Loads this thread's 4 float4 of a 128 x 32 panel (rows row0.., k in [k, k+32)) and
+// centres them. Elements outside [0,n) x [k0,k1) are 0 after centring.
+__device__ inline void load_panel(const GramParams& P, int64_t row0, int64_t k, int64_t k1,
+                                  const float mrow[4], f32x4 out[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int f = threadIdx.x + G_THREADS * s;
+    const int r = f >> 3, c4 = f & 7;
+    const int64_t row = row0 + r;
+    const int64_t kk = k + c4 * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < P.n) {
+      const float* src = P.X + row * P.ldx + kk;
+      if (P.vec && kk + 3 < k1) {
+        v = *reinterpret_cast<const f32x4*>(src);
+        v.x -= mrow[s];
+        v.y -= mrow[s];
+        v.z -= mrow[s];
+        v.w -= mrow[s];
+      } else {
+        if (kk + 0 < k1) v.x = src[0] - mrow[s];
+        if (kk + 1 < k1) v.y = src[1] - mrow[s];
+        if (kk + 2 < k1) v.z = src[2] - mrow[s];
+        if (kk + 3 < k1) v.w = src[3] - mrow[s];
+      }
+    }
+    out[s] = v;
+  }
+}
+
+__device__ inline void store_panel(float* lds, const f32x4 v[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int f = threadIdx.x + G_THREADS * s;
+    const int r = f >> 3, c4 = f & 7;
+    *reinterpret_cast<f32x4*>(lds + r * GLD + c4 * 4) = v[s];
+  }
+}
+
+// Epilogue for one element: rdm = 1 - clamp(G/d / (s_i s_j + c)), exactly the
+// reference's fp32 operation order; NaN propagates like torch.clamp.
+__device__ inline float rdm_value(float g, float inv_unused, int64_t i, int64_t j,
+                                  const GramParams& P, float si, float sj) {
+  (void)inv_unused;
+  float cov = g / (float)P.d;
+  float c = cov / (si * sj + P.correction);
+  c = (c < -1.f) ? -1.f : ((c > 1.f) ? 1.f : c);
+  if (i == j) c = 1.f;
+  return 1.f - c;
+}
+
+__global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * 2 * G_STAGE];  // [buf][A/B]
+  const int nwg = gridDim.x;
+  const int id = (int)xcd_remap(blockIdx.x, (uint32_t)nwg);
+  const int tile = id / P.splits, split = id % P.splits;
+  int bi, bj;
+  tile_coords(tile, P.T, bi, bj);
+  const bool diag = (bi == bj);
+  const int64_t row0 = (int64_t)bi * GT, col0 = (int64_t)bj * GT;
+  const int64_t k0 = (int64_t)split * P.kslice;
+  const int64_t k1 = min(P.d, k0 + P.kslice);
+  const int nk = (int)((k1 - k0 + GK - 1) / GK);
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+
+  float mA[4], mB[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int r = (threadIdx.x + G_THREADS * s) >> 3;
+    mA[s] = (row0 + r < P.n) ? P.mean[row0 + r] : 0.f;
+    mB[s] = (col0 + r < P.n) ? P.mean[col0 + r] : 0.f;
+  }
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  f32x4 ga[4], gb[4];
+  if (nk > 0) {
+    load_panel(P, row0, k0, k1, mA, ga);
+    if (!diag) load_panel(P, col0, k0, k1, mB, gb);
+    store_panel(lds, ga);
+    if (!diag) store_panel(lds + G_STAGE, gb);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const float* As = lds + cur * 2 * G_STAGE;
+    const float* Bs = diag ? As : As + G_STAGE;
+    const bool more = kt + 1 < nk;
+    if (more) {  // issue next panel loads early; they land under the MFMAs below
+      const int64_t kn = k0 + (int64_t)(kt + 1) * GK;
+      load_panel(P, row0, kn, k1, mA, ga);
+      if (!diag) load_panel(P, col0, kn, k1, mB, gb);
+    }
+    // lane half h owns k in [16h, 16h+16) of this stage (a consistent k permutation of
+    // the MFMA's 2-deep k; the Gram sums over k so any fixed permutation is exact)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 av[2], bv[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int ar = wr * 64 + m * 32 + l32;
+        av[m] = *reinterpret_cast<const f32x4*>(As + ar * GLD + h * 16 + q * 4);
+        const int br = wc * 64 + m * 32 + l32;
+        bv[m] = *reinterpret_cast<const f32x4*>(Bs + br * GLD + h * 16 + q * 4);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int nn = 0; nn < 2; ++nn)
+            acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bv[nn][e], acc[m][nn], 0, 0, 0);
+    }
+    if (more) {
+      float* nxt = lds + (cur ^ 1) * 2 * G_STAGE;
+      store_panel(nxt, ga);
+      if (!diag) store_panel(nxt + G_STAGE, gb);
+    }
+    __syncthreads();
+  }
+
+  // C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  if (P.splits == 1) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        const int64_t j = col0 + wc * 64 + nn * 32 + l32;
+        const float sj = (j < P.n) ? P.stdv[j] : 1.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int64_t ib = row0 + wr * 64 + m * 32 + 8 * g + 4 * h;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t i = ib + e;
+            const float si = (i < P.n) ? P.stdv[i] : 1.f;
+            v[e] = rdm_value(acc[m][nn][4 * g + e], 0.f, i, j, P, si, sj);
+            if (i < P.n && j < P.n) P.rdm[i * P.ldr + j] = v[e];
+          }
+          if (!diag && j < P.n) {  // mirror: rows ib..ib+3 are 4 consecutive columns of row j
+            float* dst = P.rdm + j * P.ldr + ib;
+            if (P.vec && ib + 3 < P.n && ((P.ldr & 3) == 0)) {
+              f32x4 w = {v[0], v[1], v[2], v[3]};
+              *reinterpret_cast<f32x4*>(dst) = w;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (ib + e < P.n) dst[e] = v[e];
+            }
+          }
+        }
+      }
+  } else {
+    float* out = P.partial + ((int64_t)split * P.ntiles + tile) * (GT * GT);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        const int lj = wc * 64 + nn * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int li = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          out[li * GT + lj] = acc[m][nn][r];
+        }
+      }
+  }
+}
+
+// Sums the split partials of one tile in split order and applies the epilogue; the
+// mirror half goes through an LDS transpose so both writes are row-coalesced.
+__global__ __launch_bounds__(256) void k_gram_reduce(GramParams P) {
+  __shared__ float tr[32][33];
+  const int tile = blockIdx.x;
+  int bi, bj;
+  tile_coords(tile, P.T, bi, bj);
+  const bool diag = (bi == bj);
+  const int64_t row0 = (int64_t)bi * GT, col0 = (int64_t)bj * GT;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int sb = 0; sb < (GT / 32) * (GT / 32); ++sb) {
+    const int si0 = (sb / (GT / 32)) * 32, sj0 = (sb % (GT / 32)) * 32;
+    for (int yy = ty; yy < 32; yy += 8) {
+      const int li = si0 + yy, lj = sj0 + tx;
+      float g = 0.f;
+      for (int s = 0; s < P.splits; ++s)
+        g += P.partial[((int64_t)s * P.ntiles + tile) * (GT * GT) + li * GT + lj];
+      const int64_t i = row0 + li, j = col0 + lj;
+      const float sI = (i < P.n) ? P.stdv[i] : 1.f, sJ = (j < P.n) ? P.stdv[j] : 1.f;
+      const float v = rdm_value(g, 0.f, i, j, P, sI, sJ);
+      if (i < P.n && j < P.n) P.rdm[i * P.ldr + j] = v;
+      tr[yy][tx] = v;
+    }
+    __syncthreads();
+    if (!diag) {
+      for (int yy = ty; yy < 32; yy += 8) {
+        // mirror row j = col0 + sj0 + yy, columns i = row0 + si0 + tx
+        const int64_t j = col0 + sj0 + yy, i = row0 + si0 + tx;
+        if (i < P.n && j < P.n) P.rdm[j * P.ldr + i] = tr[tx][yy];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+static void gram_geometry(int64_t n, int64_t d, int& T, int& ntiles, int& splits,
+                          int64_t& kslice) {
+  T = (int)((n + GT - 1) / GT);
+  ntiles = T * (T + 1) / 2;
+  const int64_t kt = (d + GK - 1) / GK;  // k stages
+  const int target = 2 * num_cus();     // two resident blocks per CU
+  int s = 1;
+  if (ntiles < target) {
+    s = (target + ntiles - 1) / ntiles;
+    const int64_t maxs = std::max<int64_t>(1, kt / 4);  // >= 4 stages per split
+    if (s > maxs) s = (int)maxs;
+  }
+  const int64_t per = (kt + s - 1) / s;
+  kslice = per * GK;
+  splits = (int)((d + kslice - 1) / kslice);
+  if (splits < 1) splits = 1;
+}
+
+}  // namespace vr
+
+using namespace vr;
+
+extern "C" {
+
+size_t vr_rdm_pearson_workspace(int64_t n, int64_t d) {
+  if (n <= 0 || d <= 0) return 256;
+  int T, ntiles, splits;
+  int64_t kslice;
+  gram_geometry(n, d, T, ntiles, splits, kslice);
+  Carver c(nullptr);
+  c.take<float>((size_t)n);
+  c.take<float>((size_t)n);
+  if (splits > 1) c.take<float>((size_t)splits * ntiles * GT * GT);
+  return c.bytes();
+}
+
+int vr_row_stats_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* mean,
+                     float* stdv, float correction, void* stream) {
+  VR_REQUIRE(n >= 0 && d > 0 && ldx >= d, "vr_row_stats_f32: bad shape n=%lld d=%lld ldx=%lld",
+             (long long)n, (long long)d, (long long)ldx);
+  if (n == 0) return VR_OK;
+  VR_REQUIRE(X && mean && stdv, "vr_row_stats_f32: null pointer");
+  VR_REQUIRE(n <= INT32_MAX, "vr_row_stats_f32: n too large");
+  const int vec = ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && ((ldx & 3) == 0);
+  k_row_stats<<<(unsigned)n, RSTAT_BS, 0, as_stream(stream)>>>(X, d, ldx, mean, stdv,
+                                                                correction, vec);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
+                       int64_t ldr, float correction, void* ws, size_t ws_bytes,
+                       void* stream) {
+  VR_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldr >= n,
+             "vr_rdm_pearson_f32: bad shape n=%lld d=%lld ldx=%lld ldr=%lld", (long long)n,
+             (long long)d, (long long)ldx, (long long)ldr);
+  if (n == 0) return VR_OK;
+  VR_REQUIRE(X && rdm, "vr_rdm_pearson_f32: null pointer");
+  VR_REQUIRE(n <= (1 << 24), "vr_rdm_pearson_f32: n=%lld too large", (long long)n);
+  const size_t need = vr_rdm_pearson_workspace(n, d);
+  if (ws_bytes < need || ws == nullptr) {
+    set_error("vr_rdm_pearson_f32: workspace %zu < %zu", ws_bytes, need);
+    return VR_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  GramParams P{};
+  gram_geometry(n, d, P.T, P.ntiles, P.splits, P.kslice);
+  Carver c(ws);
+  float* mean = c.take<float>((size_t)n);
+  float* stdv = c.take<float>((size_t)n);
+  P.partial = (P.splits > 1) ? c.take<float>((size_t)P.splits * P.ntiles * GT * GT) : nullptr;
+  VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
+  P.X = X;
+  P.mean = mean;
+  P.stdv = stdv;
+  P.rdm = rdm;
+  P.n = n;
+  P.d = d;
+  P.ldx = ldx;
+  P.ldr = ldr;
+  P.correction = correction;
+  P.vec = ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && ((ldx & 3) == 0) &&
+          ((reinterpret_cast<uintptr_t>(rdm) & 15) == 0);
+  const unsigned nblk = (unsigned)P.ntiles * (unsigned)P.splits;
+  k_gram<<<nblk, G_THREADS, 0, st>>>(P);
+  VR_CHECK_LAUNCH();
+  if (P.splits > 1) {
+    k_gram_reduce<<<(unsigned)P.ntiles, 256, 0, st>>>(P);
+    VR_CHECK_LAUNCH();
+  }
+  return VR_OK;
+}
+
+}  // extern "C"
