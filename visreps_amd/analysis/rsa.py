@@ -169,6 +169,8 @@ def bootstrap_spearman(
     if idx is None:
         idx_t = torch.empty((0, 0), dtype=torch.int32, device=dev)
     else:
+        if isinstance(idx, np.ndarray) and not idx.flags.writeable:
+            idx = idx.copy()
         idx_t = torch.as_tensor(idx).to(device=dev, dtype=torch.int32).contiguous()
         if idx_t.ndim != 2:
             raise ValueError("idx must be (n_sets, k)")
