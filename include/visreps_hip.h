@@ -55,6 +55,19 @@ int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float*
                        int64_t ldr, float correction, void* ws, size_t ws_bytes,
                        void* stream);
 
+/* Block-distributed form (multi-GPU): the upper-triangle tiles of 128x128 are numbered
+ * row-major (tile (bi,bj), bi <= bj); this computes tiles [tile_begin, tile_end) only and
+ * writes each tile and its mirror into rdm. Entries of other tiles are not touched, so
+ * ranks that each own a tile range and start from a zeroed rdm can combine with a sum
+ * all-reduce. vr_rdm_tile_count(n) = number of tiles, vr_rdm_tile_cost(n, t) = distinct
+ * (i <= j) entries of tile t, for balancing ranges. */
+int64_t vr_rdm_tile_count(int64_t n);
+int64_t vr_rdm_tile_cost(int64_t n, int64_t tile);
+size_t vr_rdm_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end);
+int vr_rdm_pearson_tiles_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
+                             int64_t ldr, float correction, int64_t tile_begin,
+                             int64_t tile_end, void* ws, size_t ws_bytes, void* stream);
+
 /* Row statistics of the same RDM (rsa.py:80-87): mean[i] (fp32) and
  * std[i] = sqrt(mean((x-mean)^2) + correction) with std < 10*correction -> 1.
  * Exposed so extraction can emit them alongside the feature rows. */

@@ -43,6 +43,13 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _vp, _c_sz, _vp],
     ),
+    "vr_rdm_tile_count": (_c_i64, [_c_i64]),
+    "vr_rdm_tile_cost": (_c_i64, [_c_i64, _c_i64]),
+    "vr_rdm_tiles_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64]),
+    "vr_rdm_pearson_tiles_f32": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _c_i64, _c_i64, _vp, _c_sz, _vp],
+    ),
     "vr_row_stats_f32": (
         ctypes.c_int,
         [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, ctypes.c_float, _vp],

@@ -109,6 +109,8 @@ struct GramParams {
   int T;            // tiles per dimension
   int ntiles;       // T*(T+1)/2
   int splits;
+  int tile0;        // first upper-triangle tile of this launch (block-distributed Gram)
+  int tile_count;   // tiles in this launch
   float correction;
   int vec;          // 16-B aligned rows: float4 staging
 };
@@ -167,9 +169,8 @@ __device__ inline void store_panel(float* lds, const f32x4 v[4]) {
 
 // Epilogue for one element: rdm = 1 - clamp(G/d / (s_i s_j + c)), exactly the
 // reference's fp32 operation order; NaN propagates like torch.clamp.
-__device__ inline float rdm_value(float g, float inv_unused, int64_t i, int64_t j,
-                                  const GramParams& P, float si, float sj) {
-  (void)inv_unused;
+__device__ inline float rdm_value(float g, int64_t i, int64_t j, const GramParams& P,
+                                  float si, float sj) {
   float cov = g / (float)P.d;
   float c = cov / (si * sj + P.correction);
   c = (c < -1.f) ? -1.f : ((c > 1.f) ? 1.f : c);
@@ -181,7 +182,8 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
   __shared__ __attribute__((aligned(16))) float lds[2 * 2 * G_STAGE];  // [buf][A/B]
   const int nwg = gridDim.x;
   const int id = (int)xcd_remap(blockIdx.x, (uint32_t)nwg);
-  const int tile = id / P.splits, split = id % P.splits;
+  const int ltile = id / P.splits, split = id % P.splits;
+  const int tile = P.tile0 + ltile;
   int bi, bj;
   tile_coords(tile, P.T, bi, bj);
   const bool diag = (bi == bj);
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
           for (int e = 0; e < 4; ++e) {
             const int64_t i = ib + e;
             const float si = (i < P.n) ? P.stdv[i] : 1.f;
-            v[e] = rdm_value(acc[m][nn][4 * g + e], 0.f, i, j, P, si, sj);
+            v[e] = rdm_value(acc[m][nn][4 * g + e], i, j, P, si, sj);
             if (i < P.n && j < P.n) P.rdm[i * P.ldr + j] = v[e];
           }
           if (!diag && j < P.n) {  // mirror: rows ib..ib+3 are 4 consecutive columns of row j
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
         }
       }
   } else {
-    float* out = P.partial + ((int64_t)split * P.ntiles + tile) * (GT * GT);
+    float* out = P.partial + ((int64_t)split * P.tile_count + ltile) * (GT * GT);
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -308,7 +310,8 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
 // mirror half goes through an LDS transpose so both writes are row-coalesced.
 __global__ __launch_bounds__(256) void k_gram_reduce(GramParams P) {
   __shared__ float tr[32][33];
-  const int tile = blockIdx.x;
+  const int ltile = blockIdx.x;
+  const int tile = P.tile0 + ltile;
   int bi, bj;
   tile_coords(tile, P.T, bi, bj);
   const bool diag = (bi == bj);
@@ -320,10 +323,10 @@ __global__ __launch_bounds__(256) void k_gram_reduce(GramParams P) {
       const int li = si0 + yy, lj = sj0 + tx;
       float g = 0.f;
       for (int s = 0; s < P.splits; ++s)
-        g += P.partial[((int64_t)s * P.ntiles + tile) * (GT * GT) + li * GT + lj];
+        g += P.partial[((int64_t)s * P.tile_count + ltile) * (GT * GT) + li * GT + lj];
       const int64_t i = row0 + li, j = col0 + lj;
       const float sI = (i < P.n) ? P.stdv[i] : 1.f, sJ = (j < P.n) ? P.stdv[j] : 1.f;
-      const float v = rdm_value(g, 0.f, i, j, P, sI, sJ);
+      const float v = rdm_value(g, i, j, P, sI, sJ);
       if (i < P.n && j < P.n) P.rdm[i * P.ldr + j] = v;
       tr[yy][tx] = v;
     }
@@ -339,15 +342,21 @@ __global__ __launch_bounds__(256) void k_gram_reduce(GramParams P) {
   }
 }
 
-static void gram_geometry(int64_t n, int64_t d, int& T, int& ntiles, int& splits,
-                          int64_t& kslice) {
+static int64_t gram_tiles(int64_t n) {
+  const int64_t T = (n + GT - 1) / GT;
+  return T * (T + 1) / 2;
+}
+
+// Split-K factor for `count` tiles of depth d: enough blocks for two per CU.
+static void gram_geometry(int64_t n, int64_t d, int64_t count, int& T, int& ntiles,
+                          int& splits, int64_t& kslice) {
   T = (int)((n + GT - 1) / GT);
   ntiles = T * (T + 1) / 2;
   const int64_t kt = (d + GK - 1) / GK;  // k stages
   const int target = 2 * num_cus();     // two resident blocks per CU
   int s = 1;
-  if (ntiles < target) {
-    s = (target + ntiles - 1) / ntiles;
+  if (count < target) {
+    s = (int)((target + count - 1) / count);
     const int64_t maxs = std::max<int64_t>(1, kt / 4);  // >= 4 stages per split
     if (s > maxs) s = (int)maxs;
   }
@@ -367,12 +376,37 @@ size_t vr_rdm_pearson_workspace(int64_t n, int64_t d) {
   if (n <= 0 || d <= 0) return 256;
   int T, ntiles, splits;
   int64_t kslice;
-  gram_geometry(n, d, T, ntiles, splits, kslice);
+  gram_geometry(n, d, gram_tiles(n), T, ntiles, splits, kslice);
   Carver c(nullptr);
   c.take<float>((size_t)n);
   c.take<float>((size_t)n);
   if (splits > 1) c.take<float>((size_t)splits * ntiles * GT * GT);
   return c.bytes();
+}
+
+size_t vr_rdm_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
+  if (n <= 0 || d <= 0 || tile_end <= tile_begin) return 256;
+  int T, ntiles, splits;
+  int64_t kslice;
+  gram_geometry(n, d, tile_end - tile_begin, T, ntiles, splits, kslice);
+  Carver c(nullptr);
+  c.take<float>((size_t)n);
+  c.take<float>((size_t)n);
+  if (splits > 1) c.take<float>((size_t)splits * (tile_end - tile_begin) * GT * GT);
+  return c.bytes();
+}
+
+int64_t vr_rdm_tile_count(int64_t n) { return n > 0 ? gram_tiles(n) : 0; }
+
+int64_t vr_rdm_tile_cost(int64_t n, int64_t tile) {
+  // elements of the tile on or above the diagonal (the work the balancer spreads)
+  int T = (int)((n + GT - 1) / GT), bi, bj;
+  int p = (int)tile, r = 0;
+  while (r + 1 < T && (int64_t)(r + 1) * T - (int64_t)(r + 1) * r / 2 <= p) ++r;
+  bi = r;
+  bj = r + (p - (r * T - r * (r - 1) / 2));
+  const int64_t h = std::min<int64_t>(GT, n - (int64_t)bi * GT), w = std::min<int64_t>(GT, n - (int64_t)bj * GT);
+  return bi == bj ? h * (h + 1) / 2 : h * w;
 }
 
 int vr_row_stats_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* mean,
@@ -389,27 +423,22 @@ int vr_row_stats_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* m
   return VR_OK;
 }
 
-int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
-                       int64_t ldr, float correction, void* ws, size_t ws_bytes,
-                       void* stream) {
-  VR_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldr >= n,
-             "vr_rdm_pearson_f32: bad shape n=%lld d=%lld ldx=%lld ldr=%lld", (long long)n,
-             (long long)d, (long long)ldx, (long long)ldr);
-  if (n == 0) return VR_OK;
-  VR_REQUIRE(X && rdm, "vr_rdm_pearson_f32: null pointer");
-  VR_REQUIRE(n <= (1 << 24), "vr_rdm_pearson_f32: n=%lld too large", (long long)n);
-  const size_t need = vr_rdm_pearson_workspace(n, d);
+static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm, int64_t ldr,
+                      float correction, int64_t tile_begin, int64_t tile_end, void* ws,
+                      size_t ws_bytes, void* stream, size_t need) {
   if (ws_bytes < need || ws == nullptr) {
-    set_error("vr_rdm_pearson_f32: workspace %zu < %zu", ws_bytes, need);
+    set_error("vr_rdm_pearson: workspace %zu < %zu", ws_bytes, need);
     return VR_EWORKSPACE;
   }
   hipStream_t st = as_stream(stream);
   GramParams P{};
-  gram_geometry(n, d, P.T, P.ntiles, P.splits, P.kslice);
+  gram_geometry(n, d, tile_end - tile_begin, P.T, P.ntiles, P.splits, P.kslice);
+  P.tile0 = (int)tile_begin;
+  P.tile_count = (int)(tile_end - tile_begin);
   Carver c(ws);
   float* mean = c.take<float>((size_t)n);
   float* stdv = c.take<float>((size_t)n);
-  P.partial = (P.splits > 1) ? c.take<float>((size_t)P.splits * P.ntiles * GT * GT) : nullptr;
+  P.partial = (P.splits > 1) ? c.take<float>((size_t)P.splits * P.tile_count * GT * GT) : nullptr;
   VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
   P.X = X;
   P.mean = mean;
@@ -422,14 +451,43 @@ int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float*
   P.correction = correction;
   P.vec = ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && ((ldx & 3) == 0) &&
           ((reinterpret_cast<uintptr_t>(rdm) & 15) == 0);
-  const unsigned nblk = (unsigned)P.ntiles * (unsigned)P.splits;
+  if (P.tile_count <= 0) return VR_OK;
+  const unsigned nblk = (unsigned)P.tile_count * (unsigned)P.splits;
   k_gram<<<nblk, G_THREADS, 0, st>>>(P);
   VR_CHECK_LAUNCH();
   if (P.splits > 1) {
-    k_gram_reduce<<<(unsigned)P.ntiles, 256, 0, st>>>(P);
+    k_gram_reduce<<<(unsigned)P.tile_count, 256, 0, st>>>(P);
     VR_CHECK_LAUNCH();
   }
   return VR_OK;
+}
+
+int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
+                       int64_t ldr, float correction, void* ws, size_t ws_bytes,
+                       void* stream) {
+  VR_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldr >= n,
+             "vr_rdm_pearson_f32: bad shape n=%lld d=%lld ldx=%lld ldr=%lld", (long long)n,
+             (long long)d, (long long)ldx, (long long)ldr);
+  if (n == 0) return VR_OK;
+  VR_REQUIRE(X && rdm, "vr_rdm_pearson_f32: null pointer");
+  VR_REQUIRE(n <= (1 << 20), "vr_rdm_pearson_f32: n=%lld too large", (long long)n);
+  return rdm_launch(X, n, d, ldx, rdm, ldr, correction, 0, gram_tiles(n), ws, ws_bytes, stream,
+                    vr_rdm_pearson_workspace(n, d));
+}
+
+int vr_rdm_pearson_tiles_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
+                             int64_t ldr, float correction, int64_t tile_begin,
+                             int64_t tile_end, void* ws, size_t ws_bytes, void* stream) {
+  VR_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldr >= n,
+             "vr_rdm_pearson_tiles_f32: bad shape n=%lld d=%lld", (long long)n, (long long)d);
+  VR_REQUIRE(n <= (1 << 20), "vr_rdm_pearson_tiles_f32: n too large");
+  VR_REQUIRE(tile_begin >= 0 && tile_end >= tile_begin && tile_end <= gram_tiles(n),
+             "vr_rdm_pearson_tiles_f32: tile range [%lld, %lld) outside [0, %lld)",
+             (long long)tile_begin, (long long)tile_end, (long long)gram_tiles(n));
+  if (n == 0 || tile_end == tile_begin) return VR_OK;
+  VR_REQUIRE(X && rdm, "vr_rdm_pearson_tiles_f32: null pointer");
+  return rdm_launch(X, n, d, ldx, rdm, ldr, correction, tile_begin, tile_end, ws, ws_bytes,
+                    stream, vr_rdm_tiles_workspace(n, d, tile_begin, tile_end));
 }
 
 }  // extern "C"

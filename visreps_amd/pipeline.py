@@ -1,0 +1,226 @@
+"""All-layers x all-ROIs RSA with stimulus sharding over ranks (the bench workload and the
+multi-GPU path of the eval driver).
+
+Per step (BASELINE.json configs[1]: CustomCNN points x NSD ROIs, N stimuli, 1000 boots):
+  1. extraction   each rank forwards its stimulus shard; the 14 hooked points are
+                  flattened into per-point (n_local, D) HBM buffers;
+  2. RDMs         per point / ROI: RCCL all-gather of the feature rows (the one
+                  data-path exchange), each rank computes a cost-balanced range of the
+                  128x128 upper-triangle Gram tiles into a zeroed RDM, and a sum
+                  all-reduce assembles the RDM on every rank;
+  3. rank plans   each rank sorts the triangles of the RDMs its units use;
+  4. units        (point, ROI) units are dealt round-robin to ranks; each unit is the
+                  point estimate + n_boot subsets in one engine call
+                  (evals.py:341-373 semantics, RandomState(seed) per unit);
+  5. gather       per-unit score vectors are gathered to every rank.
+Scores are exact-integer Spearman values, so they do not depend on the world size.
+"""
+from __future__ import annotations
+
+import functools
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ._lib import check, lib, stream_of, workspace
+from .analysis import rsa as R
+from .analysis._random import bootstrap_indices
+from .dataloaders.synthetic import shard_rows
+
+
+@dataclass
+class StepTimes:
+    """HIP-event totals of the hot kernels on this rank (ms)."""
+
+    gram_ms: float = 0.0
+    gram_flops: float = 0.0
+    engine_ms: float = 0.0
+    engine_bytes: float = 0.0
+    engine_calls: int = 0
+    _pending: list = field(default_factory=list)
+
+    def record(self, kind: str, start, end, work: float):
+        self._pending.append((kind, start, end, work))
+
+    def resolve(self):
+        for kind, s, e, w in self._pending:
+            ms = s.elapsed_time(e)
+            if kind == "gram":
+                self.gram_ms += ms
+                self.gram_flops += w
+            else:
+                self.engine_ms += ms
+                self.engine_bytes += w
+                self.engine_calls += 1
+        self._pending.clear()
+
+
+def _world(pg) -> Tuple[int, int]:
+    if pg is None or not dist.is_available() or not dist.is_initialized():
+        return 0, 1
+    return dist.get_rank(pg), dist.get_world_size(pg)
+
+
+# ---------------------------------------------------------------------------------------
+# block-distributed RDM
+# ---------------------------------------------------------------------------------------
+@functools.lru_cache(maxsize=16)
+def _tile_cum_cost(n: int) -> np.ndarray:
+    L = lib()
+    T = int(L.vr_rdm_tile_count(n))
+    costs = np.array([L.vr_rdm_tile_cost(n, t) for t in range(T)], dtype=np.float64)
+    return np.concatenate([[0.0], np.cumsum(costs)])
+
+
+def tile_ranges(n: int, world: int) -> List[Tuple[int, int]]:
+    """Contiguous ranges of the upper-triangle tile list with near-equal element counts."""
+    cum = _tile_cum_cost(n)
+    T = len(cum) - 1
+    bounds = [0]
+    for r in range(1, world):
+        bounds.append(int(np.searchsorted(cum, cum[-1] * r / world)))
+    bounds.append(T)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def _tile_fraction(n: int, t0: int, t1: int) -> float:
+    cum = _tile_cum_cost(n)
+    return float((cum[t1] - cum[t0]) / cum[-1]) if cum[-1] > 0 else 0.0
+
+
+def rdm_tiles_into(x: torch.Tensor, out: torch.Tensor, t0: int, t1: int,
+                   correction: float = 1e-12, times: Optional[StepTimes] = None) -> None:
+    """Write Gram tiles [t0, t1) of x's RDM (and their mirrors) into out."""
+    n, d = x.shape
+    if t1 <= t0:
+        return
+    L = lib()
+    ws = workspace.get(x.device, L.vr_rdm_tiles_workspace(n, d, t0, t1), "rdm")
+    ev = None
+    if times is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    check(L.vr_rdm_pearson_tiles_f32(x.data_ptr(), n, d, x.stride(0), out.data_ptr(), n,
+                                     float(correction), t0, t1, ws.data_ptr(), ws.numel(),
+                                     stream_of(x.device)), "vr_rdm_pearson_tiles_f32")
+    if times is not None:
+        ev[1].record()
+        times.record("gram", ev[0], ev[1], _gram_flops(n, d) * _tile_fraction(n, t0, t1))
+
+
+def _gram_flops(n: int, d: int) -> float:
+    """Algorithmic Gram FLOPs of one RDM: N(N+1)D (unique pairs, 2 FLOP/MAC)."""
+    return float(n) * (n + 1) * d
+
+
+def gather_rows(x_local: torch.Tensor, n: int, pg) -> torch.Tensor:
+    """RCCL all-gather of every rank's stimulus rows into the full (n, d) matrix."""
+    rank, world = _world(pg)
+    if world == 1:
+        return x_local
+    sizes = [len(shard_rows(n, r, world)) for r in range(world)]
+    per = max(sizes)
+    d = x_local.size(1)
+    buf = torch.zeros((per, d), dtype=x_local.dtype, device=x_local.device)
+    buf[: x_local.size(0)] = x_local
+    full = torch.empty((world * per, d), dtype=x_local.dtype, device=x_local.device)
+    dist.all_gather_into_tensor(full, buf, group=pg)
+    if all(s == per for s in sizes):
+        return full
+    return torch.cat([full[r * per: r * per + sizes[r]] for r in range(world)], 0)
+
+
+def distributed_rdm(x_local: torch.Tensor, n: int, pg=None,
+                    times: Optional[StepTimes] = None) -> torch.Tensor:
+    """Full (n, n) RDM on every rank from each rank's stimulus rows."""
+    rank, world = _world(pg)
+    x = gather_rows(x_local.float().contiguous(), n, pg)
+    if world == 1:
+        out = torch.empty((n, n), dtype=torch.float32, device=x.device)
+        rdm_tiles_into(x, out, 0, int(lib().vr_rdm_tile_count(n)), times=times)
+        return out
+    out = torch.zeros((n, n), dtype=torch.float32, device=x.device)
+    t0, t1 = tile_ranges(n, world)[rank]
+    rdm_tiles_into(x, out, t0, t1, times=times)
+    del x
+    dist.all_reduce(out, op=dist.ReduceOp.SUM, group=pg)
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# units
+# ---------------------------------------------------------------------------------------
+def engine_bytes(n: int, n_boot: int) -> float:
+    """Algorithmic bytes of one unit: 8 * [M(N) + n_boot * M(int(0.9 N))]."""
+    k = int(0.9 * n)
+    return 8.0 * (n * (n - 1) // 2 + n_boot * (k * (k - 1) // 2))
+
+
+def run_unit(plan_m: R.RankPlan, plan_n: R.RankPlan, idx: Optional[np.ndarray],
+             times: Optional[StepTimes] = None) -> torch.Tensor:
+    ev = None
+    if times is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    scores = R.bootstrap_spearman(plan_m, plan_n, idx, full_first=True)
+    if times is not None:
+        ev[1].record()
+        times.record("engine", ev[0], ev[1], engine_bytes(plan_m.n, 0 if idx is None else len(idx)))
+    return scores
+
+
+def summarize(scores: np.ndarray, bootstrap: bool) -> Dict:
+    point = float(scores[0])
+    res = {"score": point, "ci_low": None, "ci_high": None}
+    if bootstrap:
+        boot = scores[1:]
+        res["ci_low"] = R.percentile(boot, 2.5)
+        res["ci_high"] = R.percentile(boot, 97.5)
+        res["bootstrap_scores"] = boot.tolist()
+    return res
+
+
+def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[str],
+                  neural_rdms: Dict[str, torch.Tensor], n: int, *, n_boot: int = 1000,
+                  seed: int = 42, pg=None, times: Optional[StepTimes] = None,
+                  keep_plans: bool = False) -> Dict[Tuple[str, str], Dict]:
+    """Point + bootstrap Spearman RSA for every (point, region) unit; units round-robin
+    over ranks; returns the per-unit results on every rank."""
+    rank, world = _world(pg)
+    regions = list(neural_rdms)
+    units = [(p, r) for p in points for r in regions]
+    mine = [u for i, u in enumerate(units) if i % world == rank]
+    k = int(0.9 * n)
+    idx = None
+    if n_boot > 0:  # one upload of the (n_boot, k) index sets, shared by every unit
+        dev = next(iter(neural_rdms.values())).device
+        idx = torch.from_numpy(np.array(bootstrap_indices(seed, n, k, n_boot))).to(dev)
+    nplans = {}
+    local: Dict[Tuple[str, str], np.ndarray] = {}
+    by_point: Dict[str, List[str]] = {}
+    for p, r in mine:
+        by_point.setdefault(p, []).append(r)
+    for p in points:
+        rdm = model_rdm_fn(p)  # collective: every rank takes part in every point's RDM
+        if p not in by_point:
+            del rdm
+            continue
+        pm = R.RankPlan(rdm)
+        del rdm
+        for r in by_point[p]:
+            if r not in nplans:
+                nplans[r] = R.RankPlan(neural_rdms[r])
+            local[(p, r)] = run_unit(pm, nplans[r], idx, times).cpu().numpy()
+    if world > 1:
+        gathered: List[Dict] = [None] * world
+        dist.all_gather_object(gathered, local, group=pg)
+        merged = {}
+        for g in gathered:
+            merged.update(g)
+        local = merged
+    return {u: summarize(local[u], n_boot > 0) for u in units}
