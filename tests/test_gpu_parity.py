@@ -124,6 +124,28 @@ def test_spearman_exact_vs_oracle(dev, n, levels):
         assert abs(got - ref) <= 1e-9
 
 
+def test_spearman_giant_tie_group_wide_path(dev):
+    # a tie group larger than 32767 - 4096 positions forces u32 chunk ranks
+    n = 300
+    rng = np.random.RandomState(9)
+    a = rng.rand(n, n).astype(np.float32)
+    a[rng.rand(n, n) < 0.75] = 0.5
+    a = np.triu(a, 1)
+    a = a + a.T
+    b = _tied_rdm(n, 10, levels=50)
+    iu = np.triu_indices(n, 1)
+    assert np.sum(a[iu] == 0.5) > 30000
+    pa, pb = R.RankPlan(torch.from_numpy(a).to(dev)), R.RankPlan(torch.from_numpy(b).to(dev))
+    idx = np.stack([rng.choice(n, 270, replace=False) for _ in range(70)]).astype(np.int32)
+    got = R.bootstrap_spearman(pa, pb, idx).cpu().numpy()
+    assert abs(got[0] - O.midrank_spearman(a[iu], b[iu])) <= 1e-12
+    ik = np.triu_indices(270, 1)
+    for i in range(70):
+        s = idx[i]
+        ref = O.midrank_spearman(a[np.ix_(s, s)][ik], b[np.ix_(s, s)][ik])
+        assert abs(got[i + 1] - ref) <= 1e-12
+
+
 def test_spearman_nan_and_constant(dev):
     a = _tied_rdm(10, 1)
     b = a.copy()

@@ -1,0 +1,81 @@
+// Rank plan layout shared by plan.hip (construction) and engine.hip (use).
+//
+// A rank plan is the one-time per-RDM precompute behind every Spearman on that RDM:
+// the M = n(n-1)/2 strict-upper-triangle values radix-sorted, tie groups (equal fp32
+// values) marked, positions cut into chunks of ~PLAN_L pairs aligned to group starts.
+#pragma once
+
+#include "internal.h"
+
+namespace vr {
+
+constexpr uint32_t PLAN_L = 4096;  // target pairs per chunk
+
+struct PlanHeader {
+  int64_t n;
+  int64_t M;
+  uint32_t G;          // tie groups (device-written)
+  uint32_t nchunks;
+  uint32_t L;
+  uint32_t has_nan;    // device-written: any NaN in the triangle
+  uint32_t max_group;  // device-written: largest tie group
+  uint32_t pad[55];
+};
+static_assert(sizeof(PlanHeader) == 256, "header size");
+
+struct PlanView {
+  PlanHeader* hdr;
+  uint32_t* codes;          // [M]    (a << 16) | b, sorted by value
+  uint32_t* gstart;         // [M+1]  first G+1 valid: group start positions, gstart[G] = M
+  uint32_t* pos_of_pair;    // [M]    triangle index -> sorted position
+  uint32_t* chunk_of_pair;  // [M]    triangle index -> chunk of its sorted position
+  uint32_t* chunk_g;        // [nchunks+1] first group of each chunk
+  uint32_t* gflag;          // [(M+31)/32 + 2] bit i = position i starts a tie group
+};
+
+inline uint32_t plan_nchunks(int64_t M) { return (uint32_t)((M + PLAN_L - 1) / PLAN_L); }
+
+inline PlanView plan_layout(void* base, int64_t n, size_t* bytes = nullptr) {
+  const int64_t M = pairs_of(n);
+  Carver c(base);
+  PlanView v;
+  v.hdr = c.take<PlanHeader>(1);
+  v.codes = c.take<uint32_t>((size_t)M);
+  v.gstart = c.take<uint32_t>((size_t)M + 1);
+  v.pos_of_pair = c.take<uint32_t>((size_t)M);
+  v.chunk_of_pair = c.take<uint32_t>((size_t)M);
+  v.chunk_g = c.take<uint32_t>((size_t)plan_nchunks(M) + 1);
+  v.gflag = c.take<uint32_t>((size_t)(M + 31) / 32 + 2);
+  if (bytes) *bytes = c.bytes();
+  return v;
+}
+
+inline size_t plan_bytes(int64_t n) {
+  size_t b = 0;
+  plan_layout(nullptr, n, &b);
+  return b;
+}
+
+struct PlanBuildWs {
+  uint32_t *keys, *keys_alt, *vals_alt, *flags, *gidx, *radix, *scan;
+};
+
+inline PlanBuildWs plan_build_layout(void* base, int64_t n, size_t* bytes) {
+  const int64_t M = pairs_of(n);
+  Carver c(base);
+  PlanBuildWs w;
+  w.keys = c.take<uint32_t>((size_t)M);
+  w.keys_alt = c.take<uint32_t>((size_t)M);
+  w.vals_alt = c.take<uint32_t>((size_t)M);
+  w.flags = c.take<uint32_t>((size_t)M);
+  w.gidx = c.take<uint32_t>((size_t)M);
+  w.radix = c.take<uint32_t>(radix_ws_elems(M));
+  w.scan = c.take<uint32_t>(scan_ws_elems(M));
+  if (bytes) *bytes = c.bytes();
+  return w;
+}
+
+int build_plan(const float* rdm, int64_t n, int64_t ld, const PlanView& P, const PlanBuildWs& W,
+               hipStream_t st);
+
+}  // namespace vr
