@@ -133,6 +133,19 @@ int vr_bootstrap_spearman_f32(const float* A, const float* B, int64_t n, int64_t
                               void* stream);
 
 /* ------------------------------------------------------------------------------
+ * Phase-1 sparse random projection (extraction side).
+ * Replaces torch.sparse.mm(P, flat.t()).t() (visreps/models/utils.py:334-336) with P the
+ * CSR (k x D) components_ of sklearn SparseRandomProjection
+ * (visreps/models/utils.py:297-322, visreps/analysis/sparse_random_projection.py:83-150).
+ * indptr (k+1) / indices (nnz) int32, values (nnz) fp32, X (B x D, row stride ldx) fp32,
+ * out (B x k, row stride ldo) fp32 -- all device. fp32 fma in CSR order per output.
+ * -------------------------------------------------------------------------- */
+size_t vr_srp_workspace(int64_t B, int64_t D);
+int vr_srp_csr_f32(const int32_t* indptr, const int32_t* indices, const float* values,
+                   int64_t k, int64_t D, const float* X, int64_t B, int64_t ldx, float* out,
+                   int64_t ldo, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------
  * Host: legacy numpy RandomState (MT19937) index streams, bit-exact.
  * Replaces np.random.RandomState(seed) + .choice(n, k, replace=False) / .permutation(n)
  * (evals.py:260-261,356,362-364; rsa.py:169,176,248-250; evals.py:111-113).

@@ -13,15 +13,20 @@
 // mu = M'(M'+1)^2, M' = included pairs: exact integer sums -> fp64 at the end, so scores
 // do not depend on chunking, lane grouping, launch order or GPU count.
 //
-// One pass evaluates 64 subsets: lane w of every wave is subset w, masks[x] bit w says
-// whether stimulus x is in subset w (LDS). Waves own contiguous segments of chunks.
-//  k_rankA   walk A order; per tie group y'_A (segment-relative); scatter the chunk-
-//            relative rank yA~ = y'_A - 2 lp_c to the pair's B position:
-//            TB[posB][w] (u16 when chunk spans fit, else u32); segment sums n, n y', n y'^2
-//  k_scan_seg + k_add_base   chunk bases baseA[c][w] (segment prefix + local prefix)
-//  k_rankB   walk B order streaming TB rows; yA = 2 baseA[chunkA(pair)][w] + yA~; per B
-//            tie group S = sum of included yA, then y'_B S, n y'_B, n y'_B^2 (segment-rel.)
-//  k_final   combine segments with their bases -> rho per lane
+// One pass evaluates 64 subsets: lane s of every wave is subset s, masks[x] bit s says
+// whether stimulus x is in subset s (LDS). Waves own contiguous segments of chunks and
+// walk them in 64-position windows: lane j looks up pair w0+j (one coalesced code load,
+// two LDS mask reads), and a 64x64 bit transpose across the wave hands lane s the
+// inclusion bits of all 64 pairs for subset s. Counts before any position are then
+// popcounts, so a tie group [gs, ge) closes in O(1): y = c(gs) + c(ge) + 1.
+//  k_rankA   A order: per group the segment-relative y'_A; TB[pos][s] = y'_A - 2 lp_chunk
+//            written in A order (streaming rows; u16 when chunk spans fit, else u32);
+//            segment sums  sum k y', sum k y'^2;  lpA[chunk] = chunk start count
+//  scan      per-lane prefix over segments -> baseA[chunk] = segA_pre + lpA
+//  k_rankB   B order: yA = 2 baseA[chunkA] + TB[posA] gathered per pair (one 128-byte
+//            row per pair); per B group S = sum of included yA; sums S y'_B, S, k y'_B,
+//            k y'_B^2 (segment-relative)
+//  scan + k_final_part + k_final_top   combine segments with their bases -> rho per lane
 #include <type_traits>
 #include <vector>
 
@@ -32,14 +37,14 @@ namespace vr {
 typedef unsigned __int128 u128;
 typedef __int128 i128;
 
-constexpr int ENG_THREADS = 1024;  // 16 waves per workgroup
+constexpr int ENG_THREADS = 1024;  // 16 waves per workgroup share one LDS mask table
 constexpr int WAVES_PER_WG = ENG_THREADS / 64;
 constexpr int LANES = 64;
-constexpr int U = 16;  // pairs per block: one vector load brings 16 pair codes
+constexpr int SCAN_SEGS = 256;     // segments per block in the segment scans / final fold
 
 struct EngineCfg {
-  int grid;      // persistent workgroups
-  int nwaves;    // grid * WAVES_PER_WG = number of chunk segments
+  int grid;      // workgroups
+  int nwaves;    // grid * WAVES_PER_WG = number of chunk segments (A and B each)
   size_t lds;    // dynamic LDS for the masks (0: masks read from global)
   bool use_lds;
 };
@@ -56,37 +61,50 @@ static EngineCfg engine_cfg(int64_t n) {
   return c;
 }
 
+static inline uint32_t scan_blocks(uint32_t nseg) { return (nseg + SCAN_SEGS - 1) / SCAN_SEGS; }
+
+// Segment partials are structure-of-arrays [field][seg][lane] so every access is a row.
+enum { PA_TIEL = 0, PA_TIEH, PA_N };
+enum { PB_ACCL = 0, PB_ACCH, PB_ST, PB_TIEL, PB_TIEH, PB_N };
+
 struct EngineWs {
   uint64_t* masks;      // [n]
-  uint32_t* posB_byA;   // [M]  A position -> B position (per unit)
+  uint32_t* posA_byB;   // [M]  B position -> A position (per unit)
   uint32_t* chunkA_byB; // [M]  B position -> A chunk (per unit)
-  void* TB;             // [M * lw] u16 or u32 chunk-relative yA~
-  uint32_t* lpA;        // [nch * 64] local prefix at chunk start within its segment
-  uint32_t* baseA;      // [nch * 64]
+  void* TB;             // [M * lw] u16 or u32 chunk-relative yA~, A order
+  uint32_t* lpA;        // [nch * 64] count at chunk start, relative to its segment
+  uint32_t* baseA;      // [nch * 64] absolute count at chunk start
   uint32_t* segA_tot;   // [nw * 64]
-  uint64_t* segA_part;  // [nw * 64 * 3]  sum n y', sum n y'^2 (u128)
+  uint64_t* segA_part;  // [PA_N][nw][64]  tie term sum (k^3 - k)
   uint32_t* segA_pre;   // [nw * 64]
   uint32_t* segB_tot;   // [nw * 64]
-  uint64_t* segB_part;  // [nw * 64 * 6]  acc (u128), St, NY, NY2 (u128)
-  uint32_t* totA;       // [64]
+  uint64_t* segB_part;  // [PB_N][nw][64]  sum S y'_B, sum S, tie term
+  uint32_t* segB_pre;   // [nw * 64]
+  uint32_t* bsum;       // [scan_blocks * 64] scan scratch
+  uint64_t* fpart;      // [scan_blocks][6][64] final-fold partials
+  uint32_t* totA;       // [64] included pairs per subset
 };
 
 static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t* bytes) {
   const int64_t M = pairs_of(n);
   const size_t nch = plan_nchunks(M);
+  const size_t nsb = scan_blocks((uint32_t)nwaves);
   Carver c(base);
   EngineWs e;
   e.masks = c.take<uint64_t>((size_t)n);
-  e.posB_byA = c.take<uint32_t>((size_t)M);
+  e.posA_byB = c.take<uint32_t>((size_t)M);
   e.chunkA_byB = c.take<uint32_t>((size_t)M);
   e.TB = c.take<uint32_t>((size_t)M * (size_t)lw);  // sized for u32
   e.lpA = c.take<uint32_t>(nch * LANES);
   e.baseA = c.take<uint32_t>(nch * LANES);
   e.segA_tot = c.take<uint32_t>((size_t)nwaves * LANES);
-  e.segA_part = c.take<uint64_t>((size_t)nwaves * LANES * 3);
+  e.segA_part = c.take<uint64_t>((size_t)nwaves * LANES * PA_N);
   e.segA_pre = c.take<uint32_t>((size_t)nwaves * LANES);
   e.segB_tot = c.take<uint32_t>((size_t)nwaves * LANES);
-  e.segB_part = c.take<uint64_t>((size_t)nwaves * LANES * 6);
+  e.segB_part = c.take<uint64_t>((size_t)nwaves * LANES * PB_N);
+  e.segB_pre = c.take<uint32_t>((size_t)nwaves * LANES);
+  e.bsum = c.take<uint32_t>(nsb * LANES);
+  e.fpart = c.take<uint64_t>(nsb * 6 * LANES);
   e.totA = c.take<uint32_t>(LANES);
   if (bytes) *bytes = c.bytes();
   return e;
@@ -95,15 +113,16 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
 // ---------------------------------------------------------------------------------
 // per-unit join and per-pass masks
 // ---------------------------------------------------------------------------------
-__global__ void k_join(const uint32_t* __restrict__ codesA, const uint32_t* __restrict__ codesB,
-                       int64_t M, int64_t n, const uint32_t* __restrict__ posOfPairB,
+__global__ void k_join(const uint32_t* __restrict__ codesB, int64_t M, int64_t n,
+                       const uint32_t* __restrict__ posOfPairA,
                        const uint32_t* __restrict__ chunkOfPairA,
-                       uint32_t* __restrict__ posB_byA, uint32_t* __restrict__ chunkA_byB) {
+                       uint32_t* __restrict__ posA_byB, uint32_t* __restrict__ chunkA_byB) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M) return;
-  const uint32_t ca = codesA[i], cb = codesB[i];
-  posB_byA[i] = posOfPairB[tri_index(ca >> 16, ca & 0xffffu, (uint64_t)n)];
-  chunkA_byB[i] = chunkOfPairA[tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n)];
+  const uint32_t cb = codesB[i];
+  const uint64_t t = tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n);
+  posA_byB[i] = posOfPairA[t];
+  chunkA_byB[i] = chunkOfPairA[t];
 }
 
 // bit w of masks[x] <- x in subset (set0 + w); subset 0 is "all stimuli" when full_first.
@@ -143,144 +162,289 @@ __device__ inline uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_re
 __device__ inline uint32_t readlane_u32(uint32_t v, uint32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
-__device__ inline uint64_t readlane_u64(uint64_t v, uint32_t l) {
-  return ((uint64_t)readlane_u32((uint32_t)(v >> 32), l) << 32) | readlane_u32((uint32_t)v, l);
-}
 
-// Group-start bits of positions [p, p+16) (bit t <-> position p+t), wave-uniform.
-__device__ inline uint32_t flags16(const uint32_t* __restrict__ gflag, uint32_t p) {
-  const uint32_t w = p >> 5, sh = p & 31;
-  const uint64_t two = ((uint64_t)gflag[w + 1] << 32) | gflag[w];
-  return (uint32_t)(two >> sh) & 0xffffu;
-}
-
-// Lane (l & 15) looks up both stimulus masks of pair p + (l & 15); the AND is then
-// broadcast per pair with readlane.
-__device__ inline uint64_t block_masks(const uint64_t* m, const uint32_t* __restrict__ codes,
-                                       uint32_t p, uint32_t cnt, int lane) {
-  const uint32_t sub = lane & (U - 1);
-  uint64_t both = 0;
-  if (sub < cnt) {
-    const uint32_t code = codes[p + sub];
-    both = m[code >> 16] & m[code & 0xffffu];
-  }
-  return both;
-}
-
-__device__ inline uint32_t incl(uint64_t both_block, int t, int lane) {
-  return (uint32_t)(readlane_u64(both_block, t) >> lane) & 1u;
-}
-
-// Uniform-address load through the constant address space: always selected as SMEM
-// (s_load, lgkmcnt) so it never queues behind the wave's outstanding vector stores.
+// Uniform-address load through the constant address space: selected as SMEM (s_load).
 template <typename T>
 __device__ inline T sload(const T* p) {
   return *(const __attribute__((address_space(4))) T*)p;
 }
 
+__device__ inline uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// 64x64 bit-matrix transpose across the wave: on entry bit s of lane j is element (j, s);
+// on exit bit j of lane s is. Recursive block swap, 6 stages of one 64-bit exchange.
+__device__ inline uint64_t transpose64(uint64_t x, int lane) {
+  constexpr uint64_t K[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                             0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int st = 0; st < 6; ++st) {
+    const int w = 32 >> st;
+    const uint64_t p = shfl_xor64(x, w);
+    const uint64_t hi = (x & ~K[st]) | ((p & ~K[st]) >> w);  // lanes with bit w set
+    const uint64_t lo = (x & K[st]) | ((p & K[st]) << w);
+    const uint64_t sel = 0ull - (uint64_t)((lane >> (5 - st)) & 1);  // branch-free select
+    x = (hi & sel) | (lo & ~sel);
+  }
+  return x;
+}
+
+__device__ inline uint64_t lowmask(uint32_t b) { return b >= 64 ? ~0ull : ((1ull << b) - 1ull); }
+
+// Inclusion bits of the window for this lane's subset (bit j <-> position w0 + j), from
+// the window's codes (lane j holds pair w0 + j).
+__device__ inline uint64_t window_bits(const uint64_t* m, uint32_t code, uint32_t w0, uint32_t P0,
+                                       uint32_t P1, int lane, bool active) {
+  const uint32_t pos = w0 + (uint32_t)lane;
+  uint64_t x = 0;
+  if (pos >= P0 && pos < P1) x = m[code >> 16] & m[code & 0xffffu];
+  x = transpose64(x, lane);
+  return active ? x : 0ull;
+}
+
+// The window's 64 codes and group-start flags through the scalar unit (s_load_dwordx16 x4
+// + s_load_dwordx2). Issued one window ahead (k_rankA), they never queue behind the wave's
+// own TB stores the way a vector load would (vmcnt is in order on CDNA). Reads past the
+// segment stay inside the plan buffer (gstart follows codes; gflag has 2 spare words).
+struct WindowScalars {
+  uint32_t c[64];
+  uint32_t f0, f1;
+};
+__device__ inline void load_window(const uint32_t* __restrict__ codes,
+                                   const uint32_t* __restrict__ gflag, uint32_t w0,
+                                   WindowScalars& w) {
+#pragma unroll
+  for (int j = 0; j < 64; ++j) w.c[j] = sload(codes + w0 + j);
+  w.f0 = sload(gflag + (w0 >> 5));
+  w.f1 = sload(gflag + (w0 >> 5) + 1);
+}
+// lane j <- c[j] (v_writelane from SGPRs)
+__device__ inline uint32_t place_codes(const WindowScalars& w) {
+  uint32_t code = 0;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) asm("v_writelane_b32 %0, %1, %2" : "+v"(code) : "s"(w.c[j]), "i"(j));
+  return code;
+}
+
+__device__ inline uint64_t restrict_flags(uint64_t F, uint32_t w0, uint32_t P0, uint32_t P1) {
+  if (P0 >= w0) F &= ~lowmask(P0 - w0 + 1);
+  if (P1 - w0 < 64) F = (F & lowmask(P1 - w0)) | (1ull << (P1 - w0));
+  return F;
+}
+
+// sum over tie groups of k^3 - k = k (k^2 - 1). When the plan's largest tie group is below
+// 2^16 (BIGT false, the normal case) one 32x32+64 multiply-add per group, and the sum stays
+// below 2^63 for any segment; otherwise 128-bit.
+template <bool BIGT>
+__device__ inline void tie_add(uint64_t& t64, u128& tbig, uint32_t k) {
+  if (!BIGT) {
+    t64 += (uint64_t)k * (k * k - 1u);
+  } else {
+    tbig += (u128)((uint64_t)k * k) * k - k;
+  }
+}
+
+// rows [r0, r0 + cnt) of TB get v in this lane's column: row addresses are wave-uniform
+// (SGPR base + lane offset), four rows per step
+template <bool FULL, typename TBT>
+__device__ inline void store_rows(TBT* __restrict__ TB, uint32_t stride, uint32_t r0, uint32_t cnt,
+                                  int lane, TBT v) {
+  TBT* row = TB + (size_t)r0 * stride + lane;
+  uint32_t i = 0;
+  for (; i + 4 <= cnt; i += 4, row += 4 * (size_t)stride) {
+    __builtin_nontemporal_store(v, row);
+    __builtin_nontemporal_store(v, row + stride);
+    __builtin_nontemporal_store(v, row + 2 * stride);
+    __builtin_nontemporal_store(v, row + 3 * stride);
+  }
+  for (; i < cnt; ++i, row += stride) __builtin_nontemporal_store(v, row);
+}
+
+__device__ inline uint32_t popc64(uint64_t x) { return (uint32_t)__popcll(x); }
+
 struct Segment {
   uint32_t c0, c1;
 };
-__device__ inline Segment my_segment(uint32_t nchunks, uint32_t nwaves, uint32_t wave) {
-  const uint32_t per = (nchunks + nwaves - 1) / nwaves;
-  const uint32_t c0 = min(nchunks, wave * per);
-  return {c0, min(nchunks, c0 + per)};
+// Wave w owns chunks [floor(w C / W), floor((w+1) C / W)): every wave gets floor or ceil
+// of C / W chunks. seg_of_chunk is the inverse.
+__host__ __device__ inline Segment my_segment(uint32_t nchunks, uint32_t nwaves, uint32_t wave) {
+  return {(uint32_t)((uint64_t)wave * nchunks / nwaves),
+          (uint32_t)((uint64_t)(wave + 1) * nchunks / nwaves)};
+}
+__host__ __device__ inline uint32_t seg_of_chunk(uint32_t c, uint32_t nchunks, uint32_t nwaves) {
+  return (uint32_t)(((uint64_t)(c + 1) * nwaves - 1) / nchunks);
+}
+
+__device__ inline uint32_t chunk_start(const uint32_t* __restrict__ gstart,
+                                       const uint32_t* __restrict__ chunk_g, uint32_t c) {
+  return sload(gstart + sload(chunk_g + c));
 }
 
 // ---------------------------------------------------------------------------------
 // A pass
 // ---------------------------------------------------------------------------------
-// Every load in this loop is scalar (codes, posB, flags: s_load) or LDS (masks), so
-// the only vector-memory instructions are the TB stores: nothing ever waits on vmcnt
-// (CDNA4 counts loads and stores in one in-order vmcnt; a vector load consumed after
-// outstanding stores would wait for all of them).
-template <bool LDS, bool FULL, typename TBT>
-__global__ __launch_bounds__(ENG_THREADS) void k_rankA(
+template <bool LDS, bool FULL, typename TBT, bool BIGT>
+__global__ __launch_bounds__(ENG_THREADS, 2) void k_rankA(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
-    const uint64_t* __restrict__ gmask, int64_t n, const uint32_t* __restrict__ posB_byA,
-    TBT* __restrict__ TB, int lw, uint32_t* __restrict__ lpA, uint32_t* __restrict__ seg_tot,
-    uint64_t* __restrict__ seg_part) {
+    const uint64_t* __restrict__ gmask, int64_t n, TBT* __restrict__ TB, int lw,
+    uint32_t* __restrict__ lpA, uint32_t* __restrict__ seg_tot, uint64_t* __restrict__ seg_part,
+    uint32_t nseg) {
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
   const int lane = threadIdx.x & 63;
   const bool active = FULL || lane < lw;
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
   const uint32_t wave = wave_uniform(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
-  const Segment sg = my_segment(nchunks, gridDim.x * WAVES_PER_WG, wave);
-  TBT* tb_lane = TB + lane;
+  const Segment sg = my_segment(nchunks, nseg, wave);
 
-  // chunk sums of k y~, k y~^2: 64-bit while chunk spans fit 16-bit ranks, else 128-bit
-  using Acc = std::conditional_t<sizeof(TBT) == 2, uint64_t, u128>;
-  uint32_t csl = 0;  // included count since the segment start
-  u128 seg_k = 0, seg_ky = 0, seg_ky2 = 0;  // sums over the segment of k, k y', k y'^2
-  for (uint32_t c = sg.c0; c < sg.c1; ++c) {
-    lpA[(size_t)c * LANES + lane] = csl;
-    const uint32_t p0 = sload(gstart + sload(chunk_g + c)), p1 = sload(gstart + sload(chunk_g + c + 1));
-    uint32_t cl = 0, k = 0, gs = p0;     // chunk-relative count, open group's count/start
-    Acc ky = 0, ky2 = 0;
-    auto close_group = [&](uint32_t ge) {
-      const uint32_t y = 2u * cl + k + 1u;  // chunk-relative doubled midrank
-      if (active) {
-        const TBT v = (TBT)y;
-        for (uint32_t q = gs; q < ge; ++q) tb_lane[(size_t)sload(posB_byA + q) * stride] = v;
-      }
-      const uint64_t t = (uint64_t)k * y;
-      ky += t;
-      ky2 += (Acc)t * y;
-      cl += k;
-      k = 0;
-      gs = ge;
-    };
-    uint32_t p = p0;
-    for (; p < p1; p += 32) {
-      const uint32_t nb = min(32u, p1 - p);
-      const uint32_t f = (uint32_t)((((uint64_t)sload(gflag + (p >> 5) + 1) << 32) |
-                                      sload(gflag + (p >> 5))) >> (p & 31));
-#pragma unroll 8
-      for (uint32_t t = 0; t < nb; ++t) {
-        if (((f >> t) & 1u) && p + t != gs) close_group(p + t);
-        const uint32_t code = sload(codes + p + t);
-        const uint64_t both = m[code >> 16] & m[code & 0xffffu];
-        k += (uint32_t)(both >> lane) & 1u;
-      }
+  uint64_t tie = 0;  // sum over groups of k^3 - k (k < 2^16)
+  u128 tie_big = 0;  //   (k >= 2^16)
+  uint32_t cw = 0;   // included count before the window (segment-relative)
+  if (sg.c0 < sg.c1) {
+    const uint32_t P0 = chunk_start(gstart, chunk_g, sg.c0);
+    const uint32_t P1 = chunk_start(gstart, chunk_g, sg.c1);
+    uint32_t cn = sg.c0;  // next chunk whose start is not yet recorded
+    uint32_t pn = P0;
+    uint32_t lp = 0;      // count at the current chunk's start
+    while (cn < sg.c1 && pn == P0) {
+      lpA[(size_t)cn * LANES + lane] = 0;
+      ++cn;
+      pn = cn < sg.c1 ? chunk_start(gstart, chunk_g, cn) : P1;
     }
-    close_group(p1);  // chunks end on a group boundary
-    // fold the chunk into the segment sums with its base lp = csl:  y' = y~ + 2 lp
-    const u128 lp = csl, K = cl;
-    seg_k += K;
-    seg_ky += (u128)ky + 2 * lp * K;
-    seg_ky2 += (u128)ky2 + 4 * lp * (u128)ky + 4 * lp * lp * K;
-    csl += cl;
+    uint32_t gs = P0, cgs = 0;  // open group start and the count before it
+    // close the open group [gs, xe) given ce = included count before xe
+    auto close = [&](uint32_t xe, uint32_t ce) {
+      tie_add<BIGT>(tie, tie_big, ce - cgs);
+      if (active) store_rows<FULL, TBT>(TB, stride, gs, xe - gs, lane, (TBT)(cgs + ce + 1u - 2u * lp));
+      gs = xe;
+      cgs = ce;
+      while (cn < sg.c1 && pn == xe) {  // chunk boundaries are group starts
+        lpA[(size_t)cn * LANES + lane] = ce;
+        lp = ce;
+        ++cn;
+        pn = cn < sg.c1 ? chunk_start(gstart, chunk_g, cn) : P1;
+      }
+    };
+    uint32_t w0 = P0 & ~63u;
+    // next window's codes (vector, lane j = pair w0 + j) and flags (scalar), one ahead
+    uint32_t cd = (w0 + lane >= P0 && w0 + lane < P1) ? codes[w0 + lane] : 0u;
+    uint32_t f0 = sload(gflag + (w0 >> 5)), f1 = sload(gflag + (w0 >> 5) + 1);
+    for (; w0 < P1; w0 += 64) {
+      const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+      uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
+      asm volatile("" ::"v"(x) : "memory");
+      if (w0 + 64 < P1) {
+        const uint32_t q = w0 + 64 + lane;
+        cd = q < P1 ? codes[q] : 0u;
+        f0 = sload(gflag + ((w0 + 64) >> 5));
+        f1 = sload(gflag + ((w0 + 64) >> 5) + 1);
+      }
+      if (F == ~0ull) {  // every position starts a group: close the carried one, then
+        close(w0, cw);   // 63 singletons need only a running count
+        if (cn >= sg.c1 || pn > w0 + 63u) {
+          uint32_t t = 2u * (cw - lp) + 1u;
+          TBT* row = TB + (size_t)w0 * stride + lane;
+#pragma unroll
+          for (int j = 0; j < 63; ++j) {
+            const uint32_t bit = (uint32_t)(x >> j) & 1u;
+            const uint32_t v = t + bit;
+            if (active) __builtin_nontemporal_store((TBT)v, row + (size_t)j * stride);
+            t = v + bit;
+          }
+          gs = w0 + 63u;
+          cgs = cw + popc64(x & lowmask(63));
+          F = 0;
+        } else {
+          F &= ~1ull;
+        }
+      }
+      while (F) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(F);
+        F &= F - 1;
+        close(w0 + b, cw + popc64(x & lowmask(b)));
+      }
+      cw += popc64(x);
+    }
+    if ((P1 & 63u) == 0) close(P1, cw);  // a 64-aligned segment end is in no window
   }
-  seg_tot[(size_t)wave * LANES + lane] = csl;
-  uint64_t* o = seg_part + ((size_t)wave * LANES + lane) * 3;
-  o[0] = (uint64_t)seg_ky;  // sum k y' fits 64 bits for any segment of < 2^31 pairs
-  o[1] = (uint64_t)seg_ky2;
-  o[2] = (uint64_t)(seg_ky2 >> 64);
-  (void)seg_k;
+  const size_t o = (size_t)wave * LANES + lane, fs = (size_t)nseg * LANES;
+  const u128 t = tie_big + tie;
+  seg_tot[o] = cw;
+  seg_part[PA_TIEL * fs + o] = (uint64_t)t;
+  seg_part[PA_TIEH * fs + o] = (uint64_t)(t >> 64);
 }
 
-// Exclusive scan of per-segment totals (per lane), one block of 16 waves.
-__global__ __launch_bounds__(1024) void k_scan_seg(const uint32_t* __restrict__ tot,
-                                                  uint32_t nseg, uint32_t* __restrict__ pre,
-                                                  uint32_t* __restrict__ total) {
+// ---------------------------------------------------------------------------------
+// per-lane exclusive scan over segments: tot[nseg][64] -> pre[nseg][64], total[64]
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_lscan_reduce(const uint32_t* __restrict__ tot,
+                                                      uint32_t nseg, uint32_t* __restrict__ bsum) {
   __shared__ uint32_t part[16][LANES];
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
-  const uint32_t per = (nseg + 15) / 16;
-  const uint32_t s0 = min(nseg, v * per), s1 = min(nseg, s0 + per);
+  const uint32_t s0 = blockIdx.x * SCAN_SEGS + v * (SCAN_SEGS / 16);
   uint32_t s = 0;
-  for (uint32_t i = s0; i < s1; ++i) s += tot[(size_t)i * LANES + lane];
+#pragma unroll
+  for (int i = 0; i < SCAN_SEGS / 16; ++i)
+    if (s0 + i < nseg) s += tot[(size_t)(s0 + i) * LANES + lane];
   part[v][lane] = s;
   __syncthreads();
+  if (v == 0) {
+    uint32_t r = 0;
+    for (int u = 0; u < 16; ++u) r += part[u][lane];
+    bsum[(size_t)blockIdx.x * LANES + lane] = r;
+  }
+}
+
+__global__ void k_lscan_top(uint32_t* __restrict__ bsum, uint32_t nblk, uint32_t* __restrict__ total) {
+  const int lane = threadIdx.x;
   uint32_t run = 0;
-  for (int u = 0; u < v; ++u) run += part[u][lane];
-  for (uint32_t i = s0; i < s1; ++i) {
-    const uint32_t t = tot[(size_t)i * LANES + lane];
-    pre[(size_t)i * LANES + lane] = run;
+  for (uint32_t b = 0; b < nblk; ++b) {
+    const uint32_t t = bsum[(size_t)b * LANES + lane];
+    bsum[(size_t)b * LANES + lane] = run;
     run += t;
   }
-  if (v == 15 && total) total[lane] = run;
+  if (total) total[lane] = run;
+}
+
+__global__ __launch_bounds__(1024) void k_lscan_down(const uint32_t* __restrict__ tot,
+                                                    uint32_t nseg, const uint32_t* __restrict__ bsum,
+                                                    uint32_t* __restrict__ pre) {
+  __shared__ uint32_t part[16][LANES];
+  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  constexpr int PER = SCAN_SEGS / 16;
+  const uint32_t s0 = blockIdx.x * SCAN_SEGS + v * PER;
+  uint32_t t[PER];
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    t[i] = s0 + i < nseg ? tot[(size_t)(s0 + i) * LANES + lane] : 0u;
+    s += t[i];
+  }
+  part[v][lane] = s;
+  __syncthreads();
+  uint32_t run = bsum[(size_t)blockIdx.x * LANES + lane];
+  for (int u = 0; u < v; ++u) run += part[u][lane];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    if (s0 + i < nseg) pre[(size_t)(s0 + i) * LANES + lane] = run;
+    run += t[i];
+  }
+}
+
+static int lane_scan(const uint32_t* tot, uint32_t nseg, uint32_t* bsum, uint32_t* pre,
+                     uint32_t* total, hipStream_t st) {
+  const uint32_t nb = scan_blocks(nseg);
+  k_lscan_reduce<<<nb, 1024, 0, st>>>(tot, nseg, bsum);
+  VR_CHECK_LAUNCH();
+  k_lscan_top<<<1, LANES, 0, st>>>(bsum, nb, total);
+  VR_CHECK_LAUNCH();
+  k_lscan_down<<<nb, 1024, 0, st>>>(tot, nseg, bsum, pre);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
 }
 
 __global__ void k_add_base(const uint32_t* __restrict__ lpA, const uint32_t* __restrict__ segpre,
@@ -288,100 +452,100 @@ __global__ void k_add_base(const uint32_t* __restrict__ lpA, const uint32_t* __r
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)nchunks * LANES) return;
   const uint32_t c = (uint32_t)(i / LANES), lane = (uint32_t)(i % LANES);
-  const uint32_t per = (nchunks + nwaves - 1) / nwaves;
-  baseA[i] = segpre[(size_t)(c / per) * LANES + lane] + lpA[i];
+  baseA[i] = segpre[(size_t)seg_of_chunk(c, nchunks, nwaves) * LANES + lane] + lpA[i];
 }
 
 // ---------------------------------------------------------------------------------
 // B pass
 // ---------------------------------------------------------------------------------
-// Loads only (no stores in the loop): 16 TB rows + 16 baseA rows + one lane-parallel
-// code / chunk load per 16 pairs. Per-group sums are u64 and chunk-local; each chunk is
-// folded into the u128 segment sums once.
-template <bool LDS, bool FULL, typename TBT, bool WIDEB>
-__global__ __launch_bounds__(ENG_THREADS) void k_rankB(
+// Loads only. Per window three coalesced rows (codes, posA, chunkA) fetched one window
+// ahead; per pair its TB row (HBM, random) and A-chunk base row (L2-resident), issued 16
+// pairs at a time.
+constexpr int BB = 8;  // pairs per gather batch
+
+template <bool LDS, bool FULL, typename TBT, bool BIGT>
+__global__ __launch_bounds__(ENG_THREADS, 2) void k_rankB(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
     const uint64_t* __restrict__ gmask, int64_t n, const TBT* __restrict__ TB, int lw,
-    const uint32_t* __restrict__ chunkA_byB, const uint32_t* __restrict__ baseA,
-    uint32_t* __restrict__ seg_tot, uint64_t* __restrict__ seg_part) {
+    const uint32_t* __restrict__ posA_byB, const uint32_t* __restrict__ chunkA_byB,
+    const uint32_t* __restrict__ baseA, uint32_t* __restrict__ seg_tot,
+    uint64_t* __restrict__ seg_part, uint32_t nseg) {
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
   const int lane = threadIdx.x & 63;
-  const uint32_t sub = lane & (U - 1);
   const bool active = FULL || lane < lw;
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
   const uint32_t wave = wave_uniform(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
-  const Segment sg = my_segment(nchunks, gridDim.x * WAVES_PER_WG, wave);
+  const Segment sg = my_segment(nchunks, nseg, wave);
   const TBT* tb_lane = TB + lane;
   const uint32_t* base_lane = baseA + lane;
 
-  // chunk sums: 64-bit unless B's chunks can span > 32k positions or ranks exceed 2^32/2^16
-  using Acc = std::conditional_t<WIDEB, u128, uint64_t>;
-  uint32_t csl = 0;
-  u128 acc = 0, St = 0, ny = 0, ny2 = 0;  // segment sums (B side relative to segment start)
-  for (uint32_t c = sg.c0; c < sg.c1; ++c) {
-    const uint32_t p0 = gstart[chunk_g[c]], p1 = gstart[chunk_g[c + 1]];
-    uint32_t cl = 0, k = 0;
-    uint64_t S = 0;
-    Acc cacc = 0, cSt = 0, cny = 0, cny2 = 0;
-    auto close_group = [&]() {
-      const uint32_t y = 2u * cl + k + 1u;  // chunk-relative doubled B midrank
-      cacc += (Acc)S * y;
-      cSt += S;
-      const uint64_t t = (uint64_t)k * y;
-      cny += t;
-      cny2 += (Acc)t * y;
-      cl += k;
-      k = 0;
+  u128 acc = 0;       // sum over B groups of S y'_B
+  uint64_t St = 0;    // sum of S (= sum of included yA)
+  uint64_t tie = 0;   // sum of k^3 - k
+  u128 tie_big = 0;
+  uint32_t cw = 0;
+  if (sg.c0 < sg.c1) {
+    const uint32_t P0 = chunk_start(gstart, chunk_g, sg.c0);
+    const uint32_t P1 = chunk_start(gstart, chunk_g, sg.c1);
+    uint32_t cgs = 0;
+    uint64_t S = 0;  // sum of included yA (absolute doubled A midranks) in the open group
+    auto close = [&](uint32_t ce) {
+      const uint32_t y = cgs + ce + 1u;
+      acc += (u128)S * y;
+      St += S;
+      tie_add<BIGT>(tie, tie_big, ce - cgs);
       S = 0;
+      cgs = ce;
     };
-    auto block = [&](uint32_t p, uint32_t nb, auto full_tag) {
-      constexpr bool FB = decltype(full_tag)::value;
-      const uint32_t f = flags16(gflag, p);
-      const uint32_t ca = (FB || sub < nb) ? chunkA_byB[p + sub] : 0u;
-      const TBT* row = tb_lane + (size_t)p * stride;
-      uint32_t ya[U];
+    uint32_t w0 = P0 & ~63u;
+    auto fetch = [&](uint32_t w, uint32_t& pa, uint32_t& ca, uint32_t& cd, uint32_t& f0,
+                     uint32_t& f1) {
+      const uint32_t pos = w + (uint32_t)lane;
+      const bool valid = pos >= P0 && pos < P1;
+      pa = valid ? posA_byB[pos] : 0u;
+      ca = valid ? chunkA_byB[pos] : 0u;
+      cd = valid ? codes[pos] : 0u;
+      f0 = sload(gflag + (w >> 5));
+      f1 = sload(gflag + (w >> 5) + 1);
+    };
+    uint32_t pa, ca, cd, f0, f1;
+    fetch(w0, pa, ca, cd, f0, f1);
+    for (; w0 < P1; w0 += 64) {
+      const uint32_t pa_c = pa, ca_c = ca;
+      const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+      const uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
+      if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
 #pragma unroll
-      for (int t = 0; t < U; ++t) {
-        if (active && (FB || (uint32_t)t < nb)) {
-          const uint32_t cat = readlane_u32(ca, t);
-          ya[t] = 2u * base_lane[(size_t)cat * LANES] + (uint32_t)row[(size_t)t * stride];
-        } else {
-          ya[t] = 0u;
+      for (int h = 0; h < 64 / BB; ++h) {
+        uint32_t ya[BB];
+#pragma unroll
+        for (int q = 0; q < BB; ++q) {
+          const uint32_t j = h * BB + q;
+          const uint32_t paj = readlane_u32(pa_c, j), caj = readlane_u32(ca_c, j);
+          ya[q] = active ? 2u * base_lane[(size_t)caj * LANES] + (uint32_t)tb_lane[(size_t)paj * stride]
+                         : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < BB; ++q) {
+          const uint32_t j = h * BB + q;
+          if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
+          S += ((x >> j) & 1ull) ? (uint64_t)ya[q] : 0ull;
         }
       }
-      const uint64_t both = block_masks(m, codes, p, nb, lane);
-#pragma unroll
-      for (int t = 0; t < U; ++t) {
-        if (FB || (uint32_t)t < nb) {
-          if ((f >> t) & 1u) close_group();  // empty groups contribute nothing
-          const uint32_t inc = incl(both, t, lane);
-          S += inc ? (uint64_t)ya[t] : 0ull;
-          k += inc;
-        }
-      }
-    };
-    uint32_t p = p0;
-    for (; p + U <= p1; p += U) block(p, (uint32_t)U, std::true_type{});
-    if (p < p1) block(p, p1 - p, std::false_type{});
-    close_group();
-    // fold: y'_B = y~ + 2 lp with lp = csl (segment-relative)
-    const u128 lp = csl, K = cl;
-    acc += (u128)cacc + 2 * lp * (u128)cSt;
-    St += cSt;
-    ny += (u128)cny + 2 * lp * K;
-    ny2 += (u128)cny2 + 4 * lp * (u128)cny + 4 * lp * lp * K;
-    csl += cl;
+      cw += popc64(x);
+    }
+    if ((P1 & 63u) == 0) close(cw);  // a 64-aligned segment end is in no window
   }
-  seg_tot[(size_t)wave * LANES + lane] = csl;
-  uint64_t* o = seg_part + ((size_t)wave * LANES + lane) * 6;
-  o[0] = (uint64_t)acc;
-  o[1] = (uint64_t)(acc >> 64);
-  o[2] = (uint64_t)St;
-  o[3] = (uint64_t)ny;
-  o[4] = (uint64_t)ny2;
-  o[5] = (uint64_t)(ny2 >> 64);
+  const size_t o = (size_t)wave * LANES + lane, fs = (size_t)nseg * LANES;
+  const u128 tt = tie_big + tie;
+  seg_tot[o] = cw;
+  seg_part[PB_ACCL * fs + o] = (uint64_t)acc;
+  seg_part[PB_ACCH * fs + o] = (uint64_t)(acc >> 64);
+  seg_part[PB_ST * fs + o] = St;
+  seg_part[PB_TIEL * fs + o] = (uint64_t)tt;
+  seg_part[PB_TIEH * fs + o] = (uint64_t)(tt >> 64);
 }
 
 // ---------------------------------------------------------------------------------
@@ -394,57 +558,70 @@ __device__ inline double i128_to_f64(i128 x) {
   return neg ? -d : d;
 }
 
-__global__ __launch_bounds__(1024) void k_final(
-    const uint32_t* __restrict__ segA_tot, const uint64_t* __restrict__ segA_part,
-    const uint32_t* __restrict__ segA_pre, const uint32_t* __restrict__ segB_tot,
-    const uint64_t* __restrict__ segB_part, uint32_t nseg, const PlanHeader* __restrict__ hA,
-    const PlanHeader* __restrict__ hB, int nl, double* __restrict__ scores) {
-  __shared__ uint32_t cnt[16][LANES];
+__device__ inline u128 ld128(const uint64_t* p, size_t lo, size_t hi) {
+  return ((u128)p[hi] << 64) | p[lo];
+}
+
+// Per block of SCAN_SEGS segments, reduced in a fixed order:
+//   tA = sum (k^3 - k) over A groups,  tB = same over B groups,
+//   ab = sum yA yB = sum_seg (acc + 2 bB St)  (bB = B segment base)
+__global__ __launch_bounds__(1024) void k_final_part(
+    const uint64_t* __restrict__ segA_part, const uint64_t* __restrict__ segB_part,
+    const uint32_t* __restrict__ segB_pre, uint32_t nseg, uint64_t* __restrict__ fpart) {
   __shared__ u128 red[3][16][LANES];
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
-  const uint32_t per = (nseg + 15) / 16;
-  const uint32_t s0 = min(nseg, v * per), s1 = min(nseg, s0 + per);
-  uint32_t c = 0;
-  for (uint32_t s = s0; s < s1; ++s) c += segB_tot[(size_t)s * LANES + lane];
-  cnt[v][lane] = c;
-  __syncthreads();
-  u128 bB = 0;
-  for (int u = 0; u < v; ++u) bB += cnt[u][lane];
-  u128 a2 = 0, ab = 0, b2 = 0;
-  for (uint32_t s = s0; s < s1; ++s) {
-    const size_t i = (size_t)s * LANES + lane;
-    // A side: sum over groups of k (2 bA + y')^2
-    const u128 kA = segA_tot[i], bA = segA_pre[i];
-    const uint64_t* pa = segA_part + i * 3;
-    const u128 nyA = pa[0], ny2A = ((u128)pa[2] << 64) | pa[1];
-    a2 += 4 * bA * bA * kA + 4 * bA * nyA + ny2A;
-    // B side
-    const u128 kB = segB_tot[i];
-    const uint64_t* pb = segB_part + i * 6;
-    const u128 acc = ((u128)pb[1] << 64) | pb[0];
-    const u128 St = pb[2], nyB = pb[3], ny2B = ((u128)pb[5] << 64) | pb[4];
-    ab += acc + 2 * bB * St;
-    b2 += 4 * bB * bB * kB + 4 * bB * nyB + ny2B;
-    bB += kB;
+  constexpr int PER = SCAN_SEGS / 16;
+  const uint32_t s0 = blockIdx.x * SCAN_SEGS + v * PER;
+  const size_t fs = (size_t)nseg * LANES;
+  u128 tA = 0, ab = 0, tB = 0;
+  for (int i = 0; i < PER; ++i) {
+    if (s0 + i >= nseg) break;
+    const size_t o = (size_t)(s0 + i) * LANES + lane;
+    tA += ld128(segA_part, PA_TIEL * fs + o, PA_TIEH * fs + o);
+    tB += ld128(segB_part, PB_TIEL * fs + o, PB_TIEH * fs + o);
+    ab += ld128(segB_part, PB_ACCL * fs + o, PB_ACCH * fs + o) +
+          2 * (u128)segB_pre[o] * (u128)segB_part[PB_ST * fs + o];
   }
-  red[0][v][lane] = a2;
+  red[0][v][lane] = tA;
   red[1][v][lane] = ab;
-  red[2][v][lane] = b2;
+  red[2][v][lane] = tB;
   __syncthreads();
   if (v != 0) return;
-  uint32_t Mp32 = 0;
-  for (int u = 0; u < 16; ++u) Mp32 += cnt[u][lane];
   for (int u = 1; u < 16; ++u) {
-    a2 += red[0][u][lane];
+    tA += red[0][u][lane];
     ab += red[1][u][lane];
-    b2 += red[2][u][lane];
+    tB += red[2][u][lane];
+  }
+  uint64_t* f = fpart + (size_t)blockIdx.x * 6 * LANES + lane;
+  f[0 * LANES] = (uint64_t)tA;
+  f[1 * LANES] = (uint64_t)(tA >> 64);
+  f[2 * LANES] = (uint64_t)ab;
+  f[3 * LANES] = (uint64_t)(ab >> 64);
+  f[4 * LANES] = (uint64_t)tB;
+  f[5 * LANES] = (uint64_t)(tB >> 64);
+}
+
+// rho from exact integers. With M' included pairs and doubled midranks y:
+//   sum y = M'(M'+1),  mu = M'(M'+1)^2,
+//   sum k y^2 = 4 M'(M'+1)(2M'+1)/6 - sum_g (k^3 - k)/3   (untied squares minus tie spread)
+__global__ void k_final_top(const uint64_t* __restrict__ fpart, uint32_t nblk,
+                            const uint32_t* __restrict__ totA, const PlanHeader* __restrict__ hA,
+                            const PlanHeader* __restrict__ hB, int nl, double* __restrict__ scores) {
+  const int lane = threadIdx.x;
+  u128 tA = 0, ab = 0, tB = 0;
+  for (uint32_t b = 0; b < nblk; ++b) {
+    const uint64_t* f = fpart + (size_t)b * 6 * LANES + lane;
+    tA += ((u128)f[1 * LANES] << 64) | f[0 * LANES];
+    ab += ((u128)f[3 * LANES] << 64) | f[2 * LANES];
+    tB += ((u128)f[5 * LANES] << 64) | f[4 * LANES];
   }
   if (lane >= nl) return;
-  const u128 Mp = Mp32;
+  const u128 Mp = totA[lane];
   const u128 mu = Mp * (Mp + 1) * (Mp + 1);
+  const u128 sq = 4 * (Mp * (Mp + 1) * (2 * Mp + 1) / 6);
   const i128 num = (i128)ab - (i128)mu;
-  const i128 va = (i128)a2 - (i128)mu;
-  const i128 vb = (i128)b2 - (i128)mu;
+  const i128 va = (i128)(sq - tA / 3) - (i128)mu;
+  const i128 vb = (i128)(sq - tB / 3) - (i128)mu;
   double r;
   if (hA->has_nan || hB->has_nan || Mp < 2 || va <= 0 || vb <= 0) {
     r = __builtin_nan("");
@@ -463,55 +640,83 @@ __global__ void k_fill_nan(double* out, int64_t count) {
 // ---------------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------------
-template <bool LDS, bool FULL, typename TBT, bool WIDEB>
+template <bool LDS, bool FULL, typename TBT, bool BTA, bool BTB>
 static int set_lds_attr() {
   static bool done = false;
   if (LDS && !done) {
     const int mx = 160 * 1024;
-    VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_rankA<LDS, FULL, TBT>,
+    VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_rankA<LDS, FULL, TBT, BTA>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, mx));
-    VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_rankB<LDS, FULL, TBT, WIDEB>,
+    VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_rankB<LDS, FULL, TBT, BTB>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, mx));
     done = true;
   }
   return VR_OK;
 }
 
-template <bool LDS, bool FULL, typename TBT, bool WIDEB>
+template <bool LDS, bool FULL, typename TBT, bool BTA, bool BTB>
 static int run_pass(const PlanView& A, const PlanView& B, int64_t n, const EngineWs& E, int lw,
                     int nl, double* scores_out, const EngineCfg& cfg, hipStream_t st) {
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
-  VR_TRY((set_lds_attr<LDS, FULL, TBT, WIDEB>()));
+  const uint32_t nseg = (uint32_t)cfg.nwaves;
+  VR_TRY((set_lds_attr<LDS, FULL, TBT, BTA, BTB>()));
   TBT* TB = static_cast<TBT*>(E.TB);
-  k_rankA<LDS, FULL, TBT><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
-      A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, E.posB_byA, TB, lw, E.lpA,
-      E.segA_tot, E.segA_part);
+  k_rankA<LDS, FULL, TBT, BTA><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
+      A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, TB, lw, E.lpA, E.segA_tot,
+      E.segA_part, nseg);
   VR_CHECK_LAUNCH();
-  k_scan_seg<<<1, 1024, 0, st>>>(E.segA_tot, (uint32_t)cfg.nwaves, E.segA_pre, E.totA);
-  VR_CHECK_LAUNCH();
+  VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
   const size_t nb = ((size_t)nch * LANES + 255) / 256;
-  k_add_base<<<(unsigned)nb, 256, 0, st>>>(E.lpA, E.segA_pre, nch, (uint32_t)cfg.nwaves, E.baseA);
+  k_add_base<<<(unsigned)nb, 256, 0, st>>>(E.lpA, E.segA_pre, nch, nseg, E.baseA);
   VR_CHECK_LAUNCH();
-  k_rankB<LDS, FULL, TBT, WIDEB><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
-      B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, TB, lw, E.chunkA_byB, E.baseA,
-      E.segB_tot, E.segB_part);
+  k_rankB<LDS, FULL, TBT, BTB><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
+      B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, TB, lw, E.posA_byB, E.chunkA_byB,
+      E.baseA, E.segB_tot, E.segB_part, nseg);
   VR_CHECK_LAUNCH();
-  k_final<<<1, 1024, 0, st>>>(E.segA_tot, E.segA_part, E.segA_pre, E.segB_tot, E.segB_part,
-                              (uint32_t)cfg.nwaves, A.hdr, B.hdr, nl, scores_out);
+  VR_TRY(lane_scan(E.segB_tot, nseg, E.bsum, E.segB_pre, nullptr, st));
+  const uint32_t nsb = scan_blocks(nseg);
+  k_final_part<<<nsb, 1024, 0, st>>>(E.segA_part, E.segB_part, E.segB_pre, nseg, E.fpart);
+  VR_CHECK_LAUNCH();
+  k_final_top<<<1, LANES, 0, st>>>(E.fpart, nsb, E.totA, A.hdr, B.hdr, nl, scores_out);
   VR_CHECK_LAUNCH();
   return VR_OK;
 }
 
+// runtime plan properties -> kernel instantiation
+struct PassKind {
+  bool lds, full, narrow, bigA, bigB;
+};
+
+template <bool LDS, bool FULL, typename TBT, bool BTA>
+static int dispatch_btb(const PassKind& k, const PlanView& A, const PlanView& B, int64_t n,
+                        const EngineWs& E, int lw, int nl, double* out, const EngineCfg& cfg,
+                        hipStream_t st) {
+  return k.bigB ? run_pass<LDS, FULL, TBT, BTA, true>(A, B, n, E, lw, nl, out, cfg, st)
+                : run_pass<LDS, FULL, TBT, BTA, false>(A, B, n, E, lw, nl, out, cfg, st);
+}
+template <bool LDS, bool FULL, typename TBT>
+static int dispatch_bta(const PassKind& k, const PlanView& A, const PlanView& B, int64_t n,
+                        const EngineWs& E, int lw, int nl, double* out, const EngineCfg& cfg,
+                        hipStream_t st) {
+  return k.bigA ? dispatch_btb<LDS, FULL, TBT, true>(k, A, B, n, E, lw, nl, out, cfg, st)
+                : dispatch_btb<LDS, FULL, TBT, false>(k, A, B, n, E, lw, nl, out, cfg, st);
+}
 template <bool LDS, bool FULL>
-static int run_pass_tb(bool narrow, bool wideb, const PlanView& A, const PlanView& B, int64_t n,
+static int dispatch_tb(const PassKind& k, const PlanView& A, const PlanView& B, int64_t n,
                        const EngineWs& E, int lw, int nl, double* out, const EngineCfg& cfg,
                        hipStream_t st) {
-  if (narrow)
-    return wideb ? run_pass<LDS, FULL, uint16_t, true>(A, B, n, E, lw, nl, out, cfg, st)
-                 : run_pass<LDS, FULL, uint16_t, false>(A, B, n, E, lw, nl, out, cfg, st);
-  return wideb ? run_pass<LDS, FULL, uint32_t, true>(A, B, n, E, lw, nl, out, cfg, st)
-               : run_pass<LDS, FULL, uint32_t, false>(A, B, n, E, lw, nl, out, cfg, st);
+  return k.narrow ? dispatch_bta<LDS, FULL, uint16_t>(k, A, B, n, E, lw, nl, out, cfg, st)
+                  : dispatch_bta<LDS, FULL, uint32_t>(k, A, B, n, E, lw, nl, out, cfg, st);
+}
+static int dispatch_pass(const PassKind& k, const PlanView& A, const PlanView& B, int64_t n,
+                         const EngineWs& E, int lw, int nl, double* out, const EngineCfg& cfg,
+                         hipStream_t st) {
+  if (k.lds)
+    return k.full ? dispatch_tb<true, true>(k, A, B, n, E, lw, nl, out, cfg, st)
+                  : dispatch_tb<true, false>(k, A, B, n, E, lw, nl, out, cfg, st);
+  return k.full ? dispatch_tb<false, true>(k, A, B, n, E, lw, nl, out, cfg, st)
+                : dispatch_tb<false, false>(k, A, B, n, E, lw, nl, out, cfg, st);
 }
 
 // Scores for `total` subsets (full set first if full_first), 64 per pass.
@@ -526,16 +731,20 @@ static int run_engine(const PlanView& A, const PlanView& B, int64_t n, const int
     VR_CHECK_LAUNCH();
     return VR_OK;
   }
-  // u16 chunk-relative ranks need every chunk span (< L + largest tie group) <= 32767;
-  // B's 64-bit chunk sums need the same of B and absolute ranks (2M+1) below 2^33
+  // u16 chunk-relative ranks y~ <= 2 span + 1 need every chunk span (< L + largest tie
+  // group of A) <= 32767; 64-bit tie sums need every group below 2^16
   PlanHeader h[2];
   VR_CHECK_HIP(hipMemcpyAsync(&h[0], A.hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
   VR_CHECK_HIP(hipMemcpyAsync(&h[1], B.hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
   VR_CHECK_HIP(hipStreamSynchronize(st));
-  const bool narrow = (uint64_t)PLAN_L + h[0].max_group <= 32767u;
-  const bool wideb = (uint64_t)PLAN_L + h[1].max_group > 32767u || M > (int64_t)1 << 30;
-  k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(A.codes, B.codes, M, n, B.pos_of_pair,
-                                                     A.chunk_of_pair, E.posB_byA, E.chunkA_byB);
+  PassKind kind;
+  kind.lds = cfg.use_lds;
+  kind.full = lw == LANES;
+  kind.narrow = (uint64_t)PLAN_L + h[0].max_group <= 32767u;
+  kind.bigA = h[0].max_group >= 65536u;
+  kind.bigB = h[1].max_group >= 65536u;
+  k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(B.codes, M, n, A.pos_of_pair,
+                                                     A.chunk_of_pair, E.posA_byB, E.chunkA_byB);
   VR_CHECK_LAUNCH();
   for (int64_t set0 = 0; set0 < total; set0 += lw) {
     const int nl = (int)std::min<int64_t>(lw, total - set0);
@@ -550,18 +759,7 @@ static int run_engine(const PlanView& A, const PlanView& B, int64_t n, const int
       k_masks_sets<<<grid, 256, 0, st>>>(idx, k, set0, nl, full_first, E.masks);
       VR_CHECK_LAUNCH();
     }
-    double* out = scores + set0;
-    if (cfg.use_lds) {
-      if (lw == LANES)
-        VR_TRY((run_pass_tb<true, true>(narrow, wideb, A, B, n, E, lw, nl, out, cfg, st)));
-      else
-        VR_TRY((run_pass_tb<true, false>(narrow, wideb, A, B, n, E, lw, nl, out, cfg, st)));
-    } else {
-      if (lw == LANES)
-        VR_TRY((run_pass_tb<false, true>(narrow, wideb, A, B, n, E, lw, nl, out, cfg, st)));
-      else
-        VR_TRY((run_pass_tb<false, false>(narrow, wideb, A, B, n, E, lw, nl, out, cfg, st)));
-    }
+    VR_TRY(dispatch_pass(kind, A, B, n, E, lw, nl, scores + set0, cfg, st));
   }
   return VR_OK;
 }
