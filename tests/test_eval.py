@@ -1,0 +1,96 @@
+"""`--mode eval` drop-in (evals.eval / run CLI) on the synthetic NSD-shaped source.
+
+CPU: CLI argument handling, config validation, loader ordering (string order for phase
+1, int order for shared test IDs, as neural.py:170/:474).
+GPU: eval() end to end at small size; the phase-2 point estimate and bootstrap are then
+re-derived with the CPU oracle from the same exact activations (|d rho| < 1e-4: the GPU
+and numpy RDMs differ in the last fp32 bits, which can move individual ranks)."""
+import numpy as np
+import pytest
+import torch
+
+from visreps_amd import utils
+from visreps_amd.run import main
+
+
+def _cfg(**over):
+    items = ["synthetic.n_test=96", "synthetic.n_train=160", "n_select=80", "n_bootstrap=20",
+             "region=[V1,hV4]", "subject_idx=[0]", "batchsize=64"]
+    items += [f"{k}={v}" for k, v in over.items()]
+    cfg = utils.load_config("configs/eval/base.json", items + ["mode=eval"])
+    return utils.validate_config(cfg)
+
+
+def test_cli_train_mode_refused(capsys):
+    assert main(["--mode", "train"]) == 2
+    assert "out of scope" in capsys.readouterr().err
+
+
+def test_config_synthetic_defaults():
+    cfg = _cfg()
+    assert cfg.neural_dataset == "synthetic" and cfg.random_init is True
+    assert cfg.region == ["V1", "hV4"] and cfg.subject_idx == [0]
+    assert cfg.synthetic["n_test"] == 96
+
+
+def test_config_rejects_bad_compare_method():
+    with pytest.raises(AssertionError):
+        _cfg(compare_method="cosine")
+
+
+def test_loader_orders():
+    from visreps_amd.dataloaders.neural import StimulusLoader, SyntheticStimuli
+
+    st = SyntheticStimuli({str(i): i for i in range(12)}, 1, "cpu")
+    ids = [k for _, ks in StimulusLoader(st, 5) for k in ks]
+    assert ids == sorted(ids, key=str) and ids[:4] == ["0", "1", "10", "11"]
+    imgs, _ = next(iter(StimulusLoader(st, 5)))
+    assert imgs.shape == (5, 3, 224, 224)
+
+
+def test_loader_images_match_generator():
+    from visreps_amd.dataloaders import synthetic as syn
+    from visreps_amd.dataloaders.neural import SyntheticStimuli
+
+    st = SyntheticStimuli({str(i): i for i in range(130)}, 3, "cpu")
+    got = st.images([129, 0, 64, 5])
+    ref = syn.make_images(range(0, 192), seed=3, device="cpu")
+    assert torch.equal(got, ref[[129, 0, 64, 5]])
+
+
+@pytest.mark.gpu
+def test_eval_end_to_end_matches_oracle(dev):
+    from oracle import rsa_oracle as O
+    from visreps_amd import evals
+    from visreps_amd.dataloaders.neural import _make_loader, load_synthetic_data
+    from visreps_amd.models import utils as mutils
+
+    cfg = _cfg()
+    df = evals.eval(cfg)
+    assert len(df) == 2
+    assert set(df.columns) >= {"layer", "compare_method", "score", "ci_low", "ci_high",
+                               "analysis", "layer_selection_scores", "bootstrap_scores"}
+    for _, row in df.iterrows():
+        sel = row["layer_selection_scores"]
+        assert len(sel) == 14
+        best = max(range(len(sel)), key=lambda i: (sel[i]["score"], -i))
+        assert sel[best]["layer"] == row["layer"]
+        assert len(row["bootstrap_scores"]) == 20 and row["ci_low"] <= row["ci_high"]
+
+    # oracle re-derivation of phase 2 from the same exact activations
+    cfg2 = _cfg()
+    cfg2 = evals._load_cfg(cfg2)
+    model = mutils.configure_feature_extractor(cfg2, mutils.load_model(cfg2, dev))
+    data = load_synthetic_data(cfg2, [0], ["V1", "hV4"])
+    test = data["stimuli"].subset(data["shared_test_ids"])
+    for i, region in enumerate(["V1", "hV4"]):
+        layer = df.iloc[i]["layer"]
+        acts, got_ids = mutils.extract_single_layer(model, _make_loader(test, None, 64, 0), dev, layer,
+                                                    data["shared_test_ids"])
+        assert got_ids == data["shared_test_ids"]
+        resp = np.stack([data["neural"][region][0]["test"][s] for s in data["shared_test_ids"]])
+        m_rdm = O.compute_rdm(acts.numpy())
+        n_rdm = O.compute_rdm(resp.astype(np.float32))
+        point, scores, lo, hi = O.bootstrap_rsa(m_rdm, n_rdm, n_bootstrap=20, seed=42)
+        assert abs(df.iloc[i]["score"] - point) < 1e-4
+        assert np.max(np.abs(np.asarray(df.iloc[i]["bootstrap_scores"]) - scores)) < 1e-4

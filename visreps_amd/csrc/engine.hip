@@ -287,7 +287,7 @@ __device__ inline uint32_t chunk_start(const uint32_t* __restrict__ gstart,
 // A pass
 // ---------------------------------------------------------------------------------
 template <bool LDS, bool FULL, typename TBT, bool BIGT>
-__global__ __launch_bounds__(ENG_THREADS, 2) void k_rankA(
+__global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
     const uint64_t* __restrict__ gmask, int64_t n, TBT* __restrict__ TB, int lw,
@@ -464,7 +464,7 @@ __global__ void k_add_base(const uint32_t* __restrict__ lpA, const uint32_t* __r
 constexpr int BB = 8;  // pairs per gather batch
 
 template <bool LDS, bool FULL, typename TBT, bool BIGT>
-__global__ __launch_bounds__(ENG_THREADS, 2) void k_rankB(
+__global__ __launch_bounds__(ENG_THREADS, 8) void k_rankB(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
     const uint64_t* __restrict__ gmask, int64_t n, const TBT* __restrict__ TB, int lw,
