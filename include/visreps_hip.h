@@ -63,6 +63,11 @@ int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float*
  * (i <= j) entries of tile t, for balancing ranges. */
 int64_t vr_rdm_tile_count(int64_t n);
 int64_t vr_rdm_tile_cost(int64_t n, int64_t tile);
+/* Rectangle of upper-triangle tile `tile`: rows [row0, row0+rows) x cols
+ * [col0, col0+cols), col0 >= row0 (a diagonal tile covers its upper half). Host only;
+ * for planners that place tile ranges on ranks (multi-GPU block-distributed RDM). */
+int vr_rdm_tile_rect(int64_t n, int64_t tile, int64_t* row0, int64_t* col0, int64_t* rows,
+                     int64_t* cols);
 size_t vr_rdm_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end);
 int vr_rdm_pearson_tiles_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
                              int64_t ldr, float correction, int64_t tile_begin,

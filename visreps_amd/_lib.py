@@ -45,6 +45,7 @@ _PROTOTYPES = {
     ),
     "vr_rdm_tile_count": (_c_i64, [_c_i64]),
     "vr_rdm_tile_cost": (_c_i64, [_c_i64, _c_i64]),
+    "vr_rdm_tile_rect": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "vr_rdm_tiles_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64]),
     "vr_rdm_pearson_tiles_f32": (
         ctypes.c_int,

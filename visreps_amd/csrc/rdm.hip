@@ -409,6 +409,22 @@ int64_t vr_rdm_tile_cost(int64_t n, int64_t tile) {
   return bi == bj ? h * (h + 1) / 2 : h * w;
 }
 
+int vr_rdm_tile_rect(int64_t n, int64_t tile, int64_t* row0, int64_t* col0, int64_t* rows,
+                     int64_t* cols) {
+  VR_REQUIRE(n > 0 && tile >= 0 && tile < gram_tiles(n), "vr_rdm_tile_rect: tile %lld of %lld",
+             (long long)tile, (long long)(n > 0 ? gram_tiles(n) : 0));
+  VR_REQUIRE(row0 && col0 && rows && cols, "vr_rdm_tile_rect: null output");
+  const int T = (int)((n + GT - 1) / GT);
+  int p = (int)tile, r = 0;
+  while (r + 1 < T && (int64_t)(r + 1) * T - (int64_t)(r + 1) * r / 2 <= p) ++r;
+  const int bi = r, bj = r + (p - (r * T - r * (r - 1) / 2));
+  *row0 = (int64_t)bi * GT;
+  *col0 = (int64_t)bj * GT;
+  *rows = std::min<int64_t>(GT, n - *row0);
+  *cols = std::min<int64_t>(GT, n - *col0);
+  return VR_OK;
+}
+
 int vr_row_stats_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* mean,
                      float* stdv, float correction, void* stream) {
   VR_REQUIRE(n >= 0 && d > 0 && ldx >= d, "vr_row_stats_f32: bad shape n=%lld d=%lld ldx=%lld",

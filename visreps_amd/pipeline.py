@@ -88,6 +88,15 @@ def tile_ranges(n: int, world: int) -> List[Tuple[int, int]]:
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
+def tile_rect(n: int, tile: int) -> Tuple[int, int, int, int]:
+    """(row0, col0, rows, cols) of upper-triangle tile `tile` (vr_rdm_tile_rect)."""
+    import ctypes
+
+    v = [ctypes.c_int64() for _ in range(4)]
+    check(lib().vr_rdm_tile_rect(n, tile, *[ctypes.byref(x) for x in v]), "vr_rdm_tile_rect")
+    return tuple(int(x.value) for x in v)
+
+
 def _tile_fraction(n: int, t0: int, t1: int) -> float:
     cum = _tile_cum_cost(n)
     return float((cum[t1] - cum[t0]) / cum[-1]) if cum[-1] > 0 else 0.0
@@ -129,24 +138,31 @@ def gather_rows(x_local: torch.Tensor, n: int, pg) -> torch.Tensor:
     buf = torch.zeros((per, d), dtype=x_local.dtype, device=x_local.device)
     buf[: x_local.size(0)] = x_local
     full = torch.empty((world * per, d), dtype=x_local.dtype, device=x_local.device)
-    dist.all_gather_into_tensor(full, buf, group=pg)
+    if dist.get_backend(pg) == "nccl":
+        dist.all_gather_into_tensor(full, buf, group=pg)
+    else:  # gloo (CPU tests of the orchestration)
+        dist.all_gather(list(full.chunk(world)), buf, group=pg)
     if all(s == per for s in sizes):
         return full
     return torch.cat([full[r * per: r * per + sizes[r]] for r in range(world)], 0)
 
 
 def distributed_rdm(x_local: torch.Tensor, n: int, pg=None,
-                    times: Optional[StepTimes] = None) -> torch.Tensor:
-    """Full (n, n) RDM on every rank from each rank's stimulus rows."""
+                    times: Optional[StepTimes] = None, tiles_into=None) -> torch.Tensor:
+    """Full (n, n) RDM on every rank from each rank's stimulus rows: all-gather the rows,
+    each rank writes its balanced tile range (and mirrors) into a zeroed matrix, and a
+    sum all-reduce assembles it (every entry has exactly one writer, so the sum is exact).
+    tiles_into(x, out, t0, t1, times=...) defaults to the HIP Gram kernel."""
+    tiles_into = tiles_into or rdm_tiles_into
     rank, world = _world(pg)
     x = gather_rows(x_local.float().contiguous(), n, pg)
     if world == 1:
         out = torch.empty((n, n), dtype=torch.float32, device=x.device)
-        rdm_tiles_into(x, out, 0, int(lib().vr_rdm_tile_count(n)), times=times)
+        tiles_into(x, out, 0, int(lib().vr_rdm_tile_count(n)), times=times)
         return out
     out = torch.zeros((n, n), dtype=torch.float32, device=x.device)
     t0, t1 = tile_ranges(n, world)[rank]
-    rdm_tiles_into(x, out, t0, t1, times=times)
+    tiles_into(x, out, t0, t1, times=times)
     del x
     dist.all_reduce(out, op=dist.ReduceOp.SUM, group=pg)
     return out
@@ -188,9 +204,13 @@ def summarize(scores: np.ndarray, bootstrap: bool) -> Dict:
 def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[str],
                   neural_rdms: Dict[str, torch.Tensor], n: int, *, n_boot: int = 1000,
                   seed: int = 42, pg=None, times: Optional[StepTimes] = None,
-                  keep_plans: bool = False) -> Dict[Tuple[str, str], Dict]:
+                  keep_plans: bool = False, plan_fn=None, unit_fn=None
+                  ) -> Dict[Tuple[str, str], Dict]:
     """Point + bootstrap Spearman RSA for every (point, region) unit; units round-robin
-    over ranks; returns the per-unit results on every rank."""
+    over ranks; returns the per-unit results on every rank. plan_fn / unit_fn default to
+    RankPlan / run_unit (the HIP engine)."""
+    plan_fn = plan_fn or R.RankPlan
+    unit_fn = unit_fn or run_unit
     rank, world = _world(pg)
     regions = list(neural_rdms)
     units = [(p, r) for p in points for r in regions]
@@ -210,12 +230,12 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
         if p not in by_point:
             del rdm
             continue
-        pm = R.RankPlan(rdm)
+        pm = plan_fn(rdm)
         del rdm
         for r in by_point[p]:
             if r not in nplans:
-                nplans[r] = R.RankPlan(neural_rdms[r])
-            local[(p, r)] = run_unit(pm, nplans[r], idx, times).cpu().numpy()
+                nplans[r] = plan_fn(neural_rdms[r])
+            local[(p, r)] = np.asarray(torch.as_tensor(unit_fn(pm, nplans[r], idx, times)).cpu())
     if world > 1:
         gathered: List[Dict] = [None] * world
         dist.all_gather_object(gathered, local, group=pg)
