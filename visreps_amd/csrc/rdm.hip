@@ -128,10 +128,22 @@ __device__ inline void tile_coords(int p, int T, int& bi, int& bj) {
   bj = r + (p - off(r));
 }
 
-// Loads this thread's 4 float4 of a 128 x 32 panel (rows row0.., k in [k, k+32)) and
-// centres them. Elements outside [0,n) x [k0,k1) are 0 after centring.
-__device__ inline void load_panel(const GramParams& P, int64_t row0, int64_t k, int64_t k1,
-                                  const float mrow[4], f32x4 out[4]) {
+// Loads this thread's 4 float4 of a 128 x 32 panel (rows row0.., k in [k, k+32)).
+// Interior stages (whole panel inside [0,n) x [k0,k1), 16-B rows) take the unguarded
+// path: four independent loads whose data is first touched after the stage's MFMAs, so
+// their latency hides under them. Edge stages zero-fill outside the matrix; centring is
+// applied at the LDS store (store_panel), where out-of-range elements stay exactly 0.
+__device__ inline void load_panel_fast(const GramParams& P, int64_t row0, int64_t k, f32x4 out[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int f = threadIdx.x + G_THREADS * s;
+    const int r = f >> 3, c4 = f & 7;
+    out[s] = *reinterpret_cast<const f32x4*>(P.X + (row0 + r) * P.ldx + k + c4 * 4);
+  }
+}
+
+__device__ inline void load_panel_edge(const GramParams& P, int64_t row0, int64_t k, int64_t k1,
+                                       f32x4 out[4]) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int f = threadIdx.x + G_THREADS * s;
@@ -141,29 +153,43 @@ __device__ inline void load_panel(const GramParams& P, int64_t row0, int64_t k, 
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (row < P.n) {
       const float* src = P.X + row * P.ldx + kk;
-      if (P.vec && kk + 3 < k1) {
-        v = *reinterpret_cast<const f32x4*>(src);
-        v.x -= mrow[s];
-        v.y -= mrow[s];
-        v.z -= mrow[s];
-        v.w -= mrow[s];
-      } else {
-        if (kk + 0 < k1) v.x = src[0] - mrow[s];
-        if (kk + 1 < k1) v.y = src[1] - mrow[s];
-        if (kk + 2 < k1) v.z = src[2] - mrow[s];
-        if (kk + 3 < k1) v.w = src[3] - mrow[s];
-      }
+      if (kk + 0 < k1) v.x = src[0];
+      if (kk + 1 < k1) v.y = src[1];
+      if (kk + 2 < k1) v.z = src[2];
+      if (kk + 3 < k1) v.w = src[3];
     }
     out[s] = v;
   }
 }
 
-__device__ inline void store_panel(float* lds, const f32x4 v[4]) {
+// Both panels of a stage behind one uniform branch (a diagonal tile's B rows are its A
+// rows: the duplicate loads hit cache and are not staged).
+__device__ inline void load_stage(const GramParams& P, bool fast, int64_t row0, int64_t col0,
+                                  int64_t k, int64_t k1, f32x4 a[4], f32x4 b[4]) {
+  if (fast) {
+    load_panel_fast(P, row0, k, a);
+    load_panel_fast(P, col0, k, b);
+  } else {
+    load_panel_edge(P, row0, k, k1, a);
+    load_panel_edge(P, col0, k, k1, b);
+  }
+}
+
+// Centre and stage a panel: element (r, k) <- x - mean_r inside the matrix, 0 outside.
+__device__ inline void store_panel(const GramParams& P, float* lds, int64_t row0, int64_t k,
+                                   int64_t k1, const float mrow[4], const f32x4 v[4]) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int f = threadIdx.x + G_THREADS * s;
     const int r = f >> 3, c4 = f & 7;
-    *reinterpret_cast<f32x4*>(lds + r * GLD + c4 * 4) = v[s];
+    const int64_t kk = k + c4 * 4;
+    const bool rin = row0 + r < P.n;
+    f32x4 w;
+    w.x = (rin && kk + 0 < k1) ? v[s].x - mrow[s] : 0.f;
+    w.y = (rin && kk + 1 < k1) ? v[s].y - mrow[s] : 0.f;
+    w.z = (rin && kk + 2 < k1) ? v[s].z - mrow[s] : 0.f;
+    w.w = (rin && kk + 3 < k1) ? v[s].w - mrow[s] : 0.f;
+    *reinterpret_cast<f32x4*>(lds + r * GLD + c4 * 4) = w;
   }
 }
 
@@ -211,12 +237,14 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
+  // a stage is "fast" when both panels lie inside the matrix (rows and k) with 16-B rows
+  const bool rows_in = P.vec && row0 + GT <= P.n && col0 + GT <= P.n;
+  auto fast_at = [&](int64_t k) { return rows_in && k + GK <= k1; };
   f32x4 ga[4], gb[4];
   if (nk > 0) {
-    load_panel(P, row0, k0, k1, mA, ga);
-    if (!diag) load_panel(P, col0, k0, k1, mB, gb);
-    store_panel(lds, ga);
-    if (!diag) store_panel(lds + G_STAGE, gb);
+    load_stage(P, fast_at(k0), row0, col0, k0, k1, ga, gb);
+    store_panel(P, lds, row0, k0, k1, mA, ga);
+    if (!diag) store_panel(P, lds + G_STAGE, col0, k0, k1, mB, gb);
   }
   __syncthreads();
 
@@ -225,11 +253,8 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
     const float* As = lds + cur * 2 * G_STAGE;
     const float* Bs = diag ? As : As + G_STAGE;
     const bool more = kt + 1 < nk;
-    if (more) {  // issue next panel loads early; they land under the MFMAs below
-      const int64_t kn = k0 + (int64_t)(kt + 1) * GK;
-      load_panel(P, row0, kn, k1, mA, ga);
-      if (!diag) load_panel(P, col0, kn, k1, mB, gb);
-    }
+    const int64_t kn = k0 + (int64_t)(kt + 1) * GK;
+    if (more) load_stage(P, fast_at(kn), row0, col0, kn, k1, ga, gb);  // lands under the MFMAs
     // lane half h owns k in [16h, 16h+16) of this stage (a consistent k permutation of
     // the MFMA's 2-deep k; the Gram sums over k so any fixed permutation is exact)
 #pragma unroll
@@ -252,8 +277,8 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
     }
     if (more) {
       float* nxt = lds + (cur ^ 1) * 2 * G_STAGE;
-      store_panel(nxt, ga);
-      if (!diag) store_panel(nxt + G_STAGE, gb);
+      store_panel(P, nxt, row0, kn, k1, mA, ga);
+      if (!diag) store_panel(P, nxt + G_STAGE, col0, kn, k1, mB, gb);
     }
     __syncthreads();
   }
