@@ -38,6 +38,59 @@ __global__ __launch_bounds__(1024) void store_u16_drain(uint16_t* tb, uint32_t r
   }
 }
 
+// same bytes with W-byte lanes: each instruction covers 64*W contiguous bytes
+template <typename T>
+__global__ __launch_bounds__(1024) void store_w(T* tb, uint32_t rows, uint32_t per_wave) {
+  const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  constexpr uint32_t RPI = sizeof(T) / 2;  // 128-byte rows per instruction
+  const uint32_t r0 = wave * per_wave;
+  for (uint32_t r = r0; r < r0 + per_wave && r < rows; r += RPI) {
+    T v;
+    __builtin_memset(&v, (int)(r + lane), sizeof(T));
+    __builtin_nontemporal_store(v, reinterpret_cast<T*>(reinterpret_cast<char*>(tb) + (size_t)r * 128) + lane);
+  }
+}
+
+// u16 rows with ALU work between stores (a dependent chain of `work` fmas per row)
+__global__ __launch_bounds__(1024) void store_u16_alu(uint16_t* tb, uint32_t rows, uint32_t per_wave,
+                                                      int work, float* sink) {
+  const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t r0 = wave * per_wave;
+  float a = lane * 0.5f;
+  for (uint32_t r = r0; r < r0 + per_wave && r < rows; ++r) {
+    for (int i = 0; i < work; ++i) a = __builtin_fmaf(a, 1.0001f, 0.5f);
+    __builtin_nontemporal_store((uint16_t)((uint32_t)a + r), tb + (size_t)r * 64 + lane);
+  }
+  if (a == 12345.f) sink[0] = a;
+}
+
+// wave-specialised: even waves store all the rows (twice the rows each), odd waves only
+// run the fma chain (work per row of the full workload)
+__global__ __launch_bounds__(1024) void store_split(uint16_t* tb, uint32_t rows, uint32_t per_wave2,
+                                                    int work, float* sink) {
+  const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t r0 = (wave >> 1) * per_wave2;
+  if ((wave & 1) == 0) {
+    for (uint32_t r = r0; r < r0 + per_wave2 && r < rows; ++r)
+      __builtin_nontemporal_store((uint16_t)(r + lane), tb + (size_t)r * 64 + lane);
+  } else {
+    float a = lane * 0.5f;
+    for (uint32_t r = r0; r < r0 + per_wave2 && r < rows; ++r)
+      for (int i = 0; i < work; ++i) a = __builtin_fmaf(a, 1.0001f, 0.5f);
+    if (a == 12345.f) sink[0] = a;
+  }
+}
+
+// fma chain only (no stores), same per-row work as store_u16_alu
+__global__ __launch_bounds__(1024) void alu_only(uint32_t rows, uint32_t per_wave, int work, float* sink) {
+  const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t r0 = wave * per_wave;
+  float a = lane * 0.5f;
+  for (uint32_t r = r0; r < r0 + per_wave && r < rows; ++r)
+    for (int i = 0; i < work; ++i) a = __builtin_fmaf(a, 1.0001f, 0.5f);
+  if (a == 12345.f) sink[0] = a;
+}
+
 __global__ __launch_bounds__(1024) void store_x4(uint4* tb, uint32_t rows, uint32_t per_wave) {
   const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t r0 = wave * per_wave;  // rows of 128 B; 8 rows per 1 KB instruction
@@ -83,7 +136,7 @@ int main() {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int grid : {256, 512, 1024}) {
+  for (int grid : {512}) {
     const uint32_t waves = grid * 16, per = (rows + waves - 1) / waves;
     CK(hipMalloc(&out, (size_t)waves * 64 * 4));
     auto run = [&](const char* name, auto launch) -> int {
@@ -105,9 +158,17 @@ int main() {
     run("u16_drain64", [&] { store_u16_drain<<<grid, 1024>>>(tb, rows, per, waves, 1); });
     run("u16_3/4+drain", [&] { store_u16_drain<<<grid, 1024>>>(tb, rows, per_act, act, 1); });
     run("store_x4", [&] { store_x4<<<grid, 1024>>>((uint4*)tb, rows, (per + 7) / 8 * 8); });
-    run("gather16", [&] { gather_u16<16><<<grid, 1024>>>(tb, perm, rows, per, out); });
-    run("gather32", [&] { gather_u16<32><<<grid, 1024>>>(tb, perm, rows, per, out); });
-    run("gather64", [&] { gather_u16<64><<<grid, 1024>>>(tb, perm, rows, per, out); });
+    run("nt_u16", [&] { store_w<uint16_t><<<grid, 1024>>>(tb, rows, per); });
+    run("nt_u32", [&] { store_w<uint32_t><<<grid, 1024>>>((uint32_t*)tb, rows, (per + 1) / 2 * 2); });
+    run("nt_u64", [&] { store_w<uint64_t><<<grid, 1024>>>((uint64_t*)tb, rows, (per + 3) / 4 * 4); });
+    for (int work : {4, 8})
+      run(work == 4 ? "u16+4fma" : "u16+8fma",
+          [&] { store_u16_alu<<<grid, 1024>>>(tb, rows, per, work, (float*)out); });
+    run("alu8_only", [&] { alu_only<<<grid, 1024>>>(rows, per, 8, (float*)out); });
+    run("split8", [&] { store_split<<<grid, 1024>>>(tb, rows, 2 * per, 16, (float*)out); });
+    if (0) run("gather16", [&] { gather_u16<16><<<grid, 1024>>>(tb, perm, rows, per, out); });
+    if (0) run("gather32", [&] { gather_u16<32><<<grid, 1024>>>(tb, perm, rows, per, out); });
+    if (0) run("gather64", [&] { gather_u16<64><<<grid, 1024>>>(tb, perm, rows, per, out); });
     CK(hipFree(out));
   }
   return 0;

@@ -463,6 +463,38 @@ __global__ void k_add_base(const uint32_t* __restrict__ lpA, const uint32_t* __r
 // pairs at a time.
 constexpr int BB = 8;  // pairs per gather batch
 
+// BB pairs' yA = 2 baseA[chunkA] + TB[posA] for this lane. The loads are issued in the
+// saddr form (wave-uniform 64-bit row address in SGPRs + 32-bit lane byte offset), which
+// the compiler does not select on its own here; their completion is an explicit
+// s_waitcnt tied to every result. This kernel issues no vector stores and all of the
+// compiler's own vector loads are older than these, so its waits stay conservative.
+template <typename TBT>
+__device__ inline void gather_batch(const TBT* __restrict__ TB, const uint32_t* __restrict__ baseA,
+                                    uint32_t stride, uint32_t pa, uint32_t ca, uint32_t j0,
+                                    uint32_t lane_bt, uint32_t lane_b4, uint32_t ya[BB]) {
+  uint32_t t[BB], b[BB];
+#pragma unroll
+  for (int q = 0; q < BB; ++q) {
+    const char* trow = reinterpret_cast<const char*>(TB) +
+                       (size_t)readlane_u32(pa, j0 + q) * (stride * sizeof(TBT));
+    const char* brow = reinterpret_cast<const char*>(baseA) + (size_t)readlane_u32(ca, j0 + q) * (LANES * 4);
+    if constexpr (sizeof(TBT) == 2)
+      asm volatile("global_load_ushort %0, %1, %2" : "=v"(t[q]) : "v"(lane_bt), "s"(trow) : "memory");
+    else
+      asm volatile("global_load_dword %0, %1, %2" : "=v"(t[q]) : "v"(lane_bt), "s"(trow) : "memory");
+    asm volatile("global_load_dword %0, %1, %2" : "=v"(b[q]) : "v"(lane_b4), "s"(brow) : "memory");
+  }
+  static_assert(BB == 8, "the wait below names 16 registers");
+  asm volatile("s_waitcnt vmcnt(0)"
+               : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+                 "+v"(t[7]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]),
+                 "+v"(b[6]), "+v"(b[7])
+               :
+               : "memory");
+#pragma unroll
+  for (int q = 0; q < BB; ++q) ya[q] = 2u * b[q] + t[q];
+}
+
 template <bool LDS, bool FULL, typename TBT, bool BIGT>
 __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankB(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
@@ -478,9 +510,6 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankB(
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
   const uint32_t wave = wave_uniform(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
   const Segment sg = my_segment(nchunks, nseg, wave);
-  const TBT* tb_lane = TB + lane;
-  const uint32_t* base_lane = baseA + lane;
-
   u128 acc = 0;       // sum over B groups of S y'_B
   uint64_t St = 0;    // sum of S (= sum of included yA)
   uint64_t tie = 0;   // sum of k^3 - k
@@ -514,18 +543,19 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankB(
     fetch(w0, pa, ca, cd, f0, f1);
     for (; w0 < P1; w0 += 64) {
       const uint32_t pa_c = pa, ca_c = ca;
+      uint32_t lane_b4, lane_bt;  // opaque per window, so the base + lane sum is not hoisted
+      asm("" : "=v"(lane_b4) : "0"((uint32_t)lane * 4u));
+      asm("" : "=v"(lane_bt) : "0"((uint32_t)lane * (uint32_t)sizeof(TBT)));
       const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
       const uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
       if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
 #pragma unroll
       for (int h = 0; h < 64 / BB; ++h) {
         uint32_t ya[BB];
+        gather_batch<TBT>(TB, baseA, stride, pa_c, ca_c, h * BB, lane_bt, lane_b4, ya);
+        if (!active) {
 #pragma unroll
-        for (int q = 0; q < BB; ++q) {
-          const uint32_t j = h * BB + q;
-          const uint32_t paj = readlane_u32(pa_c, j), caj = readlane_u32(ca_c, j);
-          ya[q] = active ? 2u * base_lane[(size_t)caj * LANES] + (uint32_t)tb_lane[(size_t)paj * stride]
-                         : 0u;
+          for (int q = 0; q < BB; ++q) ya[q] = 0u;
         }
 #pragma unroll
         for (int q = 0; q < BB; ++q) {

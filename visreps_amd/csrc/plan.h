@@ -9,7 +9,7 @@
 
 namespace vr {
 
-constexpr uint32_t PLAN_L = 4096;  // target pairs per chunk
+constexpr uint32_t PLAN_L = 2048;  // target pairs per chunk (sets the per-wave work grain)
 
 struct PlanHeader {
   int64_t n;
