@@ -138,6 +138,26 @@ int vr_bootstrap_spearman_f32(const float* A, const float* B, int64_t n, int64_t
                               void* stream);
 
 /* ------------------------------------------------------------------------------
+ * Kendall tau-a of two RDMs' upper triangles: replaces
+ * compute_rdm_correlation(rdm1, rdm2, correlation="Kendall") -> _kendall_tau_a
+ * (visreps/analysis/rsa.py:22-40,96-129): scipy.stats.kendalltau tau-b from exact
+ * discordant / tie counts, converted to tau-a = tau_b sqrt((n0-tx)(n0-ty)) / n0.
+ * out [dev] one double; NaN for n <= 1, NaN input or a constant triangle.
+ * -------------------------------------------------------------------------- */
+size_t vr_kendall_triu_workspace(int64_t n);
+int vr_kendall_triu_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out,
+                        void* ws, size_t ws_bytes, void* stream);
+
+/* Bootstrapped Kendall RSA on two rank plans: the bootstrap loop of evals.py:355-373 /
+ * rsa.py:233-261 with compare_method="kendall". Arguments as
+ * vr_bootstrap_spearman_plans; the workspace depends on the number of subsets:
+ * vr_bootstrap_kendall_workspace(n, n_sets) covers up to n_sets subsets plus the full set. */
+size_t vr_bootstrap_kendall_workspace(int64_t n, int64_t n_sets);
+int vr_bootstrap_kendall_plans(const void* planA, const void* planB, int64_t n,
+                               const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
+                               double* scores, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------
  * Phase-1 sparse random projection (extraction side).
  * Replaces torch.sparse.mm(P, flat.t()).t() (visreps/models/utils.py:334-336) with P the
  * CSR (k x D) components_ of sklearn SparseRandomProjection

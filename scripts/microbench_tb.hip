@@ -166,9 +166,9 @@ int main() {
           [&] { store_u16_alu<<<grid, 1024>>>(tb, rows, per, work, (float*)out); });
     run("alu8_only", [&] { alu_only<<<grid, 1024>>>(rows, per, 8, (float*)out); });
     run("split8", [&] { store_split<<<grid, 1024>>>(tb, rows, 2 * per, 16, (float*)out); });
-    if (0) run("gather16", [&] { gather_u16<16><<<grid, 1024>>>(tb, perm, rows, per, out); });
-    if (0) run("gather32", [&] { gather_u16<32><<<grid, 1024>>>(tb, perm, rows, per, out); });
-    if (0) run("gather64", [&] { gather_u16<64><<<grid, 1024>>>(tb, perm, rows, per, out); });
+    run("gather16", [&] { gather_u16<16><<<grid, 1024>>>(tb, perm, rows, per, out); });
+    run("gather32", [&] { gather_u16<32><<<grid, 1024>>>(tb, perm, rows, per, out); });
+    run("gather64", [&] { gather_u16<64><<<grid, 1024>>>(tb, perm, rows, per, out); });
     CK(hipFree(out));
   }
   return 0;

@@ -1,0 +1,134 @@
+"""Kendall tau-a comparison (rsa.py:22-40 `_kendall_tau_a`, compare_method="kendall") and its
+bootstrap on the HIP path vs the CPU oracle (scipy.stats.kendalltau tau-b converted to tau-a
+exactly as the reference does).
+
+Tolerances
+  * identical RDM inputs: |delta| <= 1e-12 — both sides evaluate scipy's tau-b formula and
+    the reference's tau-a conversion on the same exact integer counts in the same fp64
+    operation order (observed: bit-equal);
+  * each side building its own RDMs: |delta| < 1e-5 (north-star tolerance).
+Edge cases: n <= 3, NaN input, constant triangles, heavy ties in x, y and jointly, ties in
+one RDM only, -0.0 / +0.0, subsets of the bootstrap with the legacy RandomState stream.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import rsa_oracle as O
+from visreps_amd.analysis import rsa as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _sym(m):
+    m = np.triu(m.astype(np.float32), 1)
+    return (m + m.T).astype(np.float32)
+
+
+def _rdm(n, seed, levels=None):
+    m = np.random.RandomState(seed).rand(n, n).astype(np.float32)
+    if levels:
+        m = np.floor(m * levels).astype(np.float32) / levels
+    return _sym(m)
+
+
+def _close(got, ref, tol=1e-12):
+    if math.isnan(ref):
+        return math.isnan(got)
+    return abs(got - ref) <= tol
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 17, 64, 65, 130, 400])
+@pytest.mark.parametrize("la,lb", [(None, None), (7, None), (None, 5), (4, 6), (1000, 1000)])
+def test_kendall_point_vs_oracle(dev, n, la, lb):
+    a, b = _rdm(n, 10 + n, la), _rdm(n, 20 + n, lb)
+    got = R.compute_rdm_correlation(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev),
+                                    correlation="Kendall")
+    ref = O.compute_rdm_correlation(a, b, "Kendall")
+    assert _close(got, ref), (got, ref)
+
+
+def test_kendall_joint_ties_and_negative_zero(dev):
+    n = 90
+    rng = np.random.RandomState(3)
+    base = np.floor(rng.rand(n, n) * 5).astype(np.float32) / 5
+    a = _sym(base)
+    b = _sym(np.where(rng.rand(n, n) < 0.5, base, np.floor(rng.rand(n, n) * 3) / 3))
+    a[a == 0] = -0.0  # -0.0 ties with +0.0 (scipy compares with ==)
+    got = R.compute_rdm_correlation(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev),
+                                    correlation="Kendall")
+    assert _close(got, O.compute_rdm_correlation(a, b, "Kendall"))
+
+
+def test_kendall_nan_constant_and_tiny(dev):
+    a, b = _rdm(30, 1), _rdm(30, 2)
+    c = _sym(np.full((30, 30), 0.5, np.float32))
+    an = a.copy()
+    an[3, 7] = an[7, 3] = np.nan
+    for x, y in [(an, b), (c, b), (a, c)]:
+        got = R.compute_rdm_correlation(torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev),
+                                        correlation="Kendall")
+        assert math.isnan(got)
+    assert math.isnan(R.compute_rdm_correlation(torch.zeros(1, 1, device=dev), torch.zeros(1, 1, device=dev),
+                                                correlation="Kendall"))
+
+
+def test_kendall_identity_and_reversal(dev):
+    a = _rdm(50, 5)
+    t = torch.from_numpy(a).to(dev)
+    assert R.compute_rdm_correlation(t, t, correlation="Kendall") == 1.0
+    assert R.compute_rdm_correlation(t, -t, correlation="Kendall") == -1.0
+
+
+@pytest.mark.parametrize("n,nb,levels", [(10, 20, None), (64, 40, None), (100, 70, 9), (150, 65, None)])
+def test_kendall_bootstrap_matches_oracle(dev, n, nb, levels):
+    x = O.synthetic_features(n, [300, 200], seed=n)
+    m_rdm = O.compute_rdm(x[0])
+    n_rdm = O.compute_rdm(x[1])
+    if levels:
+        m_rdm = (np.floor(m_rdm * levels) / levels).astype(np.float32)
+    point, scores, lo, hi = R.bootstrap_rsa(torch.from_numpy(m_rdm).to(dev), torch.from_numpy(n_rdm).to(dev),
+                                            n_bootstrap=nb, seed=42, method="kendall")
+    rp, rs, rlo, rhi = O.bootstrap_rsa(m_rdm, n_rdm, n_bootstrap=nb, seed=42, method="Kendall")
+    assert _close(point, rp)
+    assert np.max(np.abs(scores - rs)) <= 1e-12
+    assert abs(lo - rlo) <= 1e-12 and abs(hi - rhi) <= 1e-12
+
+
+def test_kendall_bootstrap_end_to_end_tolerance(dev):
+    n = 200
+    feats = O.synthetic_features(n, [4096, 1000], seed=7, relu=[True, False], noise=3.0)
+    gm = R.compute_rdm(torch.from_numpy(feats[0]).to(dev))
+    gn = R.compute_rdm(torch.from_numpy(feats[1]).to(dev))
+    point, scores, lo, hi = R.bootstrap_rsa(gm, gn, n_bootstrap=30, seed=42, method="kendall")
+    rp, rs, rlo, rhi = O.bootstrap_rsa(O.compute_rdm(feats[0]), O.compute_rdm(feats[1]),
+                                       n_bootstrap=30, seed=42, method="Kendall")
+    assert abs(point - rp) < 1e-5
+    assert np.max(np.abs(scores - rs)) < 1e-5
+
+
+def test_compute_rsa_kendall_matches_oracle(dev):
+    from visreps_amd.analysis.alignment import AlignmentData
+
+    rng = np.random.RandomState(4)
+    n_train, n_test, v = 120, 40, 60
+    neural_train = rng.randn(n_train, v).astype(np.float32)
+    neural_test = rng.randn(n_test, v).astype(np.float32)
+    good_train = neural_train + 0.7 * rng.randn(n_train, v).astype(np.float32)
+    good_test = neural_test + 0.7 * rng.randn(n_test, v).astype(np.float32)
+    bad_train = rng.randn(n_train, v).astype(np.float32)
+    bad_test = rng.randn(n_test, v).astype(np.float32)
+    cfg = {"compare_method": "kendall"}
+    sel = AlignmentData({"good": torch.from_numpy(good_train), "bad": torch.from_numpy(bad_train)},
+                        torch.from_numpy(neural_train))
+    ev = AlignmentData({"good": torch.from_numpy(good_test), "bad": torch.from_numpy(bad_test)},
+                       torch.from_numpy(neural_test))
+    got = R.compute_rsa(cfg, sel, ev, n_select=80, bootstrap=True, n_bootstrap=25, seed=42)[0]
+    ref = O.compute_rsa(cfg, {"good": good_train, "bad": bad_train}, neural_train,
+                        {"good": good_test, "bad": bad_test}, neural_test,
+                        n_select=80, bootstrap=True, n_bootstrap=25, seed=42)[0]
+    assert got["layer"] == ref["layer"] == "good"
+    assert abs(got["score"] - ref["score"]) < 1e-5
+    assert np.max(np.abs(np.array(got["bootstrap_scores"]) - np.array(ref["bootstrap_scores"]))) < 1e-5

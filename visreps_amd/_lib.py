@@ -81,6 +81,16 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _vp, _c_sz, _vp],
     ),
+    "vr_kendall_triu_workspace": (_c_sz, [_c_i64]),
+    "vr_kendall_triu_f32": (
+        ctypes.c_int,
+        [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp],
+    ),
+    "vr_bootstrap_kendall_workspace": (_c_sz, [_c_i64, _c_i64]),
+    "vr_bootstrap_kendall_plans": (
+        ctypes.c_int,
+        [_vp, _vp, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _vp, _c_sz, _vp],
+    ),
     "vr_srp_workspace": (_c_sz, [_c_i64, _c_i64]),
     "vr_srp_csr_f32": (
         ctypes.c_int,

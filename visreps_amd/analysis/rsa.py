@@ -5,6 +5,7 @@ arithmetic runs in the HIP kernels of libvisreps_hip.so:
 
   compute_rdm             rsa.py:59-93    fp32 MFMA Gram + fused 1-clamp(corr) epilogue
   compute_rdm_correlation rsa.py:96-129   Spearman: sorted-triangle midrank engine
+                                          Kendall: tau-a by bitwise inversion counting
                                           Pearson: fp64 two-pass triangle reduction
   compute_rsa             rsa.py:132-281  layer selection + point + bootstrap on device
   bootstrap_rsa           evals.py:355-373 the inline NSD/TVSD bootstrap, batched
@@ -38,6 +39,7 @@ __all__ = [
     "bootstrap_rsa",
     "RankPlan",
     "bootstrap_spearman",
+    "bootstrap_kendall",
     "percentile",
     "_rank",
     "_concept_average_exact",
@@ -166,14 +168,7 @@ def bootstrap_spearman(
     if plan_a.n != plan_b.n or plan_a.device != plan_b.device:
         raise ValueError("rank plans must describe RDMs of the same size and device")
     dev, n = plan_a.device, plan_a.n
-    if idx is None:
-        idx_t = torch.empty((0, 0), dtype=torch.int32, device=dev)
-    else:
-        if isinstance(idx, np.ndarray) and not idx.flags.writeable:
-            idx = idx.copy()
-        idx_t = torch.as_tensor(idx).to(device=dev, dtype=torch.int32).contiguous()
-        if idx_t.ndim != 2:
-            raise ValueError("idx must be (n_sets, k)")
+    idx_t = _idx_tensor(idx, dev)
     n_sets, k = (int(idx_t.size(0)), int(idx_t.size(1))) if idx_t.numel() else (0, 0)
     total = n_sets + (1 if full_first else 0)
     scores = torch.empty(total, dtype=torch.float64, device=dev)
@@ -191,6 +186,52 @@ def bootstrap_spearman(
             "vr_bootstrap_spearman_plans",
         )
     return scores
+
+
+def _idx_tensor(idx, dev: torch.device) -> torch.Tensor:
+    if idx is None:
+        return torch.empty((0, 0), dtype=torch.int32, device=dev)
+    if isinstance(idx, np.ndarray) and not idx.flags.writeable:
+        idx = idx.copy()
+    idx_t = torch.as_tensor(idx).to(device=dev, dtype=torch.int32).contiguous()
+    if idx_t.ndim != 2:
+        raise ValueError("idx must be (n_sets, k)")
+    return idx_t
+
+
+def bootstrap_kendall(
+    plan_a: RankPlan,
+    plan_b: RankPlan,
+    idx: Optional[np.ndarray | torch.Tensor],
+    *,
+    full_first: bool = True,
+) -> torch.Tensor:
+    """Kendall tau-a (rsa.py:22-40) of triu(A[s][:, s]) vs triu(B[s][:, s]) for every subset s
+    (row of idx), preceded by the full set when full_first. float64 scores on the device."""
+    if plan_a.n != plan_b.n or plan_a.device != plan_b.device:
+        raise ValueError("rank plans must describe RDMs of the same size and device")
+    dev, n = plan_a.device, plan_a.n
+    idx_t = _idx_tensor(idx, dev)
+    n_sets, k = (int(idx_t.size(0)), int(idx_t.size(1))) if idx_t.numel() else (0, 0)
+    total = n_sets + (1 if full_first else 0)
+    scores = torch.empty(total, dtype=torch.float64, device=dev)
+    if total == 0:
+        return scores
+    L = lib()
+    ws = workspace.get(dev, L.vr_bootstrap_kendall_workspace(n, n_sets), "kendall")
+    with torch.cuda.device(dev):
+        check(
+            L.vr_bootstrap_kendall_plans(
+                _ptr(plan_a.buf), _ptr(plan_b.buf), n,
+                _ptr(idx_t) if idx_t.numel() else None, k, n_sets, int(full_first),
+                _ptr(scores), _ptr(ws), ws.numel(), stream_of(dev),
+            ),
+            "vr_bootstrap_kendall_plans",
+        )
+    return scores
+
+
+_ENGINES = {"spearman": bootstrap_spearman, "kendall": bootstrap_kendall}
 
 
 def percentile(scores: np.ndarray, q: float) -> float:
@@ -224,11 +265,6 @@ def compute_rdm_correlation(
     corr = correlation.lower()
     if corr not in _VALID_CMP:
         raise ValueError("correlation must be 'Pearson', 'Spearman', or 'Kendall'")
-    if corr == "kendall":
-        raise NotImplementedError(
-            "Kendall tau-a RDM comparison is not on the MI355X path yet "
-            "(SURVEY.md §8(f) rank 1); use compare_method='spearman'"
-        )
     dev = _device_for(rdm1, rdm2)
     a = _as_device_f32(rdm1, dev)
     b = _as_device_f32(rdm2, dev)
@@ -243,6 +279,13 @@ def compute_rdm_correlation(
                 L.vr_spearman_triu_f32(_ptr(a), _ptr(b), n, a.stride(0), _ptr(out),
                                        _ptr(ws), ws.numel(), stream_of(dev)),
                 "vr_spearman_triu_f32",
+            )
+        elif corr == "kendall":
+            ws = workspace.get(dev, L.vr_kendall_triu_workspace(n), "kendall_triu")
+            check(
+                L.vr_kendall_triu_f32(_ptr(a), _ptr(b), n, a.stride(0), _ptr(out),
+                                      _ptr(ws), ws.numel(), stream_of(dev)),
+                "vr_kendall_triu_f32",
             )
         else:
             ws = workspace.get(dev, L.vr_pearson_triu_workspace(n), "pearson")
@@ -268,17 +311,21 @@ def bootstrap_rsa(
     n_bootstrap: int = 1000,
     seed: int = 42,
     idx: Optional[np.ndarray] = None,
+    method: str = "spearman",
 ) -> Tuple[float, np.ndarray, float, float]:
-    """Point Spearman plus the reference's inline bootstrap: a fresh RandomState(seed),
-    n_bootstrap draws of choice(n, int(0.9 n), replace=False), Spearman of the two
-    sub-RDMs per draw, 2.5/97.5 linear percentiles. Returns
+    """Point estimate plus the reference's inline bootstrap: a fresh RandomState(seed),
+    n_bootstrap draws of choice(n, int(0.9 n), replace=False), Spearman (or Kendall tau-a)
+    of the two sub-RDMs per draw, 2.5/97.5 linear percentiles. Returns
     (point, scores[n_bootstrap], ci_low, ci_high)."""
+    engine = _ENGINES.get(method.lower())
+    if engine is None:
+        raise ValueError(f"bootstrap engine for compare_method={method!r}: spearman or kendall")
     pa = model_rdm if isinstance(model_rdm, RankPlan) else RankPlan(model_rdm)
     pb = neural_rdm if isinstance(neural_rdm, RankPlan) else RankPlan(neural_rdm)
     n = pa.n
     if idx is None:
         idx = bootstrap_indices(seed, n, int(n * 0.9), int(n_bootstrap)) if n_bootstrap else None
-    scores = bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    scores = engine(pa, pb, idx, full_first=True).cpu().numpy()
     point, boot = float(scores[0]), scores[1:].copy()
     if boot.size == 0:
         return point, boot, float("nan"), float("nan")
@@ -329,7 +376,8 @@ def compute_rsa(
         rprint(f"Building RDMs with Pearson, comparing with {method.capitalize()}", style="info")
 
     neural_rdm_sel = compute_rdm(_index_rows(selection.neural, sel_idx))
-    sel_plan = RankPlan(neural_rdm_sel) if method == "spearman" and n_sel > 1 else None
+    engine = _ENGINES.get(method)
+    sel_plan = RankPlan(neural_rdm_sel) if engine is not None and n_sel > 1 else None
 
     selection_scores = []
     best_layer, best_score = None, -float("inf")
@@ -337,7 +385,7 @@ def compute_rsa(
         flat = _flatten(_index_rows(acts, sel_idx))
         layer_rdm = compute_rdm(flat)
         if sel_plan is not None:
-            score = float(bootstrap_spearman(RankPlan(layer_rdm), sel_plan, None)[0].item())
+            score = float(engine(RankPlan(layer_rdm), sel_plan, None)[0].item())
             if math.isnan(score):
                 logger.warning("NaN returned for %s correlation", method.capitalize())
         else:
@@ -365,14 +413,14 @@ def compute_rsa(
 
     ci_low, ci_high = None, None
     bootstrap_scores_list = None
-    if method == "spearman" and n_test > 1:
+    if engine is not None and n_test > 1:
         plan_m, plan_n = RankPlan(test_model_rdm), RankPlan(test_neural_rdm)
         boot_idx = None
         if bootstrap and n_bootstrap > 0:
             k = int(n_test * 0.9)
             boot_idx = np.stack([rng.choice(n_test, size=k, replace=False)
                                  for _ in range(n_bootstrap)]).astype(np.int32)
-        scores = bootstrap_spearman(plan_m, plan_n, boot_idx, full_first=True).cpu().numpy()
+        scores = engine(plan_m, plan_n, boot_idx, full_first=True).cpu().numpy()
         point_estimate = float(scores[0])
         if math.isnan(point_estimate):
             logger.warning("NaN returned for %s correlation", method.capitalize())

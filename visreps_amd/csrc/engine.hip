@@ -30,16 +30,12 @@
 #include <type_traits>
 #include <vector>
 
-#include "plan.h"
+#include "window.h"
 
 namespace vr {
 
-typedef unsigned __int128 u128;
-typedef __int128 i128;
-
 constexpr int ENG_THREADS = 1024;  // 16 waves per workgroup share one LDS mask table
 constexpr int WAVES_PER_WG = ENG_THREADS / 64;
-constexpr int LANES = 64;
 constexpr int SCAN_SEGS = 256;     // segments per block in the segment scans / final fold
 
 struct EngineCfg {
@@ -145,90 +141,6 @@ __global__ void k_masks_full(uint64_t* __restrict__ masks, int64_t n) {
   if (x < n) masks[x] |= 1ull;  // lane 0 of the first pass
 }
 
-// ---------------------------------------------------------------------------------
-// device helpers
-// ---------------------------------------------------------------------------------
-template <bool LDS>
-__device__ inline const uint64_t* stage_masks(const uint64_t* __restrict__ gmask, int64_t n,
-                                              uint64_t* smem) {
-  if (!LDS) return gmask;
-  for (int64_t x = threadIdx.x; x < n; x += blockDim.x) smem[x] = gmask[x];
-  __syncthreads();
-  return smem;
-}
-
-__device__ inline uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-__device__ inline uint32_t readlane_u32(uint32_t v, uint32_t l) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
-}
-
-// Uniform-address load through the constant address space: selected as SMEM (s_load).
-template <typename T>
-__device__ inline T sload(const T* p) {
-  return *(const __attribute__((address_space(4))) T*)p;
-}
-
-__device__ inline uint64_t shfl_xor64(uint64_t v, int m) {
-  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
-  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// 64x64 bit-matrix transpose across the wave: on entry bit s of lane j is element (j, s);
-// on exit bit j of lane s is. Recursive block swap, 6 stages of one 64-bit exchange.
-__device__ inline uint64_t transpose64(uint64_t x, int lane) {
-  constexpr uint64_t K[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
-                             0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-  for (int st = 0; st < 6; ++st) {
-    const int w = 32 >> st;
-    const uint64_t p = shfl_xor64(x, w);
-    const uint64_t hi = (x & ~K[st]) | ((p & ~K[st]) >> w);  // lanes with bit w set
-    const uint64_t lo = (x & K[st]) | ((p & K[st]) << w);
-    const uint64_t sel = 0ull - (uint64_t)((lane >> (5 - st)) & 1);  // branch-free select
-    x = (hi & sel) | (lo & ~sel);
-  }
-  return x;
-}
-
-__device__ inline uint64_t lowmask(uint32_t b) { return b >= 64 ? ~0ull : ((1ull << b) - 1ull); }
-
-// Inclusion bits of the window for this lane's subset (bit j <-> position w0 + j), from
-// the window's codes (lane j holds pair w0 + j).
-__device__ inline uint64_t window_bits(const uint64_t* m, uint32_t code, uint32_t w0, uint32_t P0,
-                                       uint32_t P1, int lane, bool active) {
-  const uint32_t pos = w0 + (uint32_t)lane;
-  uint64_t x = 0;
-  if (pos >= P0 && pos < P1) x = m[code >> 16] & m[code & 0xffffu];
-  x = transpose64(x, lane);
-  return active ? x : 0ull;
-}
-
-// The window's 64 codes and group-start flags through the scalar unit (s_load_dwordx16 x4
-// + s_load_dwordx2). Issued one window ahead (k_rankA), they never queue behind the wave's
-// own TB stores the way a vector load would (vmcnt is in order on CDNA). Reads past the
-// segment stay inside the plan buffer (gstart follows codes; gflag has 2 spare words).
-struct WindowScalars {
-  uint32_t c[64];
-  uint32_t f0, f1;
-};
-__device__ inline void load_window(const uint32_t* __restrict__ codes,
-                                   const uint32_t* __restrict__ gflag, uint32_t w0,
-                                   WindowScalars& w) {
-#pragma unroll
-  for (int j = 0; j < 64; ++j) w.c[j] = sload(codes + w0 + j);
-  w.f0 = sload(gflag + (w0 >> 5));
-  w.f1 = sload(gflag + (w0 >> 5) + 1);
-}
-// lane j <- c[j] (v_writelane from SGPRs)
-__device__ inline uint32_t place_codes(const WindowScalars& w) {
-  uint32_t code = 0;
-#pragma unroll
-  for (int j = 0; j < 64; ++j) asm("v_writelane_b32 %0, %1, %2" : "+v"(code) : "s"(w.c[j]), "i"(j));
-  return code;
-}
-
 __device__ inline uint64_t restrict_flags(uint64_t F, uint32_t w0, uint32_t P0, uint32_t P1) {
   if (P0 >= w0) F &= ~lowmask(P0 - w0 + 1);
   if (P1 - w0 < 64) F = (F & lowmask(P1 - w0)) | (1ull << (P1 - w0));
@@ -263,8 +175,6 @@ __device__ inline void store_rows(TBT* __restrict__ TB, uint32_t stride, uint32_
   for (; i < cnt; ++i, row += stride) __builtin_nontemporal_store(v, row);
 }
 
-__device__ inline uint32_t popc64(uint64_t x) { return (uint32_t)__popcll(x); }
-
 struct Segment {
   uint32_t c0, c1;
 };
@@ -281,6 +191,22 @@ __host__ __device__ inline uint32_t seg_of_chunk(uint32_t c, uint32_t nchunks, u
 __device__ inline uint32_t chunk_start(const uint32_t* __restrict__ gstart,
                                        const uint32_t* __restrict__ chunk_g, uint32_t c) {
   return sload(gstart + sload(chunk_g + c));
+}
+
+int build_pass_masks(const int32_t* idx, int64_t k, int64_t set0, int nl, int full_first,
+                     uint64_t* masks, int64_t n, hipStream_t st) {
+  VR_CHECK_HIP(hipMemsetAsync(masks, 0, (size_t)n * sizeof(uint64_t), st));
+  if (full_first && set0 == 0) {
+    k_masks_full<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(masks, n);
+    VR_CHECK_LAUNCH();
+  }
+  const int64_t nrows = nl - ((full_first && set0 == 0) ? 1 : 0);
+  if (nrows > 0 && k > 0) {
+    dim3 grid((unsigned)std::min<int64_t>((k + 255) / 256, 64), (unsigned)nl);
+    k_masks_sets<<<grid, 256, 0, st>>>(idx, k, set0, nl, full_first, masks);
+    VR_CHECK_LAUNCH();
+  }
+  return VR_OK;
 }
 
 // ---------------------------------------------------------------------------------
@@ -461,6 +387,12 @@ __global__ void k_add_base(const uint32_t* __restrict__ lpA, const uint32_t* __r
 // Loads only. Per window three coalesced rows (codes, posA, chunkA) fetched one window
 // ahead; per pair its TB row (HBM, random) and A-chunk base row (L2-resident), issued 16
 // pairs at a time.
+#ifndef VR_RANKB_MINW
+#define VR_RANKB_MINW 8  // waves per SIMD the B pass is compiled for (8: 64 VGPRs)
+#endif
+#ifndef VR_RANKB_PIPE
+#define VR_RANKB_PIPE 0  // 1: gather batch h+1 in flight while batch h is consumed
+#endif
 constexpr int BB = 8;  // pairs per gather batch
 
 // BB pairs' yA = 2 baseA[chunkA] + TB[posA] for this lane. The loads are issued in the
@@ -469,10 +401,9 @@ constexpr int BB = 8;  // pairs per gather batch
 // s_waitcnt tied to every result. This kernel issues no vector stores and all of the
 // compiler's own vector loads are older than these, so its waits stay conservative.
 template <typename TBT>
-__device__ inline void gather_batch(const TBT* __restrict__ TB, const uint32_t* __restrict__ baseA,
+__device__ inline void gather_issue(const TBT* __restrict__ TB, const uint32_t* __restrict__ baseA,
                                     uint32_t stride, uint32_t pa, uint32_t ca, uint32_t j0,
-                                    uint32_t lane_bt, uint32_t lane_b4, uint32_t ya[BB]) {
-  uint32_t t[BB], b[BB];
+                                    uint32_t lane_bt, uint32_t lane_b4, uint32_t t[BB], uint32_t b[BB]) {
 #pragma unroll
   for (int q = 0; q < BB; ++q) {
     const char* trow = reinterpret_cast<const char*>(TB) +
@@ -484,19 +415,66 @@ __device__ inline void gather_batch(const TBT* __restrict__ TB, const uint32_t* 
       asm volatile("global_load_dword %0, %1, %2" : "=v"(t[q]) : "v"(lane_bt), "s"(trow) : "memory");
     asm volatile("global_load_dword %0, %1, %2" : "=v"(b[q]) : "v"(lane_b4), "s"(brow) : "memory");
   }
+}
+
+// wait until at most PENDING of this wave's loads are outstanding; ties t, b
+template <int PENDING>
+__device__ inline void gather_wait(uint32_t t[BB], uint32_t b[BB]) {
   static_assert(BB == 8, "the wait below names 16 registers");
-  asm volatile("s_waitcnt vmcnt(0)"
-               : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
-                 "+v"(t[7]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]),
-                 "+v"(b[6]), "+v"(b[7])
-               :
-               : "memory");
+  static_assert(PENDING == 0 || PENDING == 2 * BB, "vmcnt immediate");
+  if constexpr (PENDING == 0)
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+                   "+v"(t[7]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]),
+                   "+v"(b[6]), "+v"(b[7])
+                 :
+                 : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(16)"
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+                   "+v"(t[7]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]),
+                   "+v"(b[6]), "+v"(b[7])
+                 :
+                 : "memory");
+}
+
+// yA of the window's 64 pairs, batch by batch, handed to fn(h, ya[BB])
+template <typename TBT, typename Fn>
+__device__ inline void gather_window(const TBT* __restrict__ TB, const uint32_t* __restrict__ baseA,
+                                     uint32_t stride, uint32_t pa, uint32_t ca, uint32_t lane_bt,
+                                     uint32_t lane_b4, Fn&& fn) {
+  if constexpr (VR_RANKB_PIPE) {
+    uint32_t t[2][BB], b[2][BB];
+    gather_issue<TBT>(TB, baseA, stride, pa, ca, 0, lane_bt, lane_b4, t[0], b[0]);
 #pragma unroll
-  for (int q = 0; q < BB; ++q) ya[q] = 2u * b[q] + t[q];
+    for (int h = 0; h < 64 / BB; ++h) {
+      const int cur = h & 1;
+      if (h + 1 < 64 / BB) {
+        gather_issue<TBT>(TB, baseA, stride, pa, ca, (h + 1) * BB, lane_bt, lane_b4, t[cur ^ 1], b[cur ^ 1]);
+        gather_wait<2 * BB>(t[cur], b[cur]);
+      } else {
+        gather_wait<0>(t[cur], b[cur]);
+      }
+      uint32_t ya[BB];
+#pragma unroll
+      for (int q = 0; q < BB; ++q) ya[q] = 2u * b[cur][q] + t[cur][q];
+      fn(h, ya);
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 64 / BB; ++h) {
+      uint32_t t[BB], b[BB], ya[BB];
+      gather_issue<TBT>(TB, baseA, stride, pa, ca, h * BB, lane_bt, lane_b4, t, b);
+      gather_wait<0>(t, b);
+#pragma unroll
+      for (int q = 0; q < BB; ++q) ya[q] = 2u * b[q] + t[q];
+      fn(h, ya);
+    }
+  }
 }
 
 template <bool LDS, bool FULL, typename TBT, bool BIGT>
-__global__ __launch_bounds__(ENG_THREADS, 8) void k_rankB(
+__global__ __launch_bounds__(ENG_THREADS, VR_RANKB_MINW) void k_rankB(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
     const uint64_t* __restrict__ gmask, int64_t n, const TBT* __restrict__ TB, int lw,
@@ -549,20 +527,41 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankB(
       const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
       const uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
       if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
+      if (F == ~0ull) {
+        // Every position starts a group (the normal case for continuous RDMs): after
+        // closing the carried group, positions 0..62 are singletons, whose tie term is 0
+        // and whose doubled midrank is 2 (c + 1) with c the included count before them;
+        // position 63 opens the next group. The singleton products yA (c + 1) stay below
+        // 2^50 (yA < 2^32, segment counts < 2^18), so a window sums them in 64 bits.
+        close(cw);
+        uint64_t a64 = 0;
+        uint32_t c = cw;
+        gather_window<TBT>(TB, baseA, stride, pa_c, ca_c, lane_bt, lane_b4, [&](int h, uint32_t* ya) {
 #pragma unroll
-      for (int h = 0; h < 64 / BB; ++h) {
-        uint32_t ya[BB];
-        gather_batch<TBT>(TB, baseA, stride, pa_c, ca_c, h * BB, lane_bt, lane_b4, ya);
-        if (!active) {
+          for (int q = 0; q < BB; ++q) {
+            const uint32_t j = h * BB + q;
+            const uint32_t b = (uint32_t)(x >> j) & 1u;
+            const uint32_t yb = b ? ya[q] : 0u;  // x is 0 on inactive lanes
+            if (j < 63) {
+              a64 += (uint64_t)yb * (c + 1u);
+              St += yb;
+              c += b;
+            } else {
+              S = yb;
+              cgs = c;
+            }
+          }
+        });
+        acc += (u128)a64 * 2u;
+      } else {
+        gather_window<TBT>(TB, baseA, stride, pa_c, ca_c, lane_bt, lane_b4, [&](int h, uint32_t* ya) {
 #pragma unroll
-          for (int q = 0; q < BB; ++q) ya[q] = 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < BB; ++q) {
-          const uint32_t j = h * BB + q;
-          if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
-          S += ((x >> j) & 1ull) ? (uint64_t)ya[q] : 0ull;
-        }
+          for (int q = 0; q < BB; ++q) {
+            const uint32_t j = h * BB + q;
+            if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
+            S += ((x >> j) & 1ull) ? (uint64_t)ya[q] : 0ull;  // x is 0 on inactive lanes
+          }
+        });
       }
       cw += popc64(x);
     }
@@ -778,17 +777,7 @@ static int run_engine(const PlanView& A, const PlanView& B, int64_t n, const int
   VR_CHECK_LAUNCH();
   for (int64_t set0 = 0; set0 < total; set0 += lw) {
     const int nl = (int)std::min<int64_t>(lw, total - set0);
-    VR_CHECK_HIP(hipMemsetAsync(E.masks, 0, (size_t)n * sizeof(uint64_t), st));
-    if (full_first && set0 == 0) {
-      k_masks_full<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(E.masks, n);
-      VR_CHECK_LAUNCH();
-    }
-    const int64_t nrows = nl - ((full_first && set0 == 0) ? 1 : 0);
-    if (nrows > 0 && k > 0) {
-      dim3 grid((unsigned)std::min<int64_t>((k + 255) / 256, 64), (unsigned)nl);
-      k_masks_sets<<<grid, 256, 0, st>>>(idx, k, set0, nl, full_first, E.masks);
-      VR_CHECK_LAUNCH();
-    }
+    VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
     VR_TRY(dispatch_pass(kind, A, B, n, E, lw, nl, scores + set0, cfg, st));
   }
   return VR_OK;

@@ -1,0 +1,598 @@
+// Kendall tau-a comparison of two RDMs and its bootstrap, the MI355X replacement of
+//   compute_rdm_correlation(A, B, correlation="Kendall")  -> _kendall_tau_a(triu(A), triu(B))
+// visreps/analysis/rsa.py:22-40,96-129 (scipy.stats.kendalltau tau-b, converted to tau-a)
+// and of the bootstrap loop evals.py:355-373 / rsa.py:233-261 with compare_method=kendall.
+//
+// scipy's tau-b (scipy/stats/_stats_py.py kendalltau) from exact integers, per subset:
+//   tot = M'(M'-1)/2 over the M' included pairs (elements of the triangle vectors),
+//   xtie / ytie / ntie = sum over tie groups of x / of y / of (x, y) jointly of C(k, 2),
+//   dis = discordant pairs = inversions of y's dense rank in (x, y)-lexicographic order,
+//   tau_b = (tot - xtie - ytie + ntie - 2 dis) / sqrt(tot - xtie) / sqrt(tot - ytie),
+// then the reference's conversion tau_a = tau_b sqrt((tot - xtie)(tot - ytie)) / tot,
+// each in the same fp64 operation order, so the value matches scipy + rsa.py exactly.
+//
+// Inversions are counted bit by bit of the y rank (an MSD binary radix split): at level b
+// the stream is the (x, y)-lexicographic order stably sorted by y >> (b+1); an inverted
+// pair has its highest differing y bit at exactly one level, where it is a (1 before 0)
+// pair inside one bucket of equal y >> (b+1). Each level is one stream of pair codes plus
+// two bit planes (bit b of y, bucket starts), built once per (A, B) unit by a stable split
+// of the previous level (k_level_split) and walked once per pass of 64 subsets with the
+// engine's window machinery (window.h) and the bit-parallel counters of kcount.h. Tie sums
+// are the same segmented count over the multi-element tie groups of the x-lex order (x and
+// joint ties) and of B's order (y ties). All counts are exact integers, so scores do not
+// depend on launch geometry or pass grouping.
+//
+// Memory: one level is resident at a time (streams are walked level by level, every pass
+// against it); per unit ~14 x M x 4 B of scratch.
+#include <algorithm>
+#include <cmath>
+
+#include "kcount.h"
+#include "window.h"
+
+namespace vr {
+
+constexpr int KW_THREADS = 1024;
+constexpr int KW_WAVES = KW_THREADS / 64;
+constexpr int KFIX_GROUPS = KW_THREADS / 64;
+
+enum KField { KF_DIS = 0, KF_XTIE, KF_NTIE, KF_YTIE, KF_INCL, KF_N };
+
+struct KCfg {
+  int grid;
+  int nwaves;
+  size_t lds;
+  bool use_lds;
+};
+
+static KCfg kendall_cfg(int64_t n) {
+  KCfg c;
+  const size_t need = (size_t)n * sizeof(uint64_t);
+  const size_t cap = 160 * 1024 - 1024;
+  c.use_lds = need <= cap;
+  const int per_cu = c.use_lds ? std::max<int>(1, std::min<int>(2, (int)(cap / std::max<size_t>(need, 1)))) : 2;
+  c.grid = num_cus() * per_cu;
+  c.nwaves = c.grid * KW_WAVES;
+  c.lds = c.use_lds ? need : 0;
+  return c;
+}
+
+__host__ __device__ inline int64_t kwindows(int64_t M) { return (M + 63) / 64; }
+// two u32 words per window; the plane kernels run whole 256-thread blocks (4 windows)
+static inline int64_t kflag_words(int64_t M) { return 2 * ((kwindows(M) + 3) / 4 * 4) + 2; }
+
+struct KendallWs {
+  uint64_t* masks;   // [npass][n]
+  uint32_t* gidxA;   // [M] dense tie-group index of each A position
+  uint32_t* gidxB;   // [M] ... of each B position
+  uint32_t* wcnt;    // [(M+31)/32 + 1]
+  uint32_t* keys;    // [M]
+  uint32_t* vals;    // [M]
+  uint32_t* keys_alt;
+  uint32_t* vals_alt;
+  uint32_t* radix;
+  uint32_t* scan;
+  uint32_t* ecode[2];  // level streams: pair code and y (dense B rank), ping-pong
+  uint32_t* ey[2];
+  uint32_t* zflag;
+  uint32_t* zscan;
+  uint32_t* lv_start;  // [FW] bucket starts of the current level
+  uint32_t* lv_bits;   // [FW] bit b of y
+  uint32_t* xa_start;  // [FW] x-lex order: starts / members of multi-element A groups
+  uint32_t* xa_mem;
+  uint32_t* xj_start;  //               ... of multi-element joint (A, B) groups
+  uint32_t* xj_mem;
+  uint32_t* yb_start;  // B order: starts / members of multi-element B groups
+  uint32_t* yb_mem;
+  uint64_t* w_acc;     // [nwaves][64] per-wave partials
+  uint32_t* w_zlead;
+  uint32_t* w_c;
+  uint32_t* w_seen;
+  uint32_t* w_incl;
+  uint64_t* tot;       // [KF_N][cap]
+};
+
+static KendallWs kendall_layout(void* base, int64_t n, int64_t cap_sets, int nwaves, size_t* bytes) {
+  const int64_t M = pairs_of(n);
+  const int64_t FW = kflag_words(M);
+  const int64_t npass = (cap_sets + LANES - 1) / LANES;
+  Carver c(base);
+  KendallWs w;
+  w.masks = c.take<uint64_t>((size_t)std::max<int64_t>(npass, 1) * (size_t)n);
+  w.gidxA = c.take<uint32_t>((size_t)M);
+  w.gidxB = c.take<uint32_t>((size_t)M);
+  w.wcnt = c.take<uint32_t>((size_t)(M + 31) / 32 + 1);
+  w.keys = c.take<uint32_t>((size_t)M);
+  w.vals = c.take<uint32_t>((size_t)M);
+  w.keys_alt = c.take<uint32_t>((size_t)M);
+  w.vals_alt = c.take<uint32_t>((size_t)M);
+  w.radix = c.take<uint32_t>(radix_ws_elems(M));
+  w.scan = c.take<uint32_t>(scan_ws_elems(M));
+  for (int i = 0; i < 2; ++i) {
+    w.ecode[i] = c.take<uint32_t>((size_t)M);
+    w.ey[i] = c.take<uint32_t>((size_t)M);
+  }
+  w.zflag = c.take<uint32_t>((size_t)M);
+  w.zscan = c.take<uint32_t>((size_t)M);
+  uint32_t** fl[] = {&w.lv_start, &w.lv_bits, &w.xa_start, &w.xa_mem, &w.xj_start, &w.xj_mem,
+                     &w.yb_start, &w.yb_mem};
+  for (uint32_t** f : fl) *f = c.take<uint32_t>((size_t)FW);
+  w.w_acc = c.take<uint64_t>((size_t)nwaves * LANES);
+  w.w_zlead = c.take<uint32_t>((size_t)nwaves * LANES);
+  w.w_c = c.take<uint32_t>((size_t)nwaves * LANES);
+  w.w_seen = c.take<uint32_t>((size_t)nwaves * LANES);
+  w.w_incl = c.take<uint32_t>((size_t)nwaves * LANES);
+  w.tot = c.take<uint64_t>((size_t)KF_N * (size_t)std::max<int64_t>(cap_sets, 1));
+  if (bytes) *bytes = c.bytes();
+  return w;
+}
+
+// ---------------------------------------------------------------------------------
+// per-unit precompute
+// ---------------------------------------------------------------------------------
+__global__ void k_word_popc(const uint32_t* __restrict__ gflag, int64_t words,
+                            uint32_t* __restrict__ out) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < words) out[w] = (uint32_t)__popc(gflag[w]);
+}
+
+// gidx[p] = dense index of the tie group holding sorted position p
+__global__ void k_group_index(const uint32_t* __restrict__ gflag, const uint32_t* __restrict__ wpre,
+                              int64_t M, uint32_t* __restrict__ gidx) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= M) return;
+  const uint32_t w = gflag[p >> 5];
+  gidx[p] = wpre[p >> 5] + (uint32_t)__popc(w & (0xFFFFFFFFu >> (31 - (p & 31)))) - 1u;
+}
+
+// B position i -> (key = A group of its pair, value = i); sorting stably by key from B
+// order gives the (x, y)-lexicographic order of scipy's kendalltau
+__global__ void k_kendall_keys(const uint32_t* __restrict__ codesB, int64_t M, int64_t n,
+                               const uint32_t* __restrict__ posOfPairA,
+                               const uint32_t* __restrict__ gidxA, uint32_t* __restrict__ keys,
+                               uint32_t* __restrict__ vals) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const uint32_t cb = codesB[i];
+  keys[i] = gidxA[posOfPairA[tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n)]];
+  vals[i] = (uint32_t)i;
+}
+
+__global__ void k_kendall_elems(const uint32_t* __restrict__ vals, const uint32_t* __restrict__ codesB,
+                                const uint32_t* __restrict__ gidxB, int64_t M,
+                                uint32_t* __restrict__ ecode, uint32_t* __restrict__ ey) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= M) return;
+  const uint32_t i = vals[p];
+  ecode[p] = codesB[i];
+  ey[p] = gidxB[i];
+}
+
+// 64 positions per wave -> two u32 words of each bit plane
+__device__ inline void put_plane(uint32_t* plane, int64_t p, bool bit) {
+  const uint64_t b = __ballot(bit);
+  if ((threadIdx.x & 63) == 0) {
+    plane[(p >> 6) * 2] = (uint32_t)b;
+    plane[(p >> 6) * 2 + 1] = (uint32_t)(b >> 32);
+  }
+}
+
+// x-lex order tie planes: starts and members of multi-element A groups and of
+// multi-element joint (A, B) groups
+__global__ void k_xlex_flags(const uint32_t* __restrict__ gA, const uint32_t* __restrict__ ey,
+                             int64_t M, uint32_t* __restrict__ xa_start, uint32_t* __restrict__ xa_mem,
+                             uint32_t* __restrict__ xj_start, uint32_t* __restrict__ xj_mem) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool v = p < M;
+  bool nsA = false, memA = false, nsJ = false, memJ = false;
+  if (v) {
+    const uint32_t a = gA[p], y = ey[p];
+    const bool sA = p == 0 || gA[p - 1] != a;
+    const bool sJ = sA || ey[p - 1] != y;
+    const bool last = p + 1 >= M;
+    const bool sA1 = last || gA[p + 1] != a;
+    const bool sJ1 = sA1 || ey[p + 1] != y;
+    nsA = sA && !sA1;
+    memA = !(sA && sA1);
+    nsJ = sJ && !sJ1;
+    memJ = !(sJ && sJ1);
+  }
+  put_plane(xa_start, p, nsA);
+  put_plane(xa_mem, p, memA);
+  put_plane(xj_start, p, nsJ);
+  put_plane(xj_mem, p, memJ);
+}
+
+// B order tie planes from the plan's group-start bitmask
+__global__ void k_border_flags(const uint32_t* __restrict__ gflag, int64_t M,
+                               uint32_t* __restrict__ yb_start, uint32_t* __restrict__ yb_mem) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool v = p < M;
+  bool ns = false, mem = false;
+  if (v) {
+    const bool s = (gflag[p >> 5] >> (p & 31)) & 1u;
+    const int64_t q = p + 1;
+    const bool s1 = q >= M || ((gflag[q >> 5] >> (q & 31)) & 1u);
+    ns = s && !s1;
+    mem = !(s && s1);
+  }
+  put_plane(yb_start, p, ns);
+  put_plane(yb_mem, p, mem);
+}
+
+// level b planes of the current stream (sorted by y >> (b+1)): bit b of y, bucket starts;
+// zero flags for the split
+__global__ void k_level_flags(const uint32_t* __restrict__ ey, int64_t M, int b,
+                              uint32_t* __restrict__ lv_start, uint32_t* __restrict__ lv_bits,
+                              uint32_t* __restrict__ zflag) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool v = p < M;
+  bool st = false, bit = false;
+  if (v) {
+    const uint32_t y = ey[p];
+    bit = (y >> b) & 1u;
+    st = p == 0 || (ey[p - 1] >> (b + 1)) != (y >> (b + 1));
+    zflag[p] = bit ? 0u : 1u;
+  }
+  put_plane(lv_start, p, st);
+  put_plane(lv_bits, p, bit);
+}
+
+// stable split of every bucket by bit b: the stream for level b-1 (sorted by y >> b).
+// gstartB[g] = number of elements with y < g, so the bucket of y >> (b+1) starts at
+// gstartB[(y >> (b+1)) << (b+1)] and its one-half at gstartB[(y >> b) << b].
+__global__ void k_level_split(const uint32_t* __restrict__ ecode, const uint32_t* __restrict__ ey,
+                              const uint32_t* __restrict__ zscan, const uint32_t* __restrict__ gstartB,
+                              int64_t M, int b, uint32_t* __restrict__ ecode_out,
+                              uint32_t* __restrict__ ey_out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= M) return;
+  const uint32_t y = ey[p];
+  const uint32_t bs = gstartB[(y >> (b + 1)) << (b + 1)];
+  const uint32_t zb = zscan[bs], zp = zscan[p];
+  uint32_t np;
+  if ((y >> b) & 1u)
+    np = gstartB[(y >> b) << b] + ((uint32_t)p - bs) - (zp - zb);
+  else
+    np = bs + (zp - zb);
+  ecode_out[np] = ecode[p];
+  ey_out[np] = y;
+}
+
+// ---------------------------------------------------------------------------------
+// per-pass stream walk
+// ---------------------------------------------------------------------------------
+// TIE: o = z = included members (aux plane) of multi-element groups, S = their starts;
+// else (inversions): o / z = included positions with bit b of y set / clear (aux plane),
+// S = bucket starts.
+template <bool LDS, bool TIE>
+__global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
+    const uint32_t* __restrict__ codes, const uint32_t* __restrict__ sflag,
+    const uint32_t* __restrict__ aux, int64_t M, const uint64_t* __restrict__ gmask, int64_t n,
+    int nl, uint32_t nwaves, uint64_t* __restrict__ w_acc, uint32_t* __restrict__ w_zlead,
+    uint32_t* __restrict__ w_c, uint32_t* __restrict__ w_seen, uint32_t* __restrict__ w_incl) {
+  extern __shared__ uint64_t smask[];
+  const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
+  const int lane = threadIdx.x & 63;
+  const bool active = lane < nl;
+  const uint32_t wave = wave_uniform(blockIdx.x * KW_WAVES + (threadIdx.x >> 6));
+  const uint64_t nwin = (uint64_t)kwindows(M);
+  const uint32_t wb = (uint32_t)(nwin * wave / nwaves), we = (uint32_t)(nwin * (wave + 1) / nwaves);
+  KSeg a{0ull, 0u, 0u};
+  bool seen = false;
+  uint32_t incl = 0;
+  uint32_t cd = 0;
+  if (wb < we) {
+    const uint32_t p0 = wb * 64u + (uint32_t)lane;
+    cd = p0 < (uint64_t)M ? codes[p0] : 0u;
+  }
+  for (uint32_t win = wb; win < we; ++win) {
+    const uint32_t pos = win * 64u + (uint32_t)lane;
+    const bool valid = pos < (uint64_t)M;
+    uint64_t mb = valid ? (m[cd >> 16] & m[cd & 0xffffu]) : 0ull;
+    if (win + 1 < we) {  // next window's code, one ahead
+      const uint32_t q = pos + 64u;
+      cd = q < (uint64_t)M ? codes[q] : 0u;
+    }
+    uint64_t x = transpose64(mb, lane);
+    if (!active) x = 0ull;
+    const uint64_t S = ((uint64_t)sload(sflag + 2 * win + 1) << 32) | sload(sflag + 2 * win);
+    const uint64_t X = ((uint64_t)sload(aux + 2 * win + 1) << 32) | sload(aux + 2 * win);
+    incl += popc64(x);
+    if (TIE) {
+      const uint64_t o = x & X;
+      kseg_window<true>(o, o, S, a, seen);
+    } else {
+      kseg_window<false>(x & X, x & ~X, S, a, seen);
+    }
+  }
+  const size_t o = (size_t)wave * LANES + lane;
+  w_acc[o] = a.acc;
+  w_zlead[o] = a.zlead;
+  w_c[o] = a.c;
+  w_seen[o] = seen ? 1u : 0u;
+  w_incl[o] = incl;
+}
+
+// Stream total per lane: sum of wave partials + cross-wave fix-up (kcount.h), added into
+// tot[field][set0 + lane]; optionally the included-pair count into tot[KF_INCL].
+__global__ __launch_bounds__(KW_THREADS) void k_kfix(
+    const uint64_t* __restrict__ w_acc, const uint32_t* __restrict__ w_zlead,
+    const uint32_t* __restrict__ w_c, const uint32_t* __restrict__ w_seen,
+    const uint32_t* __restrict__ w_incl, uint32_t nwaves, int nl, int field, int add_incl,
+    uint64_t* __restrict__ tot, int64_t cap, int64_t set0) {
+  __shared__ uint64_t s_sum[KFIX_GROUPS][LANES], s_g[KFIX_GROUPS][LANES], s_a[KFIX_GROUPS][LANES],
+      s_inc[KFIX_GROUPS][LANES];
+  __shared__ uint32_t s_b[KFIX_GROUPS][LANES];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const uint32_t per = (nwaves + KFIX_GROUPS - 1) / KFIX_GROUPS;
+  const uint32_t w0 = grp * per, w1 = min(nwaves, w0 + per);
+  KFix F = kfix_identity();
+  uint64_t sum = 0, inc = 0;
+  for (uint32_t w = w0; w < w1; ++w) {
+    const size_t o = (size_t)w * LANES + lane;
+    sum += w_acc[o];
+    inc += w_incl[o];
+    kfix_push(F, w_zlead[o], w_c[o], w_seen[o] != 0u);
+  }
+  s_sum[grp][lane] = sum + F.f0;
+  s_g[grp][lane] = F.g;
+  s_a[grp][lane] = F.a;
+  s_b[grp][lane] = F.b;
+  s_inc[grp][lane] = inc;
+  __syncthreads();
+  if (grp != 0) return;
+  uint64_t C = 0, total = 0, incl = 0;
+  for (int g = 0; g < KFIX_GROUPS; ++g) {
+    total += s_sum[g][lane] + s_g[g][lane] * C;
+    C = s_a[g][lane] + (s_b[g][lane] ? C : 0ull);
+    incl += s_inc[g][lane];
+  }
+  if (lane < nl) {
+    tot[(size_t)field * cap + set0 + lane] += total;
+    if (add_incl) tot[(size_t)KF_INCL * cap + set0 + lane] = incl;
+  }
+}
+
+// tau-a per subset from the exact counts, in scipy's / rsa.py's fp64 operation order
+__global__ void k_kfinal(const uint64_t* __restrict__ tot, int64_t cap, int64_t total_sets,
+                         double* __restrict__ scores) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= total_sets) return;
+  const uint64_t Mp = tot[(size_t)KF_INCL * cap + s];
+  const uint64_t dis = tot[(size_t)KF_DIS * cap + s];
+  const uint64_t xt = tot[(size_t)KF_XTIE * cap + s];
+  const uint64_t nt = tot[(size_t)KF_NTIE * cap + s];
+  const uint64_t yt = tot[(size_t)KF_YTIE * cap + s];
+  double r = __builtin_nan("");
+  if (Mp >= 2) {
+    const uint64_t t = Mp * (Mp - 1) / 2;
+    if (xt != t && yt != t) {
+      const int64_t cmd = (int64_t)(t - xt - yt + nt) - 2 * (int64_t)dis;
+      double taub = (double)cmd / sqrt((double)(t - xt)) / sqrt((double)(t - yt));
+      taub = fmin(1.0, fmax(-1.0, taub));
+      const double denom = sqrt((double)(t - xt) * (double)(t - yt));
+      r = denom == 0.0 ? __builtin_nan("") : taub * denom / (double)t;
+    }
+  }
+  scores[s] = r;
+}
+
+__global__ void k_kfill_nan(double* out, int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) out[i] = __builtin_nan("");
+}
+
+// ---------------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------------
+static unsigned blocks_for(int64_t count, int bs) { return (unsigned)((count + bs - 1) / bs); }
+
+template <bool LDS>
+static int set_kwalk_attr() {
+  static bool done = false;
+  if (LDS && !done) {
+    const int mx = 160 * 1024;
+    VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk<LDS, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, mx));
+    VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk<LDS, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, mx));
+    done = true;
+  }
+  return VR_OK;
+}
+
+// one stream against every pass, totals into tot[field]
+static int walk_stream(bool tie, const uint32_t* codes, const uint32_t* sflag, const uint32_t* aux,
+                       int64_t M, const KendallWs& W, int64_t n, int64_t total, int field,
+                       bool add_incl, int64_t cap, const KCfg& cfg, hipStream_t st) {
+  for (int64_t set0 = 0, p = 0; set0 < total; set0 += LANES, ++p) {
+    const int nl = (int)std::min<int64_t>(LANES, total - set0);
+    const uint64_t* mk = W.masks + (size_t)p * (size_t)n;
+    if (cfg.use_lds) {
+      VR_TRY(set_kwalk_attr<true>());
+      if (tie)
+        k_kwalk<true, true><<<cfg.grid, KW_THREADS, cfg.lds, st>>>(codes, sflag, aux, M, mk, n, nl, cfg.nwaves,
+                                                                  W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl);
+      else
+        k_kwalk<true, false><<<cfg.grid, KW_THREADS, cfg.lds, st>>>(codes, sflag, aux, M, mk, n, nl, cfg.nwaves,
+                                                                   W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl);
+    } else {
+      if (tie)
+        k_kwalk<false, true><<<cfg.grid, KW_THREADS, 0, st>>>(codes, sflag, aux, M, mk, n, nl, cfg.nwaves,
+                                                             W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl);
+      else
+        k_kwalk<false, false><<<cfg.grid, KW_THREADS, 0, st>>>(codes, sflag, aux, M, mk, n, nl, cfg.nwaves,
+                                                              W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl);
+    }
+    VR_CHECK_LAUNCH();
+    k_kfix<<<1, KW_THREADS, 0, st>>>(W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl, (uint32_t)cfg.nwaves,
+                                     nl, field, add_incl ? 1 : 0, W.tot, cap, set0);
+    VR_CHECK_LAUNCH();
+  }
+  return VR_OK;
+}
+
+static int group_index(const PlanView& P, int64_t M, const KendallWs& W, uint32_t* gidx,
+                       hipStream_t st) {
+  const int64_t words = (M + 31) / 32;
+  k_word_popc<<<blocks_for(words, 256), 256, 0, st>>>(P.gflag, words, W.wcnt);
+  VR_CHECK_LAUNCH();
+  VR_TRY(scan_exclusive_u32(W.wcnt, W.wcnt, words, nullptr, W.scan, st));
+  k_group_index<<<blocks_for(M, 256), 256, 0, st>>>(P.gflag, W.wcnt, M, gidx);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const int32_t* idx, int64_t k,
+                       int64_t n_sets, int full_first, double* scores, const KendallWs& W,
+                       int64_t cap, const KCfg& cfg, hipStream_t st) {
+  const int64_t M = pairs_of(n);
+  const int64_t total = n_sets + (full_first ? 1 : 0);
+  if (total == 0) return VR_OK;
+  PlanHeader h[2];
+  if (M > 0) {
+    VR_CHECK_HIP(hipMemcpyAsync(&h[0], A.hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
+    VR_CHECK_HIP(hipMemcpyAsync(&h[1], B.hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
+    VR_CHECK_HIP(hipStreamSynchronize(st));
+  }
+  // no pairs, a NaN anywhere, or a constant triangle: NaN for every subset (scipy:
+  // empty input / nan_policy='propagate' / xtie == tot)
+  if (M == 0 || h[0].has_nan || h[1].has_nan || h[0].G <= 1 || h[1].G <= 1) {
+    k_kfill_nan<<<blocks_for(total, 256), 256, 0, st>>>(scores, total);
+    VR_CHECK_LAUNCH();
+    return VR_OK;
+  }
+  const unsigned gbM = blocks_for(M, 256);
+  const unsigned gbW = blocks_for(kwindows(M) * 64, 256);  // whole windows: ballots
+  // dense group ranks of both orders
+  VR_TRY(group_index(A, M, W, W.gidxA, st));
+  VR_TRY(group_index(B, M, W, W.gidxB, st));
+  // (x, y)-lexicographic order: stable sort of B order by A group
+  k_kendall_keys<<<gbM, 256, 0, st>>>(B.codes, M, n, A.pos_of_pair, W.gidxA, W.keys, W.vals);
+  VR_CHECK_LAUNCH();
+  VR_TRY(radix_sort_kv(W.keys, W.vals, W.keys_alt, W.vals_alt, M, W.radix, st));
+  k_kendall_elems<<<gbM, 256, 0, st>>>(W.vals, B.codes, W.gidxB, M, W.ecode[0], W.ey[0]);
+  VR_CHECK_LAUNCH();
+  // masks of every pass, totals zeroed
+  for (int64_t set0 = 0, p = 0; set0 < total; set0 += LANES, ++p) {
+    const int nl = (int)std::min<int64_t>(LANES, total - set0);
+    VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, W.masks + (size_t)p * (size_t)n, n, st));
+  }
+  VR_CHECK_HIP(hipMemsetAsync(W.tot, 0, sizeof(uint64_t) * (size_t)KF_N * (size_t)cap, st));
+  // tie streams (only when the plans have multi-element groups)
+  if (h[0].max_group > 1) {
+    k_xlex_flags<<<gbW, 256, 0, st>>>(W.keys, W.ey[0], M, W.xa_start, W.xa_mem, W.xj_start, W.xj_mem);
+    VR_CHECK_LAUNCH();
+    VR_TRY(walk_stream(true, W.ecode[0], W.xa_start, W.xa_mem, M, W, n, total, KF_XTIE, false, cap, cfg, st));
+    VR_TRY(walk_stream(true, W.ecode[0], W.xj_start, W.xj_mem, M, W, n, total, KF_NTIE, false, cap, cfg, st));
+  }
+  if (h[1].max_group > 1) {
+    k_border_flags<<<gbW, 256, 0, st>>>(B.gflag, M, W.yb_start, W.yb_mem);
+    VR_CHECK_LAUNCH();
+    VR_TRY(walk_stream(true, B.codes, W.yb_start, W.yb_mem, M, W, n, total, KF_YTIE, false, cap, cfg, st));
+  }
+  // inversion levels, most significant y bit first
+  const uint32_t G = h[1].G;
+  int Lb = 0;
+  while (Lb < 32 && ((G - 1u) >> Lb) != 0u) ++Lb;
+  int cur = 0;
+  for (int b = Lb - 1; b >= 0; --b) {
+    k_level_flags<<<gbW, 256, 0, st>>>(W.ey[cur], M, b, W.lv_start, W.lv_bits, W.zflag);
+    VR_CHECK_LAUNCH();
+    VR_TRY(walk_stream(false, W.ecode[cur], W.lv_start, W.lv_bits, M, W, n, total, KF_DIS, b == Lb - 1,
+                       cap, cfg, st));
+    if (b > 0) {
+      VR_TRY(scan_exclusive_u32(W.zflag, W.zscan, M, nullptr, W.scan, st));
+      k_level_split<<<gbM, 256, 0, st>>>(W.ecode[cur], W.ey[cur], W.zscan, B.gstart, M, b,
+                                         W.ecode[cur ^ 1], W.ey[cur ^ 1]);
+      VR_CHECK_LAUNCH();
+      cur ^= 1;
+    }
+  }
+  k_kfinal<<<blocks_for(total, 256), 256, 0, st>>>(W.tot, cap, total, scores);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+static size_t k_oneshot_bytes(int64_t n, int64_t cap, int nwaves, void* base, PlanView* A, PlanView* B,
+                              PlanBuildWs* PW, KendallWs* W) {
+  Carver c(base);
+  const size_t pb = plan_bytes(n);
+  char* pa = c.take<char>(pb);
+  char* pbb = c.take<char>(pb);
+  size_t wb = 0, kb = 0;
+  plan_build_layout(nullptr, n, &wb);
+  kendall_layout(nullptr, n, cap, nwaves, &kb);
+  char* wsb = c.take<char>(std::max(wb, kb));  // plan-build scratch is dead once plans exist
+  if (base) {
+    *A = plan_layout(pa, n);
+    *B = plan_layout(pbb, n);
+    *PW = plan_build_layout(wsb, n, nullptr);
+    *W = kendall_layout(wsb, n, cap, nwaves, nullptr);
+  }
+  return c.bytes();
+}
+
+}  // namespace vr
+
+using namespace vr;
+
+extern "C" {
+
+size_t vr_bootstrap_kendall_workspace(int64_t n, int64_t n_sets) {
+  size_t b = 0;
+  n = n < 0 ? 0 : n;
+  n_sets = n_sets < 0 ? 0 : n_sets;
+  kendall_layout(nullptr, n, n_sets + 1, kendall_cfg(n).nwaves, &b);
+  return b;
+}
+
+int vr_bootstrap_kendall_plans(const void* planA, const void* planB, int64_t n, const int32_t* idx,
+                               int64_t k, int64_t n_sets, int full_first, double* scores, void* ws,
+                               size_t ws_bytes, void* stream) {
+  VR_REQUIRE(n >= 0 && n <= 65535, "vr_bootstrap_kendall_plans: n=%lld out of range", (long long)n);
+  VR_REQUIRE(planA && planB && scores, "vr_bootstrap_kendall_plans: null pointer");
+  VR_REQUIRE(k >= 0 && k <= n && n_sets >= 0, "vr_bootstrap_kendall_plans: bad k=%lld sets=%lld",
+             (long long)k, (long long)n_sets);
+  VR_REQUIRE(idx != nullptr || n_sets == 0 || k == 0, "vr_bootstrap_kendall_plans: null idx");
+  const KCfg cfg = kendall_cfg(n);
+  const int64_t cap = n_sets + 1;
+  size_t need = 0;
+  KendallWs W = kendall_layout(ws, n, cap, cfg.nwaves, &need);
+  if (ws_bytes < need || ws == nullptr) {
+    set_error("vr_bootstrap_kendall_plans: workspace %zu < %zu", ws_bytes, need);
+    return VR_EWORKSPACE;
+  }
+  PlanView A = plan_layout(const_cast<void*>(planA), n);
+  PlanView B = plan_layout(const_cast<void*>(planB), n);
+  return run_kendall(A, B, n, idx, k, n_sets, full_first, scores, W, cap, cfg, as_stream(stream));
+}
+
+size_t vr_kendall_triu_workspace(int64_t n) {
+  n = n < 0 ? 0 : n;
+  return k_oneshot_bytes(n, 1, kendall_cfg(n).nwaves, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+
+int vr_kendall_triu_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out, void* ws,
+                        size_t ws_bytes, void* stream) {
+  VR_REQUIRE(n >= 0 && n <= 65535 && ld >= n, "vr_kendall_triu_f32: bad shape n=%lld ld=%lld",
+             (long long)n, (long long)ld);
+  VR_REQUIRE(out != nullptr, "vr_kendall_triu_f32: null out");
+  const KCfg cfg = kendall_cfg(n);
+  const size_t need = k_oneshot_bytes(n, 1, cfg.nwaves, nullptr, nullptr, nullptr, nullptr, nullptr);
+  if (ws_bytes < need || ws == nullptr) {
+    set_error("vr_kendall_triu_f32: workspace %zu < %zu", ws_bytes, need);
+    return VR_EWORKSPACE;
+  }
+  PlanView PA, PB;
+  PlanBuildWs PW;
+  KendallWs W;
+  k_oneshot_bytes(n, 1, cfg.nwaves, ws, &PA, &PB, &PW, &W);
+  hipStream_t st = as_stream(stream);
+  VR_TRY(build_plan(A, n, ld, PA, PW, st));
+  VR_TRY(build_plan(B, n, ld, PB, PW, st));
+  return run_kendall(PA, PB, n, nullptr, 0, 0, 1, out, W, 1, cfg, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,87 @@
+// 64-position window machinery shared by the rank engines (engine.hip: Spearman,
+// kendall.hip: Kendall tau-a).
+//
+// A pass evaluates up to 64 stimulus subsets at once: lane s of a wave is subset s and
+// masks[x] bit s says whether stimulus x is in subset s. A stream of pair codes
+// ((a << 16) | b, in some sorted order) is walked in windows of 64 positions: lane j
+// loads the code of position w0 + j, ANDs the masks of its two stimuli, and a 64x64 bit
+// transpose across the wave hands lane s the inclusion bits of all 64 positions for its
+// subset. Per-window counts are then popcounts.
+#pragma once
+
+#include "plan.h"
+
+namespace vr {
+
+typedef unsigned __int128 u128;
+typedef __int128 i128;
+
+constexpr int LANES = 64;
+
+__device__ inline uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ inline uint32_t readlane_u32(uint32_t v, uint32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+// Uniform-address load through the constant address space: selected as SMEM (s_load).
+template <typename T>
+__device__ inline T sload(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+
+__device__ inline uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// 64x64 bit-matrix transpose across the wave: on entry bit s of lane j is element (j, s);
+// on exit bit j of lane s is. Recursive block swap, 6 stages of one 64-bit exchange.
+__device__ inline uint64_t transpose64(uint64_t x, int lane) {
+  constexpr uint64_t K[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                             0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int st = 0; st < 6; ++st) {
+    const int w = 32 >> st;
+    const uint64_t p = shfl_xor64(x, w);
+    const uint64_t hi = (x & ~K[st]) | ((p & ~K[st]) >> w);  // lanes with bit w set
+    const uint64_t lo = (x & K[st]) | ((p & K[st]) << w);
+    const uint64_t sel = 0ull - (uint64_t)((lane >> (5 - st)) & 1);  // branch-free select
+    x = (hi & sel) | (lo & ~sel);
+  }
+  return x;
+}
+
+__host__ __device__ inline uint64_t lowmask(uint32_t b) { return b >= 64 ? ~0ull : ((1ull << b) - 1ull); }
+
+__device__ inline uint32_t popc64(uint64_t x) { return (uint32_t)__popcll(x); }
+
+// Inclusion bits of the window for this lane's subset (bit j <-> position w0 + j), from
+// the window's codes (lane j holds pair w0 + j).
+__device__ inline uint64_t window_bits(const uint64_t* m, uint32_t code, uint32_t w0, uint32_t P0,
+                                       uint32_t P1, int lane, bool active) {
+  const uint32_t pos = w0 + (uint32_t)lane;
+  uint64_t x = 0;
+  if (pos >= P0 && pos < P1) x = m[code >> 16] & m[code & 0xffffu];
+  x = transpose64(x, lane);
+  return active ? x : 0ull;
+}
+
+// The block's copy of the masks: LDS when they fit, else the global table itself.
+template <bool LDS>
+__device__ inline const uint64_t* stage_masks(const uint64_t* __restrict__ gmask, int64_t n,
+                                              uint64_t* smem) {
+  if (!LDS) return gmask;
+  for (int64_t x = threadIdx.x; x < n; x += blockDim.x) smem[x] = gmask[x];
+  __syncthreads();
+  return smem;
+}
+
+// Inclusion masks of one pass: bit w of masks[x] <- stimulus x in subset (set0 + w),
+// subset 0 being "all stimuli" when full_first; lanes >= nl stay empty. masks is zeroed
+// first. idx rows hold k stimulus indices each (engine.hip).
+int build_pass_masks(const int32_t* idx, int64_t k, int64_t set0, int nl, int full_first,
+                     uint64_t* masks, int64_t n, hipStream_t st);
+
+}  // namespace vr

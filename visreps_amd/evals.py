@@ -185,16 +185,17 @@ def _eval_rsa(cfg, model, acts, ids, all_data, subjects, regions, dev, verbose):
             neural_rdm = compute_rdm(neural_tensor.to(dev))
             ci_low = ci_high = None
             boot_list = None
-            if bootstrap and method == "spearman":
+            if bootstrap and method in ("spearman", "kendall"):
                 if best_layer not in model_plans:
                     model_plans[best_layer] = RankPlan(model_rdms[best_layer])
                 point, scores, ci_low, ci_high = bootstrap_rsa(
-                    model_plans[best_layer], RankPlan(neural_rdm), n_bootstrap=n_bootstrap, seed=42)
+                    model_plans[best_layer], RankPlan(neural_rdm), n_bootstrap=n_bootstrap, seed=42,
+                    method=method)
                 boot_list = scores.tolist()
             else:
                 point = compute_rdm_correlation(model_rdms[best_layer], neural_rdm,
                                                 correlation=method.capitalize())
-                if bootstrap:  # only Spearman has the engine; others are not on this path
+                if bootstrap:  # the valid compare methods (utils.py) all have an engine
                     raise NotImplementedError(f"bootstrap with compare_method='{method}'")
             msg = f"    subj {subj} | {method.capitalize():<10}| {best_layer} = {point:.4f}"
             if bootstrap:
@@ -219,6 +220,6 @@ def _eval_rsa(cfg, model, acts, ids, all_data, subjects, regions, dev, verbose):
 
 def _compare(layer_rdm, neural_rdm, neural_plan, method: str) -> float:
     """Phase-1 comparison; Spearman reuses the neural RDM's rank plan across points."""
-    if method == "spearman":
-        return float(bootstrap_rsa(RankPlan(layer_rdm), neural_plan, n_bootstrap=0)[0])
+    if method in ("spearman", "kendall"):
+        return float(bootstrap_rsa(RankPlan(layer_rdm), neural_plan, n_bootstrap=0, method=method)[0])
     return compute_rdm_correlation(layer_rdm, neural_rdm, correlation=method.capitalize())
