@@ -130,6 +130,20 @@ int vr_bootstrap_spearman_plans(const void* planA, const void* planB, int64_t n,
                                 int full_first, double* scores, void* ws,
                                 size_t ws_bytes, void* stream);
 
+/* Units that share one RDM: the bootstrap loop of evals.py:323-373 runs every model
+ * layer against the same neural RDM with the same RandomState(42) subsets. plan_a (the
+ * shared RDM) against each of the n_b plans in planBs [host array of device pointers].
+ * Per pass of 64 subsets the rank walk of plan_a runs once for all n_b units. Row j of
+ * scores [dev] double (n_b rows, leading dimension ld_scores >= n_sets + full_first)
+ * equals vr_bootstrap_spearman_plans(planBs[j], plan_a, ...) bit for bit (Spearman is
+ * symmetric and every sum is an exact integer). Workspace grows by 8 bytes per pair for
+ * every B plan after the first. */
+size_t vr_bootstrap_multi_workspace(int64_t n, int64_t n_b);
+int vr_bootstrap_spearman_multi(const void* plan_a, const void* const* planBs, int64_t n_b,
+                                int64_t n, const int32_t* idx, int64_t k, int64_t n_sets,
+                                int full_first, double* scores, int64_t ld_scores, void* ws,
+                                size_t ws_bytes, void* stream);
+
 /* One-shot form: builds both plans in the workspace, then runs the engine. */
 size_t vr_bootstrap_spearman_workspace(int64_t n);
 int vr_bootstrap_spearman_f32(const float* A, const float* B, int64_t n, int64_t ld,

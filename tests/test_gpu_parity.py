@@ -212,6 +212,63 @@ def test_bootstrap_end_to_end_tolerance(dev):
     assert abs(lo - rlo) < 1e-5 and abs(hi - rhi) < 1e-5
 
 
+@pytest.mark.parametrize("n,d,world", [(300, 70, 3), (1000, 40, 4), (2100, 33, 5), (4000, 64, 2)])
+def test_rdm_tile_ranges_assemble_full_rdm(dev, n, d, world):
+    # the block-distributed Gram (band launch order inside each rank's tile range) writes
+    # every entry of its range exactly as the one-launch RDM does
+    from visreps_amd import pipeline as P
+
+    x = torch.randn(n, d, device=dev)
+    full = R.compute_rdm(x)
+    acc = torch.zeros(n, n, device=dev)
+    for t0, t1 in P.tile_ranges(n, world):
+        part = torch.zeros(n, n, device=dev)
+        P.rdm_tiles_into(x, part, t0, t1)
+        acc += part
+    assert torch.equal(acc, full)
+    assert torch.equal(full, full.T)
+
+
+@pytest.mark.parametrize("n,nb,levels_a",[(64, 70, None), (200, 130, None), (150, 64, 6)])
+def test_bootstrap_multi_equals_per_unit(dev, n, nb, levels_a):
+    # one shared (neural) plan against several model plans: every row bit-equal to the
+    # per-unit engine call and within 1e-12 of the oracle; one model RDM tie-heavy
+    from visreps_amd.analysis._random import bootstrap_indices
+
+    feats = O.synthetic_features(n, [200, 300, 150, 100], seed=n + 1)
+    rdms = [O.compute_rdm(f) for f in feats]
+    if levels_a:
+        rdms[0] = (np.floor(rdms[0] * levels_a) / levels_a).astype(np.float32)
+    rdms[2] = (np.floor(rdms[2] * 7) / 7).astype(np.float32)
+    neural = R.RankPlan(torch.from_numpy(rdms[0]).to(dev))
+    models = [R.RankPlan(torch.from_numpy(r).to(dev)) for r in rdms[1:]]
+    idx = bootstrap_indices(42, n, int(0.9 * n), nb)
+    multi = R.bootstrap_spearman_multi(neural, models, idx).cpu().numpy()
+    assert multi.shape == (3, nb + 1)
+    for j, pm in enumerate(models):
+        single = R.bootstrap_spearman(pm, neural, idx).cpu().numpy()
+        assert np.array_equal(multi[j], single)
+        rp, rs, _, _ = O.bootstrap_rsa(rdms[j + 1], rdms[0], n_bootstrap=nb, seed=42)
+        assert abs(multi[j][0] - rp) <= 1e-12
+        assert np.max(np.abs(multi[j][1:] - rs)) <= 1e-12
+
+
+def test_all_units_groups_match_per_unit(dev):
+    # the pipeline's grouped engine calls equal independent per-unit bootstrap_rsa runs
+    from visreps_amd import pipeline as P
+
+    n = 120
+    feats = O.synthetic_features(n, [300, 200, 100, 80, 60], seed=5)
+    rdm = {f"p{i}": torch.from_numpy(O.compute_rdm(feats[i])).to(dev) for i in range(3)}
+    neural = {"r0": torch.from_numpy(O.compute_rdm(feats[3])).to(dev),
+              "r1": torch.from_numpy(O.compute_rdm(feats[4])).to(dev)}
+    res = P.all_units_rsa(lambda p: rdm[p], list(rdm), neural, n, n_boot=40, seed=42)
+    for (p, r), v in res.items():
+        point, scores, lo, hi = R.bootstrap_rsa(rdm[p], neural[r], n_bootstrap=40, seed=42)
+        assert v["score"] == point and v["ci_low"] == lo and v["ci_high"] == hi
+        assert np.array_equal(np.array(v["bootstrap_scores"]), scores)
+
+
 def test_bootstrap_masks_large_n_global_path(dev):
     # n > 20k stimuli -> inclusion masks read from global memory instead of LDS
     n = 20500

@@ -76,6 +76,11 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _vp, _c_sz, _vp],
     ),
+    "vr_bootstrap_multi_workspace": (_c_sz, [_c_i64, _c_i64]),
+    "vr_bootstrap_spearman_multi": (
+        ctypes.c_int,
+        [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _c_sz, _vp],
+    ),
     "vr_bootstrap_spearman_workspace": (_c_sz, [_c_i64]),
     "vr_bootstrap_spearman_f32": (
         ctypes.c_int,

@@ -16,6 +16,7 @@ fallback: without a HIP device these functions raise.
 """
 from __future__ import annotations
 
+import ctypes
 import logging
 import math
 from typing import TYPE_CHECKING, Dict, List, Optional, Sequence, Tuple
@@ -39,6 +40,7 @@ __all__ = [
     "bootstrap_rsa",
     "RankPlan",
     "bootstrap_spearman",
+    "bootstrap_spearman_multi",
     "bootstrap_kendall",
     "percentile",
     "_rank",
@@ -184,6 +186,44 @@ def bootstrap_spearman(
                 _ptr(scores), _ptr(ws), ws.numel(), stream_of(dev),
             ),
             "vr_bootstrap_spearman_plans",
+        )
+    return scores
+
+
+def bootstrap_spearman_multi(
+    plan_a: RankPlan,
+    plans_b: Sequence[RankPlan],
+    idx: Optional[np.ndarray | torch.Tensor],
+    *,
+    full_first: bool = True,
+) -> torch.Tensor:
+    """Spearman of every plan in plans_b against plan_a on the same subsets:
+    (len(plans_b), total) float64 scores on the device. Row j equals
+    bootstrap_spearman(plans_b[j], plan_a, idx) bit for bit; plan_a's rank walk runs
+    once per pass of 64 subsets for all of them (a neural RDM against every layer)."""
+    plans_b = list(plans_b)
+    for pb in plans_b:
+        if pb.n != plan_a.n or pb.device != plan_a.device:
+            raise ValueError("rank plans must describe RDMs of the same size and device")
+    dev, n = plan_a.device, plan_a.n
+    idx_t = _idx_tensor(idx, dev)
+    n_sets, k = (int(idx_t.size(0)), int(idx_t.size(1))) if idx_t.numel() else (0, 0)
+    total = n_sets + (1 if full_first else 0)
+    nb = len(plans_b)
+    scores = torch.empty((nb, total), dtype=torch.float64, device=dev)
+    if total == 0 or nb == 0:
+        return scores
+    L = lib()
+    ws = workspace.get(dev, L.vr_bootstrap_multi_workspace(n, nb), "engine")
+    ptrs = (ctypes.c_void_p * nb)(*[_ptr(pb.buf) for pb in plans_b])
+    with torch.cuda.device(dev):
+        check(
+            L.vr_bootstrap_spearman_multi(
+                _ptr(plan_a.buf), ctypes.cast(ptrs, ctypes.c_void_p), nb, n,
+                _ptr(idx_t) if idx_t.numel() else None, k, n_sets, int(full_first),
+                _ptr(scores), total, _ptr(ws), ws.numel(), stream_of(dev),
+            ),
+            "vr_bootstrap_spearman_multi",
         )
     return scores
 

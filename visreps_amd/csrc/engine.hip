@@ -669,39 +669,54 @@ __global__ void k_fill_nan(double* out, int64_t count) {
 // ---------------------------------------------------------------------------------
 // host orchestration
 // ---------------------------------------------------------------------------------
-template <bool LDS, bool FULL, typename TBT, bool BTA, bool BTB>
-static int set_lds_attr() {
-  static bool done = false;
-  if (LDS && !done) {
-    const int mx = 160 * 1024;
-    VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_rankA<LDS, FULL, TBT, BTA>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, mx));
-    VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_rankB<LDS, FULL, TBT, BTB>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, mx));
-    done = true;
-  }
+template <typename K>
+static int allow_big_lds(K kernel) {
+  VR_CHECK_HIP(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024));
   return VR_OK;
 }
 
-template <bool LDS, bool FULL, typename TBT, bool BTA, bool BTB>
-static int run_pass(const PlanView& A, const PlanView& B, int64_t n, const EngineWs& E, int lw,
-                    int nl, double* scores_out, const EngineCfg& cfg, hipStream_t st) {
+// A side of a pass (shared by every B plan of the call): TB rows in A order, chunk bases
+// baseA, A segment tie sums and the included-pair totals totA.
+template <bool LDS, bool FULL, typename TBT, bool BTA>
+static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const EngineCfg& cfg,
+                  hipStream_t st) {
+  static bool attr = false;
+  if (LDS && !attr) {
+    VR_TRY(allow_big_lds(k_rankA<LDS, FULL, TBT, BTA>));
+    attr = true;
+  }
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = (uint32_t)cfg.nwaves;
-  VR_TRY((set_lds_attr<LDS, FULL, TBT, BTA, BTB>()));
-  TBT* TB = static_cast<TBT*>(E.TB);
   k_rankA<LDS, FULL, TBT, BTA><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
-      A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, TB, lw, E.lpA, E.segA_tot,
-      E.segA_part, nseg);
+      A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<TBT*>(E.TB), lw, E.lpA,
+      E.segA_tot, E.segA_part, nseg);
   VR_CHECK_LAUNCH();
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
   const size_t nb = ((size_t)nch * LANES + 255) / 256;
   k_add_base<<<(unsigned)nb, 256, 0, st>>>(E.lpA, E.segA_pre, nch, nseg, E.baseA);
   VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+// B side of a pass for one B plan, joined to A by (posA_byB, chunkA_byB): the nl scores
+// of the pass.
+template <bool LDS, bool FULL, typename TBT, bool BTB>
+static int pass_b(const PlanView& A, const PlanView& B, const uint32_t* posA_byB,
+                  const uint32_t* chunkA_byB, int64_t n, const EngineWs& E, int lw, int nl,
+                  double* scores_out, const EngineCfg& cfg, hipStream_t st) {
+  static bool attr = false;
+  if (LDS && !attr) {
+    VR_TRY(allow_big_lds(k_rankB<LDS, FULL, TBT, BTB>));
+    attr = true;
+  }
+  const int64_t M = pairs_of(n);
+  const uint32_t nch = plan_nchunks(M);
+  const uint32_t nseg = (uint32_t)cfg.nwaves;
   k_rankB<LDS, FULL, TBT, BTB><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
-      B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, TB, lw, E.posA_byB, E.chunkA_byB,
-      E.baseA, E.segB_tot, E.segB_part, nseg);
+      B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
+      posA_byB, chunkA_byB, E.baseA, E.segB_tot, E.segB_part, nseg);
   VR_CHECK_LAUNCH();
   VR_TRY(lane_scan(E.segB_tot, nseg, E.bsum, E.segB_pre, nullptr, st));
   const uint32_t nsb = scan_blocks(nseg);
@@ -712,75 +727,110 @@ static int run_pass(const PlanView& A, const PlanView& B, int64_t n, const Engin
   return VR_OK;
 }
 
-// runtime plan properties -> kernel instantiation
-struct PassKind {
-  bool lds, full, narrow, bigA, bigB;
+// compile-time pass variant: masks in LDS, all 64 lanes, TB element type
+template <bool L, bool F, typename T>
+struct PassTag {
+  static constexpr bool lds = L, full = F;
+  using tbt = T;
 };
+template <class Fn>
+static int with_pass_tag(bool lds, bool full, bool narrow, Fn&& fn) {
+  if (lds) {
+    if (full) return narrow ? fn(PassTag<true, true, uint16_t>{}) : fn(PassTag<true, true, uint32_t>{});
+    return narrow ? fn(PassTag<true, false, uint16_t>{}) : fn(PassTag<true, false, uint32_t>{});
+  }
+  if (full) return narrow ? fn(PassTag<false, true, uint16_t>{}) : fn(PassTag<false, true, uint32_t>{});
+  return narrow ? fn(PassTag<false, false, uint16_t>{}) : fn(PassTag<false, false, uint32_t>{});
+}
 
-template <bool LDS, bool FULL, typename TBT, bool BTA>
-static int dispatch_btb(const PassKind& k, const PlanView& A, const PlanView& B, int64_t n,
-                        const EngineWs& E, int lw, int nl, double* out, const EngineCfg& cfg,
-                        hipStream_t st) {
-  return k.bigB ? run_pass<LDS, FULL, TBT, BTA, true>(A, B, n, E, lw, nl, out, cfg, st)
-                : run_pass<LDS, FULL, TBT, BTA, false>(A, B, n, E, lw, nl, out, cfg, st);
-}
-template <bool LDS, bool FULL, typename TBT>
-static int dispatch_bta(const PassKind& k, const PlanView& A, const PlanView& B, int64_t n,
-                        const EngineWs& E, int lw, int nl, double* out, const EngineCfg& cfg,
-                        hipStream_t st) {
-  return k.bigA ? dispatch_btb<LDS, FULL, TBT, true>(k, A, B, n, E, lw, nl, out, cfg, st)
-                : dispatch_btb<LDS, FULL, TBT, false>(k, A, B, n, E, lw, nl, out, cfg, st);
-}
-template <bool LDS, bool FULL>
-static int dispatch_tb(const PassKind& k, const PlanView& A, const PlanView& B, int64_t n,
-                       const EngineWs& E, int lw, int nl, double* out, const EngineCfg& cfg,
-                       hipStream_t st) {
-  return k.narrow ? dispatch_bta<LDS, FULL, uint16_t>(k, A, B, n, E, lw, nl, out, cfg, st)
-                  : dispatch_bta<LDS, FULL, uint32_t>(k, A, B, n, E, lw, nl, out, cfg, st);
-}
-static int dispatch_pass(const PassKind& k, const PlanView& A, const PlanView& B, int64_t n,
-                         const EngineWs& E, int lw, int nl, double* out, const EngineCfg& cfg,
-                         hipStream_t st) {
-  if (k.lds)
-    return k.full ? dispatch_tb<true, true>(k, A, B, n, E, lw, nl, out, cfg, st)
-                  : dispatch_tb<true, false>(k, A, B, n, E, lw, nl, out, cfg, st);
-  return k.full ? dispatch_tb<false, true>(k, A, B, n, E, lw, nl, out, cfg, st)
-                : dispatch_tb<false, false>(k, A, B, n, E, lw, nl, out, cfg, st);
+// One A plan against nb B plans (one unit each). Per pass of 64 subsets the A side runs
+// once and every B side reads its TB rows, so a plan shared by several units (a neural
+// RDM against every model layer, evals.py:323-373 loops regions x layers) pays its rank
+// walk once per pass. Spearman is symmetric in its two arguments and every sum is exact,
+// so scores equal the per-unit calls bit for bit.
+// Scores of B j: scores[j * score_ld + s] for the `total` subsets (full set first if
+// full_first), 64 per pass. joins: nb pairs of M-element (posA_byB, chunkA_byB) arrays.
+static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, int64_t n,
+                            const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
+                            double* scores, int64_t score_ld, uint32_t* const* joins,
+                            const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st) {
+  const int64_t M = pairs_of(n);
+  const int64_t total = n_sets + (full_first ? 1 : 0);
+  if (total == 0 || nb == 0) return VR_OK;
+  if (M == 0) {  // no pairs: every score is NaN (scipy on empty input)
+    for (int64_t j = 0; j < nb; ++j) {
+      k_fill_nan<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(scores + j * score_ld, total);
+      VR_CHECK_LAUNCH();
+    }
+    return VR_OK;
+  }
+  // u16 chunk-relative ranks y~ <= 2 span + 1 need every chunk span (< L + largest tie
+  // group of A) <= 32767; 64-bit tie sums need every group below 2^16
+  std::vector<PlanHeader> h((size_t)nb + 1);
+  VR_CHECK_HIP(hipMemcpyAsync(&h[0], A.hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
+  for (int64_t j = 0; j < nb; ++j)
+    VR_CHECK_HIP(hipMemcpyAsync(&h[(size_t)j + 1], Bs[j].hdr, sizeof(PlanHeader),
+                                hipMemcpyDeviceToHost, st));
+  VR_CHECK_HIP(hipStreamSynchronize(st));
+  const bool narrow = (uint64_t)PLAN_L + h[0].max_group <= 32767u;
+  const bool bigA = h[0].max_group >= 65536u;
+  for (int64_t j = 0; j < nb; ++j) {
+    k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(Bs[j].codes, M, n, A.pos_of_pair,
+                                                       A.chunk_of_pair, joins[2 * j], joins[2 * j + 1]);
+    VR_CHECK_LAUNCH();
+  }
+  return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
+    using Tg = decltype(tag);
+    using TBT = typename Tg::tbt;
+    for (int64_t set0 = 0; set0 < total; set0 += lw) {
+      const int nl = (int)std::min<int64_t>(lw, total - set0);
+      VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
+      VR_TRY((bigA ? pass_a<Tg::lds, Tg::full, TBT, true>(A, n, E, lw, cfg, st)
+                   : pass_a<Tg::lds, Tg::full, TBT, false>(A, n, E, lw, cfg, st)));
+      for (int64_t j = 0; j < nb; ++j) {
+        double* out = scores + j * score_ld + set0;
+        const uint32_t* pj = joins[2 * j];
+        const uint32_t* cj = joins[2 * j + 1];
+        VR_TRY((h[(size_t)j + 1].max_group >= 65536u
+                    ? pass_b<Tg::lds, Tg::full, TBT, true>(A, Bs[j], pj, cj, n, E, lw, nl, out, cfg, st)
+                    : pass_b<Tg::lds, Tg::full, TBT, false>(A, Bs[j], pj, cj, n, E, lw, nl, out, cfg, st)));
+      }
+    }
+    return VR_OK;
+  });
 }
 
 // Scores for `total` subsets (full set first if full_first), 64 per pass.
 static int run_engine(const PlanView& A, const PlanView& B, int64_t n, const int32_t* idx,
                       int64_t k, int64_t n_sets, int full_first, double* scores,
                       const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st) {
+  uint32_t* joins[2] = {E.posA_byB, E.chunkA_byB};
+  return run_engine_multi(A, &B, 1, n, idx, k, n_sets, full_first, scores, 0, joins, E, lw, cfg, st);
+}
+
+// Workspace of the multi-B engine: the engine scratch, then the joins of B 1..nb-1 (B 0
+// uses the engine's own join arrays).
+static size_t multi_layout(void* base, int64_t n, int64_t nb, int nwaves, EngineWs* E,
+                           std::vector<uint32_t*>* joins) {
+  size_t eb = 0;
+  const EngineWs e = engine_layout(base, n, LANES, nwaves, &eb);
   const int64_t M = pairs_of(n);
-  const int64_t total = n_sets + (full_first ? 1 : 0);
-  if (total == 0) return VR_OK;
-  if (M == 0) {  // no pairs: every score is NaN (scipy on empty input)
-    k_fill_nan<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(scores, total);
-    VR_CHECK_LAUNCH();
-    return VR_OK;
+  Carver c(base ? static_cast<char*>(base) + eb : nullptr);
+  if (joins) joins->assign((size_t)std::max<int64_t>(nb, 1) * 2, nullptr);
+  if (joins && nb > 0) {
+    (*joins)[0] = e.posA_byB;
+    (*joins)[1] = e.chunkA_byB;
   }
-  // u16 chunk-relative ranks y~ <= 2 span + 1 need every chunk span (< L + largest tie
-  // group of A) <= 32767; 64-bit tie sums need every group below 2^16
-  PlanHeader h[2];
-  VR_CHECK_HIP(hipMemcpyAsync(&h[0], A.hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
-  VR_CHECK_HIP(hipMemcpyAsync(&h[1], B.hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
-  VR_CHECK_HIP(hipStreamSynchronize(st));
-  PassKind kind;
-  kind.lds = cfg.use_lds;
-  kind.full = lw == LANES;
-  kind.narrow = (uint64_t)PLAN_L + h[0].max_group <= 32767u;
-  kind.bigA = h[0].max_group >= 65536u;
-  kind.bigB = h[1].max_group >= 65536u;
-  k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(B.codes, M, n, A.pos_of_pair,
-                                                     A.chunk_of_pair, E.posA_byB, E.chunkA_byB);
-  VR_CHECK_LAUNCH();
-  for (int64_t set0 = 0; set0 < total; set0 += lw) {
-    const int nl = (int)std::min<int64_t>(lw, total - set0);
-    VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
-    VR_TRY(dispatch_pass(kind, A, B, n, E, lw, nl, scores + set0, cfg, st));
+  for (int64_t j = 1; j < nb; ++j) {
+    uint32_t* p = c.take<uint32_t>((size_t)M);
+    uint32_t* q = c.take<uint32_t>((size_t)M);
+    if (joins) {
+      (*joins)[2 * j] = p;
+      (*joins)[2 * j + 1] = q;
+    }
   }
-  return VR_OK;
+  if (E) *E = e;
+  return eb + c.bytes();
 }
 
 static size_t oneshot_bytes(int64_t n, int lw, int nwaves, void* base, PlanView* A, PlanView* B,
@@ -833,6 +883,43 @@ int vr_bootstrap_spearman_plans(const void* planA, const void* planB, int64_t n,
   PlanView A = plan_layout(const_cast<void*>(planA), n);
   PlanView B = plan_layout(const_cast<void*>(planB), n);
   return run_engine(A, B, n, idx, k, n_sets, full_first, scores, E, LANES, cfg, as_stream(stream));
+}
+
+size_t vr_bootstrap_multi_workspace(int64_t n, int64_t n_b) {
+  n = n < 0 ? 0 : n;
+  n_b = n_b < 1 ? 1 : n_b;
+  return multi_layout(nullptr, n, n_b, engine_cfg(n).nwaves, nullptr, nullptr);
+}
+
+int vr_bootstrap_spearman_multi(const void* planA, const void* const* planBs, int64_t n_b, int64_t n,
+                                const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
+                                double* scores, int64_t ld_scores, void* ws, size_t ws_bytes,
+                                void* stream) {
+  VR_REQUIRE(n >= 0 && n <= 65535, "vr_bootstrap_spearman_multi: n=%lld out of range", (long long)n);
+  VR_REQUIRE(n_b >= 0, "vr_bootstrap_spearman_multi: n_b=%lld", (long long)n_b);
+  VR_REQUIRE(planA && (n_b == 0 || (planBs && scores)), "vr_bootstrap_spearman_multi: null pointer");
+  VR_REQUIRE(k >= 0 && k <= n && n_sets >= 0, "vr_bootstrap_spearman_multi: bad k=%lld sets=%lld",
+             (long long)k, (long long)n_sets);
+  VR_REQUIRE(idx != nullptr || n_sets == 0 || k == 0, "vr_bootstrap_spearman_multi: null idx");
+  const int64_t total = n_sets + (full_first ? 1 : 0);
+  VR_REQUIRE(n_b <= 1 || ld_scores >= total, "vr_bootstrap_spearman_multi: ld_scores %lld < %lld",
+             (long long)ld_scores, (long long)total);
+  for (int64_t j = 0; j < n_b; ++j)
+    VR_REQUIRE(planBs[j] != nullptr, "vr_bootstrap_spearman_multi: planBs[%lld] is null", (long long)j);
+  const EngineCfg cfg = engine_cfg(n);
+  const size_t need = multi_layout(nullptr, n, n_b, cfg.nwaves, nullptr, nullptr);
+  if (ws_bytes < need || ws == nullptr) {
+    set_error("vr_bootstrap_spearman_multi: workspace %zu < %zu", ws_bytes, need);
+    return VR_EWORKSPACE;
+  }
+  EngineWs E;
+  std::vector<uint32_t*> joins;
+  multi_layout(ws, n, n_b, cfg.nwaves, &E, &joins);
+  const PlanView A = plan_layout(const_cast<void*>(planA), n);
+  std::vector<PlanView> Bs;
+  for (int64_t j = 0; j < n_b; ++j) Bs.push_back(plan_layout(const_cast<void*>(planBs[j]), n));
+  return run_engine_multi(A, Bs.data(), n_b, n, idx, k, n_sets, full_first, scores, ld_scores,
+                          joins.data(), E, LANES, cfg, as_stream(stream));
 }
 
 size_t vr_bootstrap_spearman_workspace(int64_t n) {

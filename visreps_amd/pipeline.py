@@ -44,11 +44,11 @@ class StepTimes:
     engine_calls: int = 0
     _pending: list = field(default_factory=list)
 
-    def record(self, kind: str, start, end, work: float):
-        self._pending.append((kind, start, end, work))
+    def record(self, kind: str, start, end, work: float, calls: int = 1):
+        self._pending.append((kind, start, end, work, calls))
 
     def resolve(self):
-        for kind, s, e, w in self._pending:
+        for kind, s, e, w, c in self._pending:
             ms = s.elapsed_time(e)
             if kind == "gram":
                 self.gram_ms += ms
@@ -56,7 +56,7 @@ class StepTimes:
             else:
                 self.engine_ms += ms
                 self.engine_bytes += w
-                self.engine_calls += 1
+                self.engine_calls += c
         self._pending.clear()
 
 
@@ -190,6 +190,30 @@ def run_unit(plan_m: R.RankPlan, plan_n: R.RankPlan, idx: Optional[np.ndarray],
     return scores
 
 
+def run_group(plan_n: R.RankPlan, plans_m: Sequence[R.RankPlan], idx: Optional[np.ndarray],
+              times: Optional[StepTimes] = None) -> torch.Tensor:
+    """Units (m, n) for every model plan m against one neural plan n in one engine call:
+    (len(plans_m), 1 + n_boot) scores; the neural plan's rank walk is shared."""
+    ev = None
+    if times is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    scores = R.bootstrap_spearman_multi(plan_n, plans_m, idx, full_first=True)
+    if times is not None:
+        ev[1].record()
+        nb = 0 if idx is None else len(idx)
+        times.record("engine", ev[0], ev[1], engine_bytes(plan_n.n, nb) * len(plans_m),
+                     calls=len(plans_m))
+    return scores
+
+
+def unit_split(units: Sequence, world: int) -> List[Tuple[int, int]]:
+    """Contiguous, near-equal [lo, hi) ranges of the unit list, one per rank."""
+    u = len(units)
+    b = [round(r * u / world) for r in range(world + 1)]
+    return [(b[r], b[r + 1]) for r in range(world)]
+
+
 def summarize(scores: np.ndarray, bootstrap: bool) -> Dict:
     point = float(scores[0])
     res = {"score": point, "ci_low": None, "ci_high": None}
@@ -204,38 +228,51 @@ def summarize(scores: np.ndarray, bootstrap: bool) -> Dict:
 def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[str],
                   neural_rdms: Dict[str, torch.Tensor], n: int, *, n_boot: int = 1000,
                   seed: int = 42, pg=None, times: Optional[StepTimes] = None,
-                  keep_plans: bool = False, plan_fn=None, unit_fn=None
+                  keep_plans: bool = False, plan_fn=None, unit_fn=None, group_fn=None
                   ) -> Dict[Tuple[str, str], Dict]:
-    """Point + bootstrap Spearman RSA for every (point, region) unit; units round-robin
-    over ranks; returns the per-unit results on every rank. plan_fn / unit_fn default to
-    RankPlan / run_unit (the HIP engine)."""
+    """Point + bootstrap Spearman RSA for every (point, region) unit; returns the
+    per-unit results on every rank.
+
+    Units are listed region-major and cut into one contiguous range per rank, so a
+    rank's units come in groups that share a neural RDM; each group is one engine call
+    (run_group: the neural plan's rank walk is shared by the group's layers). plan_fn /
+    group_fn default to RankPlan / run_group (the HIP engine); a per-unit unit_fn(model
+    plan, neural plan, idx, times) may be given instead of group_fn."""
     plan_fn = plan_fn or R.RankPlan
-    unit_fn = unit_fn or run_unit
+    if group_fn is None:
+        if unit_fn is not None:
+            def group_fn(pn, pms, idx_, t):
+                return [np.asarray(torch.as_tensor(unit_fn(pm, pn, idx_, t)).cpu()) for pm in pms]
+        else:
+            group_fn = run_group
     rank, world = _world(pg)
     regions = list(neural_rdms)
-    units = [(p, r) for p in points for r in regions]
-    mine = [u for i, u in enumerate(units) if i % world == rank]
+    units = [(p, r) for r in regions for p in points]
+    lo, hi = unit_split(units, world)[rank]
+    mine = units[lo:hi]
     k = int(0.9 * n)
     idx = None
     if n_boot > 0:  # one upload of the (n_boot, k) index sets, shared by every unit
         dev = next(iter(neural_rdms.values())).device
         idx = torch.from_numpy(np.array(bootstrap_indices(seed, n, k, n_boot))).to(dev)
-    nplans = {}
     local: Dict[Tuple[str, str], np.ndarray] = {}
-    by_point: Dict[str, List[str]] = {}
-    for p, r in mine:
-        by_point.setdefault(p, []).append(r)
+    need = {p for p, _ in mine}
+    mplans = {}
     for p in points:
         rdm = model_rdm_fn(p)  # collective: every rank takes part in every point's RDM
-        if p not in by_point:
-            del rdm
-            continue
-        pm = plan_fn(rdm)
+        if p in need:
+            mplans[p] = plan_fn(rdm)
         del rdm
-        for r in by_point[p]:
-            if r not in nplans:
-                nplans[r] = plan_fn(neural_rdms[r])
-            local[(p, r)] = np.asarray(torch.as_tensor(unit_fn(pm, nplans[r], idx, times)).cpu())
+    by_region: Dict[str, List[str]] = {}
+    for p, r in mine:
+        by_region.setdefault(r, []).append(p)
+    for r, pts in by_region.items():
+        pn = plan_fn(neural_rdms[r])
+        out = group_fn(pn, [mplans[p] for p in pts], idx, times)
+        for j, p in enumerate(pts):
+            local[(p, r)] = np.asarray(torch.as_tensor(out[j]).cpu())
+        del pn
+    del mplans
     if world > 1:
         gathered: List[Dict] = [None] * world
         dist.all_gather_object(gathered, local, group=pg)
