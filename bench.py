@@ -44,6 +44,7 @@ METRIC = "end-to-end RSA eval sec (extract→RDM→1000-bootstrap Spearman), N=1
 LAYERS = ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: FP32 matrix 157.3 TFLOP/s spec
+BF16_MFMA_PEAK_TF = 2516.6  # MI355X_MICROARCH.md / SURVEY §8(d): BF16 dense matrix peak
 
 
 def log(*a):
@@ -193,9 +194,15 @@ def main():
                 "kernel": "bootstrap engine pass chain (vr_bootstrap_spearman_plans, one call per unit)",
                 "algorithmic_bytes_per_call": per_launch,
                 "avg_call_ms": round(times.engine_ms / max(1, times.engine_calls), 3)}
-        roof_gram = {"bound": "mfma", "achieved": round(gram_tf, 2), "peak": FP32_MFMA_PEAK_TF,
-                     "unit": "TFLOP/s", "frac": round(gram_tf / FP32_MFMA_PEAK_TF, 4),
-                     "kernel": "k_gram (fp32 v_mfma_f32_32x32x2_f32)",
+        if os.environ.get("VISREPS_GRAM") == "fp32":
+            gpeak, gkern = FP32_MFMA_PEAK_TF, "k_gram (exact fp32, v_mfma_f32_32x32x2_f32)"
+        else:  # 3 bf16 MFMA products per algorithmic FLOP: ceiling = bf16 dense peak / 3
+            gpeak = round(BF16_MFMA_PEAK_TF / 3, 1)
+            gkern = ("k_gram3 (centred rows split hi+lo bf16, 3 x v_mfma_f32_32x32x16_bf16 "
+                     "per k-step, fp32 accumulate; peak = bf16 dense peak / 3)")
+        roof_gram = {"bound": "mfma", "achieved": round(gram_tf, 2), "peak": gpeak,
+                     "unit": "TFLOP/s", "frac": round(gram_tf / gpeak, 4), "kernel": gkern,
+                     "algorithmic_flops": "N(N+1)D per RDM",
                      "ms_per_step": round(times.gram_ms / args.steps, 2)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -216,7 +223,9 @@ def main():
             "higher_is_better": False,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32 (Gram) / exact int (ranks)",
+            "dtype": ("f32 Gram" if os.environ.get("VISREPS_GRAM") == "fp32" else
+                      "bf16x3-split Gram, fp32 accumulate (max |dRDM| vs fp64 <= 5e-6)")
+                     + " / exact int ranks, fp64 statistic",
             "data": "synthetic (seeded images + NSD-shaped ROI responses; random-init CustomCNN)",
             "config": {"workload": "configs[1]: CustomCNN 14 points x 4 NSD ROIs, N=10k, 1000-bootstrap Spearman RSA",
                        "n_stimuli": N, "points": len(points), "rois": list(NSD_ROIS_4),

@@ -212,7 +212,40 @@ def test_bootstrap_end_to_end_tolerance(dev):
     assert abs(lo - rlo) < 1e-5 and abs(hi - rhi) < 1e-5
 
 
-@pytest.mark.parametrize("n,d,world", [(300, 70, 3), (1000, 40, 4), (2100, 33, 5), (4000, 64, 2)])
+def _rdm_f64(x: np.ndarray) -> np.ndarray:
+    xc = x.astype(np.float64) - x.astype(np.float64).mean(1, keepdims=True)
+    s = np.sqrt((xc * xc).mean(1) + 1e-12)
+    c = np.clip((xc @ xc.T) / x.shape[1] / (np.outer(s, s) + 1e-12), -1, 1)
+    np.fill_diagonal(c, 1.0)
+    return 1.0 - c
+
+
+@pytest.mark.parametrize("n,d", [(256, 43264), (700, 4096), (130, 257), (1000, 290)])
+def test_rdm_split_gram_accuracy_vs_fp64(dev, n, d, monkeypatch):
+    # the bf16 hi/lo split Gram (default) and the exact-fp32 MFMA kernel (VISREPS_GRAM=fp32)
+    # against an fp64 reference: the split kernel within 5e-6 (observed: 6.7e-7 at n=256,
+    # D=43264; 1.8e-6 at D=257), the fp32 kernel within 1e-6 (observed 1.2e-7-1.8e-7),
+    # both inside the 2e-5 RDM tolerance
+    feats = O.synthetic_features(n, [d], seed=d % 97, relu=[True])[0]
+    ref = _rdm_f64(feats)
+    x = torch.from_numpy(feats).to(dev)
+    split = R.compute_rdm(x).double().cpu().numpy()
+    monkeypatch.setenv("VISREPS_GRAM", "fp32")
+    exact = R.compute_rdm(x).double().cpu().numpy()
+    e_split, e_exact = np.abs(split - ref).max(), np.abs(exact - ref).max()
+    assert e_split <= 5e-6 and e_exact <= 1e-6, (e_split, e_exact)
+    assert np.array_equal(split, split.T) and np.all(np.diag(split) == 0)
+
+
+@pytest.mark.parametrize("n,d", [(3, 7), (130, 257), (300, 1000)])
+def test_rdm_fp32_kernel_matches_oracle(dev, n, d, monkeypatch):
+    monkeypatch.setenv("VISREPS_GRAM", "fp32")
+    x = np.random.RandomState(n).randn(n, d).astype(np.float32)
+    got = R.compute_rdm(torch.from_numpy(x).to(dev)).cpu().numpy()
+    assert np.max(np.abs(got - O.compute_rdm(x))) <= 2e-5
+
+
+@pytest.mark.parametrize("n,d,world",[(300, 70, 3), (1000, 40, 4), (2100, 33, 5), (4000, 64, 2)])
 def test_rdm_tile_ranges_assemble_full_rdm(dev, n, d, world):
     # the block-distributed Gram (band launch order inside each rank's tile range) writes
     # every entry of its range exactly as the one-launch RDM does

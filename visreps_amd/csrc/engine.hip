@@ -34,7 +34,10 @@
 
 namespace vr {
 
-constexpr int ENG_THREADS = 1024;  // 16 waves per workgroup share one LDS mask table
+#ifndef VR_ENG_THREADS
+#define VR_ENG_THREADS 1024
+#endif
+constexpr int ENG_THREADS = VR_ENG_THREADS;  // waves per workgroup share one LDS mask table
 constexpr int WAVES_PER_WG = ENG_THREADS / 64;
 constexpr int SCAN_SEGS = 256;     // segments per block in the segment scans / final fold
 

@@ -12,6 +12,9 @@
 //                of each 128x32 panel; the epilogue writes the tile and its mirror.
 //                Split-K over d when the tile count cannot fill 256 CUs, with fp32
 //                partial tiles reduced in fixed order by k_gram_reduce.  [MFMA-bound]
+#include <cstdlib>
+#include <cstring>
+
 #include "internal.h"
 
 namespace vr {
@@ -113,6 +116,8 @@ struct GramParams {
   int tile_count;   // tiles in this launch
   float correction;
   int vec;          // 16-B aligned rows: float4 staging
+  const uint16_t* planes;  // split Gram: bf16 hi/lo stage records (null: fp32 kernel)
+  int64_t nstage;          // 32-k stages per plane row
 };
 
 __device__ inline void tile_coords(int p, int T, int& bi, int& bj) {
@@ -126,6 +131,55 @@ __device__ inline void tile_coords(int p, int T, int& bi, int& bj) {
   while (r + 1 < T && off(r + 1) <= p) ++r;
   bi = r;
   bj = r + (p - off(r));
+}
+
+// Launch order of the tiles [t0, t0 + count) of the row-major upper-triangle numbering:
+// bands of GBAND tile rows (counted from the range's first row), each band walked column
+// by column. After xcd_remap one XCD runs consecutive positions, so the ~64 blocks it
+// holds at once share ~GBAND row panels and ~GBAND column panels in its L2 instead of
+// one row panel and ~64 column panels. Position p -> tile (bi, bj); a bijection on the
+// range, so any contiguous tile range (block-distributed Gram) keeps its exact tile set.
+constexpr int GBAND = 8;
+
+__device__ inline int64_t tri_row_start(int r, int T) {
+  return (int64_t)r * T - (int64_t)r * (r - 1) / 2;
+}
+
+__device__ inline void band_tile(int p, int t0, int count, int T, int& bi, int& bj) {
+  int ra, ca, rz, cz, r, c;
+  tile_coords(t0, T, ra, ca);
+  tile_coords(t0 + count - 1, T, rz, cz);
+  tile_coords(t0 + p, T, r, c);
+  const int i0 = ra + (r - ra) / GBAND * GBAND;
+  const int i1 = min(rz, i0 + GBAND - 1);
+  const int64_t gs = (i0 == ra) ? (int64_t)t0 : tri_row_start(i0, T);
+  const int q = (int)((int64_t)t0 + p - gs);
+  // columns [lo(i), hi(i)) of band row i inside the range
+  auto lo = [&](int i) { return i == ra ? ca : i; };
+  auto hi = [&](int i) { return i == rz ? cz + 1 : T; };
+  auto before = [&](int col) {  // band tiles in columns < col
+    int s = 0;
+    for (int i = i0; i <= i1; ++i) s += max(0, min(col, hi(i)) - lo(i));
+    return s;
+  };
+  int a = 0, b = T;  // before(a) <= q < before(b)
+  while (b - a > 1) {
+    const int m = (a + b) >> 1;
+    if (before(m) <= q) a = m; else b = m;
+  }
+  int k = q - before(a);  // the k-th band row holding column a
+  bi = r;
+  bj = c;
+  for (int i = i0; i <= i1; ++i) {
+    if (lo(i) <= a && a < hi(i)) {
+      if (k == 0) {
+        bi = i;
+        bj = a;
+        return;
+      }
+      --k;
+    }
+  }
 }
 
 // Loads this thread's 4 float4 of a 128 x 32 panel (rows row0.., k in [k, k+32)).
@@ -204,14 +258,83 @@ __device__ inline float rdm_value(float g, int64_t i, int64_t j, const GramParam
   return 1.f - c;
 }
 
+// Tile epilogue (one 2x2 grid of 32x32 accumulators per wave). C/D map of the 32x32 MFMAs
+// (fp32 and bf16 alike): col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5). A diagonal
+// tile writes each i < j entry from its (i, j) accumulator to both (i, j) and (j, i), so
+// the RDM is exactly symmetric whatever the product order of the two accumulators.
+__device__ inline void gram_store(const GramParams& P, f32x16 (&acc)[2][2], int64_t row0,
+                                  int64_t col0, bool diag, int split, int ltile) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+  if (P.splits == 1) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        const int64_t j = col0 + wc * 64 + nn * 32 + l32;
+        const float sj = (j < P.n) ? P.stdv[j] : 1.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int64_t ib = row0 + wr * 64 + m * 32 + 8 * g + 4 * h;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t i = ib + e;
+            const float si = (i < P.n) ? P.stdv[i] : 1.f;
+            v[e] = rdm_value(acc[m][nn][4 * g + e], i, j, P, si, sj);
+          }
+          if (diag) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int64_t i = ib + e;
+              if (i <= j && j < P.n) {
+                P.rdm[i * P.ldr + j] = v[e];
+                if (i < j) P.rdm[j * P.ldr + i] = v[e];
+              }
+            }
+            continue;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t i = ib + e;
+            if (i < P.n && j < P.n) P.rdm[i * P.ldr + j] = v[e];
+          }
+          if (j < P.n) {  // mirror: rows ib..ib+3 are 4 consecutive columns of row j
+            float* dst = P.rdm + j * P.ldr + ib;
+            if (P.vec && ib + 3 < P.n && ((P.ldr & 3) == 0)) {
+              f32x4 w = {v[0], v[1], v[2], v[3]};
+              *reinterpret_cast<f32x4*>(dst) = w;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (ib + e < P.n) dst[e] = v[e];
+            }
+          }
+        }
+      }
+  } else {
+    float* out = P.partial + ((int64_t)split * P.tile_count + ltile) * (GT * GT);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        const int lj = wc * 64 + nn * 32 + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int li = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          out[li * GT + lj] = acc[m][nn][r];
+        }
+      }
+  }
+}
+
 __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
   __shared__ __attribute__((aligned(16))) float lds[2 * 2 * G_STAGE];  // [buf][A/B]
   const int nwg = gridDim.x;
   const int id = (int)xcd_remap(blockIdx.x, (uint32_t)nwg);
   const int ltile = id / P.splits, split = id % P.splits;
-  const int tile = P.tile0 + ltile;
   int bi, bj;
-  tile_coords(tile, P.T, bi, bj);
+  band_tile(ltile, P.tile0, P.tile_count, P.T, bi, bj);
   const bool diag = (bi == bj);
   const int64_t row0 = (int64_t)bi * GT, col0 = (int64_t)bj * GT;
   const int64_t k0 = (int64_t)split * P.kslice;
@@ -283,52 +406,153 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
     __syncthreads();
   }
 
-  // C/D map of 32x32 MFMA: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
-  if (P.splits == 1) {
+  gram_store(P, acc, row0, col0, diag, split, ltile);
+}
+
+// ------------------------------------------------------------------------------------
+// Split Gram: the centred rows as two bf16 planes, x - mean = hi + lo with
+// |x - mean - hi - lo| <= 2^-18 |x - mean|, and three bf16 MFMA products per k-step
+// (hi.hi + hi.lo + lo.hi, fp32 accumulate). The dropped lo.lo term and the lo rounding
+// are uncorrelated across k, so a Gram entry's error against the exact centred Gram is
+// ~2^-17 sqrt(sum_k x_ik^2 x_jk^2): below the fp32 summation error of the reference's own
+// sgemm for these shapes. CDNA4's bf16 matrix rate is 16x its fp32 rate.
+// ------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int SROW = 72;              // LDS row: 32 hi + 32 lo bf16 + 8 pad (144 B, conflict-free b128)
+constexpr int S_STAGE = GT * SROW;    // bf16 per panel per stage
+
+// Planes: per row and 32-k stage one 128-byte record [hi k0..31 | lo k0..31]; rows padded
+// to the tile edge and k to the stage with exact zeros (so the Gram kernel has no edges).
+__global__ void k_split3(const float* __restrict__ X, int64_t n, int64_t d, int64_t ldx,
+                         const float* __restrict__ mean, int64_t rows, int64_t nstage,
+                         uint16_t* __restrict__ planes) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (row, stage, 4-k group)
+  const int64_t per_row = nstage * 8;
+  if (t >= rows * per_row) return;
+  const int64_t r = t / per_row, q = t - r * per_row;
+  const int64_t s = q >> 3;
+  const int g = (int)(q & 7);
+  const int64_t k = s * GK + g * 4;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (r < n) {
+    const float m = mean[r];
+    const float* src = X + r * ldx + k;
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int nn = 0; nn < 2; ++nn) {
-        const int64_t j = col0 + wc * 64 + nn * 32 + l32;
-        const float sj = (j < P.n) ? P.stdv[j] : 1.f;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int64_t ib = row0 + wr * 64 + m * 32 + 8 * g + 4 * h;
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int64_t i = ib + e;
-            const float si = (i < P.n) ? P.stdv[i] : 1.f;
-            v[e] = rdm_value(acc[m][nn][4 * g + e], i, j, P, si, sj);
-            if (i < P.n && j < P.n) P.rdm[i * P.ldr + j] = v[e];
-          }
-          if (!diag && j < P.n) {  // mirror: rows ib..ib+3 are 4 consecutive columns of row j
-            float* dst = P.rdm + j * P.ldr + ib;
-            if (P.vec && ib + 3 < P.n && ((P.ldr & 3) == 0)) {
-              f32x4 w = {v[0], v[1], v[2], v[3]};
-              *reinterpret_cast<f32x4*>(dst) = w;
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                if (ib + e < P.n) dst[e] = v[e];
-            }
-          }
-        }
-      }
-  } else {
-    float* out = P.partial + ((int64_t)split * P.tile_count + ltile) * (GT * GT);
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int nn = 0; nn < 2; ++nn) {
-        const int lj = wc * 64 + nn * 32 + l32;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int li = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          out[li * GT + lj] = acc[m][nn][r];
-        }
-      }
+    for (int e = 0; e < 4; ++e)
+      if (k + e < d) v[e] = src[e] - m;
   }
+  uint32_t hw[2], lw[2];
+#pragma unroll
+  for (int e = 0; e < 4; e += 2) {
+    const __bf16 h0 = (__bf16)v[e], h1 = (__bf16)v[e + 1];
+    const __bf16 l0 = (__bf16)(v[e] - (float)h0), l1 = (__bf16)(v[e + 1] - (float)h1);
+    hw[e / 2] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    lw[e / 2] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+  }
+  uint16_t* dst = planes + (r * nstage + s) * 64 + g * 4;
+  *reinterpret_cast<uint2*>(dst) = make_uint2(hw[0], hw[1]);
+  *reinterpret_cast<uint2*>(dst + 32) = make_uint2(lw[0], lw[1]);
+}
+
+// this thread's 4 x 16 B of a panel's stage record block (128 rows x 128 B)
+__device__ inline void load_rec(const GramParams& P, int64_t row0, int64_t st, u32x4 out[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int f = threadIdx.x + G_THREADS * s;
+    const int r = f >> 3, c = f & 7;
+    out[s] = *reinterpret_cast<const u32x4*>(P.planes + ((row0 + r) * P.nstage + st) * 64 + c * 8);
+  }
+}
+
+__device__ inline void store_rec(uint16_t* lds, const u32x4 v[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int f = threadIdx.x + G_THREADS * s;
+    const int r = f >> 3, c = f & 7;
+    *reinterpret_cast<u32x4*>(lds + r * SROW + c * 8) = v[s];
+  }
+}
+
+__global__ __launch_bounds__(G_THREADS, 2) void k_gram3(GramParams P) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * S_STAGE];  // [buf][A/B]
+  const int nwg = gridDim.x;
+  const int id = (int)xcd_remap(blockIdx.x, (uint32_t)nwg);
+  const int ltile = id / P.splits, split = id % P.splits;
+  int bi, bj;
+  band_tile(ltile, P.tile0, P.tile_count, P.T, bi, bj);
+  const bool diag = (bi == bj);
+  const int64_t row0 = (int64_t)bi * GT, col0 = (int64_t)bj * GT;
+  const int64_t k0 = (int64_t)split * P.kslice;
+  const int64_t k1 = min(P.d, k0 + P.kslice);
+  const int64_t st0 = k0 / GK;
+  const int ns = (int)((k1 - k0 + GK - 1) / GK);
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 1, wc = wid & 1, h = lane >> 5, l32 = lane & 31;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  u32x4 ga[4], gb[4];
+  if (ns > 0) {
+    load_rec(P, row0, st0, ga);
+    if (!diag) load_rec(P, col0, st0, gb);
+    store_rec(lds, ga);
+    if (!diag) store_rec(lds + S_STAGE, gb);
+  }
+  __syncthreads();
+
+  for (int kt = 0; kt < ns; ++kt) {
+    const int cur = kt & 1;
+    const uint16_t* As = lds + cur * 2 * S_STAGE;
+    const uint16_t* Bs = diag ? As : As + S_STAGE;
+    const bool more = kt + 1 < ns;
+    if (more) {  // lands under the MFMAs
+      load_rec(P, row0, st0 + kt + 1, ga);
+      if (!diag) load_rec(P, col0, st0 + kt + 1, gb);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {  // k-steps of 16: lane holds k = 16t + 8h + j
+      bf16x8 aH[2], aL[2], bH[2], bL[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const uint16_t* ar = As + (wr * 64 + m * 32 + l32) * SROW + t * 16 + h * 8;
+        const uint16_t* br = Bs + (wc * 64 + m * 32 + l32) * SROW + t * 16 + h * 8;
+        aH[m] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(ar));
+        aL[m] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(ar + 32));
+        bH[m] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(br));
+        bL[m] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(br + 32));
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[m], bH[nn], acc[m][nn], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[m], bL[nn], acc[m][nn], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL[m], bH[nn], acc[m][nn], 0, 0, 0);
+    }
+    if (more) {
+      uint16_t* nxt = lds + (cur ^ 1) * 2 * S_STAGE;
+      store_rec(nxt, ga);
+      if (!diag) store_rec(nxt + S_STAGE, gb);
+    }
+    __syncthreads();
+  }
+  gram_store(P, acc, row0, col0, diag, split, ltile);
 }
 
 // Sums the split partials of one tile in split order and applies the epilogue; the
@@ -336,9 +560,8 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
 __global__ __launch_bounds__(256) void k_gram_reduce(GramParams P) {
   __shared__ float tr[32][33];
   const int ltile = blockIdx.x;
-  const int tile = P.tile0 + ltile;
   int bi, bj;
-  tile_coords(tile, P.T, bi, bj);
+  band_tile(ltile, P.tile0, P.tile_count, P.T, bi, bj);
   const bool diag = (bi == bj);
   const int64_t row0 = (int64_t)bi * GT, col0 = (int64_t)bj * GT;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
@@ -347,8 +570,10 @@ __global__ __launch_bounds__(256) void k_gram_reduce(GramParams P) {
     for (int yy = ty; yy < 32; yy += 8) {
       const int li = si0 + yy, lj = sj0 + tx;
       float g = 0.f;
+      // a diagonal tile takes (i, j) and (j, i) from one accumulator: exact symmetry
+      const int pi = (diag && li > lj) ? lj : li, pj = (diag && li > lj) ? li : lj;
       for (int s = 0; s < P.splits; ++s)
-        g += P.partial[((int64_t)s * P.tile_count + ltile) * (GT * GT) + li * GT + lj];
+        g += P.partial[((int64_t)s * P.tile_count + ltile) * (GT * GT) + pi * GT + pj];
       const int64_t i = row0 + li, j = col0 + lj;
       const float sI = (i < P.n) ? P.stdv[i] : 1.f, sJ = (j < P.n) ? P.stdv[j] : 1.f;
       const float v = rdm_value(g, i, j, P, sI, sJ);
@@ -391,6 +616,32 @@ static void gram_geometry(int64_t n, int64_t d, int64_t count, int& T, int& ntil
   if (splits < 1) splits = 1;
 }
 
+// Gram arithmetic: the bf16 split kernel unless VISREPS_GRAM=fp32 (exact fp32 MFMA).
+// Read per call, so the workspace query and the launch of one call agree.
+static bool gram_split() {
+  const char* e = getenv("VISREPS_GRAM");
+  return !(e && strcmp(e, "fp32") == 0);
+}
+
+// Scratch of one RDM launch over `count` tiles: row stats, split-K partial tiles, and the
+// bf16 plane records of the split kernel.
+static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* base, float** mean,
+                      float** stdv, float** partial, uint16_t** planes) {
+  int T, ntiles, splits;
+  int64_t kslice;
+  gram_geometry(n, d, count, T, ntiles, splits, kslice);
+  Carver c(base);
+  float* m = c.take<float>((size_t)n);
+  float* s = c.take<float>((size_t)n);
+  float* p = splits > 1 ? c.take<float>((size_t)splits * count * GT * GT) : nullptr;
+  uint16_t* pl = split3 ? c.take<uint16_t>((size_t)T * GT * (size_t)((d + GK - 1) / GK) * 64) : nullptr;
+  if (mean) *mean = m;
+  if (stdv) *stdv = s;
+  if (partial) *partial = p;
+  if (planes) *planes = pl;
+  return c.bytes();
+}
+
 }  // namespace vr
 
 using namespace vr;
@@ -399,26 +650,13 @@ extern "C" {
 
 size_t vr_rdm_pearson_workspace(int64_t n, int64_t d) {
   if (n <= 0 || d <= 0) return 256;
-  int T, ntiles, splits;
-  int64_t kslice;
-  gram_geometry(n, d, gram_tiles(n), T, ntiles, splits, kslice);
-  Carver c(nullptr);
-  c.take<float>((size_t)n);
-  c.take<float>((size_t)n);
-  if (splits > 1) c.take<float>((size_t)splits * ntiles * GT * GT);
-  return c.bytes();
+  return gram_ws(n, d, gram_tiles(n), gram_split(), nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
 size_t vr_rdm_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
   if (n <= 0 || d <= 0 || tile_end <= tile_begin) return 256;
-  int T, ntiles, splits;
-  int64_t kslice;
-  gram_geometry(n, d, tile_end - tile_begin, T, ntiles, splits, kslice);
-  Carver c(nullptr);
-  c.take<float>((size_t)n);
-  c.take<float>((size_t)n);
-  if (splits > 1) c.take<float>((size_t)splits * (tile_end - tile_begin) * GT * GT);
-  return c.bytes();
+  return gram_ws(n, d, tile_end - tile_begin, gram_split(), nullptr, nullptr, nullptr, nullptr,
+                 nullptr);
 }
 
 int64_t vr_rdm_tile_count(int64_t n) { return n > 0 ? gram_tiles(n) : 0; }
@@ -476,11 +714,20 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
   gram_geometry(n, d, tile_end - tile_begin, P.T, P.ntiles, P.splits, P.kslice);
   P.tile0 = (int)tile_begin;
   P.tile_count = (int)(tile_end - tile_begin);
-  Carver c(ws);
-  float* mean = c.take<float>((size_t)n);
-  float* stdv = c.take<float>((size_t)n);
-  P.partial = (P.splits > 1) ? c.take<float>((size_t)P.splits * P.tile_count * GT * GT) : nullptr;
+  const bool split3 = gram_split();
+  float *mean, *stdv;
+  uint16_t* planes;
+  gram_ws(n, d, P.tile_count, split3, ws, &mean, &stdv, &P.partial, &planes);
   VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
+  if (split3) {
+    const int64_t rows = (int64_t)P.T * GT, nstage = (d + GK - 1) / GK;
+    const int64_t threads = rows * nstage * 8;
+    k_split3<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(X, n, d, ldx, mean, rows, nstage,
+                                                                planes);
+    VR_CHECK_LAUNCH();
+    P.planes = planes;
+    P.nstage = nstage;
+  }
   P.X = X;
   P.mean = mean;
   P.stdv = stdv;
@@ -494,7 +741,10 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
           ((reinterpret_cast<uintptr_t>(rdm) & 15) == 0);
   if (P.tile_count <= 0) return VR_OK;
   const unsigned nblk = (unsigned)P.tile_count * (unsigned)P.splits;
-  k_gram<<<nblk, G_THREADS, 0, st>>>(P);
+  if (split3)
+    k_gram3<<<nblk, G_THREADS, 0, st>>>(P);
+  else
+    k_gram<<<nblk, G_THREADS, 0, st>>>(P);
   VR_CHECK_LAUNCH();
   if (P.splits > 1) {
     k_gram_reduce<<<(unsigned)P.tile_count, 256, 0, st>>>(P);
