@@ -66,6 +66,22 @@ def extract(extractor: FeatureExtractor, images: torch.Tensor, batch: int):
     return bufs
 
 
+def pmc_traffic():
+    """HBM bytes per unit of the engine from the committed rocprofv3 --pmc passes
+    (FETCH_SIZE + WRITE_SIZE over one multi call, scripts/gpu_pmc.sh + pmc_traffic.py).
+    Counted in a separate profiler run: a PMC pass cannot share this timed run."""
+    path = os.path.join(ROOT, "profiles", "r1_pmc_traffic_v6.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return round(float(d["engine_unit_bytes"])), (
+            "profiles/r1_pmc_traffic_v6.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate "
+            "passes over one 14-unit engine call at N=10k, raw counters (no gfx950 x2 read "
+            "correction: the engine's reads are 2-4 B/lane row gathers, not 16 B/lane streams)")
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def cpu_baseline(n: int, n_boot: int, dims: dict, voxels: dict, model_rdm: torch.Tensor,
                  neural_rdm: torch.Tensor, images: torch.Tensor, model) -> dict:
     """CPU oracle (numpy/scipy port) on a bounded sample, extrapolated to the workload."""
@@ -189,9 +205,12 @@ def main():
         gram_tf = times.gram_flops / (times.gram_ms / 1e3) / 1e12 if times.gram_ms else 0.0
         units_per_rank = math.ceil(len(points) * len(NSD_ROIS_4) / world)
         per_launch = engine_bytes(N, args.boot)
+        traffic, tsrc = pmc_traffic()
         roof = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(eng_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "bootstrap engine pass chain (vr_bootstrap_spearman_plans, one call per unit)",
+                "unit": "GB/s", "frac": round(eng_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": tsrc,
+                "kernel": ("bootstrap engine pass chain (vr_bootstrap_spearman_multi: per pass one "
+                           "A-side rank walk of the neural plan + one B-side walk per unit)"),
                 "algorithmic_bytes_per_call": per_launch,
                 "avg_call_ms": round(times.engine_ms / max(1, times.engine_calls), 3)}
         if os.environ.get("VISREPS_GRAM") == "fp32":

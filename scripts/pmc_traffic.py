@@ -1,7 +1,7 @@
 """HBM traffic per engine call / per Gram launch from the rocprofv3 --pmc passes of
 scripts/gpu_pmc.sh (FETCH_SIZE and WRITE_SIZE, kB). Writes a JSON summary.
 
-  python scripts/pmc_traffic.py gpurun_out/<tag> > profiles/<name>.json
+  python scripts/pmc_traffic.py gpurun_out/<tag> [units per call] > profiles/<name>.json
 """
 import collections
 import csv
@@ -38,10 +38,14 @@ def main(d):
         out[f"gram_launch_{c}"] = sum(g) / len(g) if g else None
     out["engine_call_bytes"] = out["engine_call_FETCH_SIZE"] + out["engine_call_WRITE_SIZE"]
     out["gram_launch_bytes"] = out["gram_launch_FETCH_SIZE"] + out["gram_launch_WRITE_SIZE"]
-    out["gram_config"] = "N=10000, D=43264 fp32"
-    out["engine_config"] = "N=10000, 1001 subsets (point + 1000 bootstrap), 16 passes"
+    nb = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    out["engine_units_per_call"] = nb
+    out["engine_unit_bytes"] = out["engine_call_bytes"] / nb
+    out["gram_config"] = "N=10000, D=43264 fp32 input (split kernel: bf16 hi/lo records)"
+    out["engine_config"] = (f"N=10000, {nb} units per call (one shared neural plan), 1001 subsets "
+                            "(point + 1000 bootstrap), 16 passes")
     json.dump(out, sys.stdout, indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1])  # argv[2]: units per engine call

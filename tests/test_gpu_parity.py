@@ -229,12 +229,27 @@ def test_rdm_split_gram_accuracy_vs_fp64(dev, n, d, monkeypatch):
     feats = O.synthetic_features(n, [d], seed=d % 97, relu=[True])[0]
     ref = _rdm_f64(feats)
     x = torch.from_numpy(feats).to(dev)
+    monkeypatch.setenv("VISREPS_GRAM", "split")
     split = R.compute_rdm(x).double().cpu().numpy()
     monkeypatch.setenv("VISREPS_GRAM", "fp32")
     exact = R.compute_rdm(x).double().cpu().numpy()
     e_split, e_exact = np.abs(split - ref).max(), np.abs(exact - ref).max()
     assert e_split <= 5e-6 and e_exact <= 1e-6, (e_split, e_exact)
     assert np.array_equal(split, split.T) and np.all(np.diag(split) == 0)
+
+
+def test_split_gram_end_to_end_spearman_tolerance(dev, monkeypatch):
+    # RSA scores from split-kernel RDMs vs the CPU path's own RDMs: |dSpearman| < 1e-5
+    monkeypatch.setenv("VISREPS_GRAM", "split")
+    n = 1500
+    feats = O.synthetic_features(n, [8192, 2000], seed=3, relu=[True, False], noise=3.0)
+    gm = R.compute_rdm(torch.from_numpy(feats[0]).to(dev))
+    gn = R.compute_rdm(torch.from_numpy(feats[1]).to(dev))
+    point, scores, lo, hi = R.bootstrap_rsa(gm, gn, n_bootstrap=8, seed=42)
+    rp, rs, _, _ = O.bootstrap_rsa(O.compute_rdm(feats[0]), O.compute_rdm(feats[1]),
+                                   n_bootstrap=8, seed=42)
+    assert abs(point - rp) < 1e-5
+    assert np.max(np.abs(scores - rs)) < 1e-5
 
 
 @pytest.mark.parametrize("n,d", [(3, 7), (130, 257), (300, 1000)])
@@ -245,12 +260,14 @@ def test_rdm_fp32_kernel_matches_oracle(dev, n, d, monkeypatch):
     assert np.max(np.abs(got - O.compute_rdm(x))) <= 2e-5
 
 
-@pytest.mark.parametrize("n,d,world",[(300, 70, 3), (1000, 40, 4), (2100, 33, 5), (4000, 64, 2)])
-def test_rdm_tile_ranges_assemble_full_rdm(dev, n, d, world):
+@pytest.mark.parametrize("mode", ["split", "fp32"])
+@pytest.mark.parametrize("n,d,world", [(300, 70, 3), (1000, 40, 4), (2100, 33, 5), (4000, 64, 2)])
+def test_rdm_tile_ranges_assemble_full_rdm(dev, n, d, world, mode, monkeypatch):
     # the block-distributed Gram (band launch order inside each rank's tile range) writes
-    # every entry of its range exactly as the one-launch RDM does
+    # every entry of its range exactly as the one-launch RDM does, with either kernel
     from visreps_amd import pipeline as P
 
+    monkeypatch.setenv("VISREPS_GRAM", mode)
     x = torch.randn(n, d, device=dev)
     full = R.compute_rdm(x)
     acc = torch.zeros(n, n, device=dev)

@@ -616,11 +616,16 @@ static void gram_geometry(int64_t n, int64_t d, int64_t count, int& T, int& ntil
   if (splits < 1) splits = 1;
 }
 
-// Gram arithmetic: the bf16 split kernel unless VISREPS_GRAM=fp32 (exact fp32 MFMA).
+// Gram arithmetic per call: VISREPS_GRAM=fp32 / =split force the exact-fp32 or the bf16
+// split kernel; otherwise the split kernel runs where the Gram costs time (n^2 d >= 1e10
+// MACs, ~0.2 ms on the fp32 kernel) and the fp32 kernel below that, where its smaller
+// rounding error keeps tie-sensitive statistics of small RDMs closest to the reference.
 // Read per call, so the workspace query and the launch of one call agree.
-static bool gram_split() {
+static bool gram_split(int64_t n, int64_t d) {
   const char* e = getenv("VISREPS_GRAM");
-  return !(e && strcmp(e, "fp32") == 0);
+  if (e && strcmp(e, "fp32") == 0) return false;
+  if (e && strcmp(e, "split") == 0) return true;
+  return (double)n * (double)n * (double)d >= 1e10;
 }
 
 // Scratch of one RDM launch over `count` tiles: row stats, split-K partial tiles, and the
@@ -650,12 +655,12 @@ extern "C" {
 
 size_t vr_rdm_pearson_workspace(int64_t n, int64_t d) {
   if (n <= 0 || d <= 0) return 256;
-  return gram_ws(n, d, gram_tiles(n), gram_split(), nullptr, nullptr, nullptr, nullptr, nullptr);
+  return gram_ws(n, d, gram_tiles(n), gram_split(n, d), nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
 size_t vr_rdm_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
   if (n <= 0 || d <= 0 || tile_end <= tile_begin) return 256;
-  return gram_ws(n, d, tile_end - tile_begin, gram_split(), nullptr, nullptr, nullptr, nullptr,
+  return gram_ws(n, d, tile_end - tile_begin, gram_split(n, d), nullptr, nullptr, nullptr, nullptr,
                  nullptr);
 }
 
@@ -714,7 +719,7 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
   gram_geometry(n, d, tile_end - tile_begin, P.T, P.ntiles, P.splits, P.kslice);
   P.tile0 = (int)tile_begin;
   P.tile_count = (int)(tile_end - tile_begin);
-  const bool split3 = gram_split();
+  const bool split3 = gram_split(n, d);
   float *mean, *stdv;
   uint16_t* planes;
   gram_ws(n, d, P.tile_count, split3, ws, &mean, &stdv, &P.partial, &planes);

@@ -9,9 +9,11 @@ Per step (BASELINE.json configs[1]: CustomCNN points x NSD ROIs, N stimuli, 1000
                   128x128 upper-triangle Gram tiles into a zeroed RDM, and a sum
                   all-reduce assembles the RDM on every rank;
   3. rank plans   each rank sorts the triangles of the RDMs its units use;
-  4. units        (point, ROI) units are dealt round-robin to ranks; each unit is the
-                  point estimate + n_boot subsets in one engine call
-                  (evals.py:341-373 semantics, RandomState(seed) per unit);
+  4. units        (point, ROI) units listed ROI-major, one contiguous range per rank; a
+                  rank's units sharing a ROI are one engine call (vr_bootstrap_spearman_multi:
+                  the neural plan's rank walk runs once per pass for all of them); each unit
+                  is the point estimate + n_boot subsets (evals.py:341-373 semantics,
+                  RandomState(seed) per unit);
   5. gather       per-unit score vectors are gathered to every rank.
 Scores are exact-integer Spearman values, so they do not depend on the world size.
 """
