@@ -103,13 +103,17 @@ class VisionTransformer(nn.Module):
         nn.init.zeros_(self.heads.head.weight)
         nn.init.zeros_(self.heads.head.bias)
 
-    def forward(self, x):
+    def forward_features(self, x):
+        """Token sequence after the encoder (B, 1 + patches, hidden); [:, 0] is the CLS
+        token (the timm forward_features contract used by vit_representations.py:34)."""
         n = x.shape[0]
         x = self.conv_proj(x)
         x = x.reshape(n, self.hidden_dim, -1).permute(0, 2, 1)
         x = torch.cat([self.class_token.expand(n, -1, -1), x], dim=1)
-        x = self.encoder(x)
-        return self.heads(x[:, 0])
+        return self.encoder(x)
+
+    def forward(self, x):
+        return self.heads(self.forward_features(x)[:, 0])
 
 
 def _maybe_load(model: nn.Module, name: str, pretrained_dataset: str) -> nn.Module:
