@@ -3,6 +3,9 @@ vr_bootstrap_spearman_multi call = NB units of N=10k, 1001 subsets each)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
+if os.environ.get("ALT_LIB"):  # A/B against another build of the library
+    import visreps_amd._lib as _L
+    _L.LIB_PATH = os.environ["ALT_LIB"]
 from visreps_amd.analysis import rsa as R
 from visreps_amd.analysis._random import bootstrap_indices
 dev = torch.device("cuda", 0)

@@ -397,6 +397,12 @@ __global__ void k_add_base(const uint32_t* __restrict__ lpA, const uint32_t* __r
 #define VR_RANKB_PIPE 0  // 1: gather batch h+1 in flight while batch h is consumed
 #endif
 constexpr int BB = 8;  // pairs per gather batch
+#ifndef VR_TB_CACHE
+#define VR_TB_CACHE " nt"  // TB rows are read once: streaming loads keep L2 for the baseA rows
+#endif
+#ifndef VR_PROBE_NO_BASEA
+#define VR_PROBE_NO_BASEA 0
+#endif
 
 // BB pairs' yA = 2 baseA[chunkA] + TB[posA] for this lane. The loads are issued in the
 // saddr form (wave-uniform 64-bit row address in SGPRs + 32-bit lane byte offset), which
@@ -413,10 +419,14 @@ __device__ inline void gather_issue(const TBT* __restrict__ TB, const uint32_t* 
                        (size_t)readlane_u32(pa, j0 + q) * (stride * sizeof(TBT));
     const char* brow = reinterpret_cast<const char*>(baseA) + (size_t)readlane_u32(ca, j0 + q) * (LANES * 4);
     if constexpr (sizeof(TBT) == 2)
-      asm volatile("global_load_ushort %0, %1, %2" : "=v"(t[q]) : "v"(lane_bt), "s"(trow) : "memory");
+      asm volatile("global_load_ushort %0, %1, %2" VR_TB_CACHE : "=v"(t[q]) : "v"(lane_bt), "s"(trow) : "memory");
     else
       asm volatile("global_load_dword %0, %1, %2" : "=v"(t[q]) : "v"(lane_bt), "s"(trow) : "memory");
+#if VR_PROBE_NO_BASEA  // timing probe only: wrong scores
+    b[q] = 0u;
+#else
     asm volatile("global_load_dword %0, %1, %2" : "=v"(b[q]) : "v"(lane_b4), "s"(brow) : "memory");
+#endif
   }
 }
 
