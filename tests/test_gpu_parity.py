@@ -366,3 +366,26 @@ def test_compute_rsa_matches_oracle(dev):
     assert np.max(np.abs(np.array(got["bootstrap_scores"]) - np.array(ref["bootstrap_scores"]))) < 1e-5
     for g, r in zip(got["layer_selection_scores"], ref["layer_selection_scores"]):
         assert g["layer"] == r["layer"] and abs(g["score"] - r["score"]) < 1e-5
+
+
+@pytest.mark.parametrize("mode", ["split", "fp32"])
+def test_rdm_generation_tail_split(dev, mode, monkeypatch):
+    # n = 4200 -> 33 x 34 / 2 = 561 tiles: one 512-block generation of whole-k tiles plus a
+    # 49-tile tail launched split over k (gram_tail). Both launch schemes and the tiles of
+    # the tail must agree with an fp64 RDM, and the matrix stays exactly symmetric.
+    n, d = 4200, 1100
+    feats = O.synthetic_features(n, [d], seed=11, relu=[True])[0]
+    x = torch.from_numpy(feats).to(dev)
+    monkeypatch.setenv("VISREPS_GRAM", mode)
+    tail = R.compute_rdm(x).double()
+    monkeypatch.setenv("VISREPS_GRAM_GEN", "0")  # one launch, no tail split
+    whole = R.compute_rdm(x).double()
+    xd = x.double()
+    xd = xd - xd.mean(1, keepdim=True)
+    s = torch.sqrt((xd * xd).mean(1) + 1e-12)
+    ref = 1.0 - ((xd @ xd.T / d) / (s[:, None] * s[None, :] + 1e-12)).clamp(-1.0, 1.0)
+    ref.fill_diagonal_(0.0)
+    bound = 5e-6 if mode == "split" else 1e-6
+    assert float((tail - ref).abs().max()) <= bound
+    assert float((whole - ref).abs().max()) <= bound
+    assert torch.equal(tail, tail.T) and torch.all(torch.diagonal(tail) == 0)

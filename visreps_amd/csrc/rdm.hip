@@ -599,15 +599,16 @@ static int64_t gram_tiles(int64_t n) {
 }
 
 // Split-K factor for `count` tiles of depth d: enough blocks for two per CU.
+// fit = true (the tail of a generation launch, gram_tail): at most one resident set.
 static void gram_geometry(int64_t n, int64_t d, int64_t count, int& T, int& ntiles,
-                          int& splits, int64_t& kslice) {
+                          int& splits, int64_t& kslice, bool fit = false) {
   T = (int)((n + GT - 1) / GT);
   ntiles = T * (T + 1) / 2;
   const int64_t kt = (d + GK - 1) / GK;  // k stages
   const int target = 2 * num_cus();     // two resident blocks per CU
   int s = 1;
   if (count < target) {
-    s = (int)((target + count - 1) / count);
+    s = fit ? (int)std::max<int64_t>(1, target / count) : (int)((target + count - 1) / count);
     const int64_t maxs = std::max<int64_t>(1, kt / 4);  // >= 4 stages per split
     if (s > maxs) s = (int)maxs;
   }
@@ -646,17 +647,35 @@ static int gram_generation(int nblk) {
   return std::max(1, gen);
 }
 
+// Tiles of a launch's last, partial generation that run as their own split-K launch.
+// With whole-k tiles the last generation of N = 10k (3160 tiles over 512 slots) keeps
+// 88 blocks busy for one full tile time while 424 slots idle; split over k the same
+// tiles fill the chip. Only a small tail (<= half a generation) of a multi-generation
+// launch is split; its fp32 partials are summed in fixed order by k_gram_reduce.
+static int64_t gram_tail(int64_t count) {
+  const int gen = 2 * num_cus();
+  if (getenv("VISREPS_GRAM_GEN") || count <= gen) return 0;
+  const int64_t tail = count % gen;
+  return (tail > 0 && tail <= gen / 2) ? tail : 0;
+}
+
 // Scratch of one RDM launch over `count` tiles: row stats, split-K partial tiles, and the
 // bf16 plane records of the split kernel.
 static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* base, float** mean,
                       float** stdv, float** partial, uint16_t** planes) {
   int T, ntiles, splits;
   int64_t kslice;
-  gram_geometry(n, d, count, T, ntiles, splits, kslice);
+  const int64_t tail = gram_tail(count);
+  gram_geometry(n, d, count - tail, T, ntiles, splits, kslice);
+  size_t part = splits > 1 ? (size_t)splits * (count - tail) : 0;
+  if (tail > 0) {
+    gram_geometry(n, d, tail, T, ntiles, splits, kslice, true);
+    if (splits > 1) part = std::max(part, (size_t)splits * tail);
+  }
   Carver c(base);
   float* m = c.take<float>((size_t)n);
   float* s = c.take<float>((size_t)n);
-  float* p = splits > 1 ? c.take<float>((size_t)splits * count * GT * GT) : nullptr;
+  float* p = part ? c.take<float>(part * GT * GT) : nullptr;
   uint16_t* pl = split3 ? c.take<uint16_t>((size_t)T * GT * (size_t)((d + GK - 1) / GK) * 64) : nullptr;
   if (mean) *mean = m;
   if (stdv) *stdv = s;
@@ -735,12 +754,10 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
   hipStream_t st = as_stream(stream);
   GramParams P{};
   gram_geometry(n, d, tile_end - tile_begin, P.T, P.ntiles, P.splits, P.kslice);
-  P.tile0 = (int)tile_begin;
-  P.tile_count = (int)(tile_end - tile_begin);
   const bool split3 = gram_split(n, d);
   float *mean, *stdv;
   uint16_t* planes;
-  gram_ws(n, d, P.tile_count, split3, ws, &mean, &stdv, &P.partial, &planes);
+  gram_ws(n, d, tile_end - tile_begin, split3, ws, &mean, &stdv, &P.partial, &planes);
   VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
   if (split3) {
     const int64_t rows = (int64_t)P.T * GT, nstage = (d + GK - 1) / GK;
@@ -762,22 +779,32 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
   P.correction = correction;
   P.vec = ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && ((ldx & 3) == 0) &&
           ((reinterpret_cast<uintptr_t>(rdm) & 15) == 0);
-  if (P.tile_count <= 0) return VR_OK;
-  const int nblk = P.tile_count * P.splits;
-  const int gen = gram_generation(nblk);
-  for (int b0 = 0; b0 < nblk; b0 += gen) {
-    P.blk0 = b0;
-    const unsigned nb = (unsigned)std::min(gen, nblk - b0);
-    if (split3)
-      k_gram3<<<nb, G_THREADS, 0, st>>>(P);
-    else
-      k_gram<<<nb, G_THREADS, 0, st>>>(P);
-    VR_CHECK_LAUNCH();
-  }
-  if (P.splits > 1) {
-    k_gram_reduce<<<(unsigned)P.tile_count, 256, 0, st>>>(P);
-    VR_CHECK_LAUNCH();
-  }
+  // tile range [t0, t0 + count): its own split-K geometry, generations, reduction
+  auto run_range = [&](int64_t t0, int64_t count, bool fit) -> int {
+    if (count <= 0) return VR_OK;
+    gram_geometry(n, d, count, P.T, P.ntiles, P.splits, P.kslice, fit);
+    P.tile0 = (int)t0;
+    P.tile_count = (int)count;
+    const int nblk = P.tile_count * P.splits;
+    const int gen = gram_generation(nblk);
+    for (int b0 = 0; b0 < nblk; b0 += gen) {
+      P.blk0 = b0;
+      const unsigned nb = (unsigned)std::min(gen, nblk - b0);
+      if (split3)
+        k_gram3<<<nb, G_THREADS, 0, st>>>(P);
+      else
+        k_gram<<<nb, G_THREADS, 0, st>>>(P);
+      VR_CHECK_LAUNCH();
+    }
+    if (P.splits > 1) {
+      k_gram_reduce<<<(unsigned)P.tile_count, 256, 0, st>>>(P);
+      VR_CHECK_LAUNCH();
+    }
+    return VR_OK;
+  };
+  const int64_t count = tile_end - tile_begin, tail = gram_tail(count);
+  VR_TRY(run_range(tile_begin, count - tail, false));
+  VR_TRY(run_range(tile_end - tail, tail, true));
   return VR_OK;
 }
 
