@@ -25,12 +25,17 @@ import os
 import sys
 import time
 
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+# MIOpen find (NORMAL) + cudnn.benchmark pick the convolution kernels by timing them during
+# warm-up: CustomCNN extraction of 10k images 349 -> 239 ms against FAST's heuristic choice
+# (scripts/probe_extract.py, profiles/r1_extract_ab.log).
+os.environ.setdefault("MIOPEN_FIND_MODE", "NORMAL")
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+torch.backends.cudnn.benchmark = True
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

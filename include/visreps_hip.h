@@ -73,6 +73,26 @@ int vr_rdm_pearson_tiles_f32(const float* X, int64_t n, int64_t d, int64_t ldx, 
                              int64_t ldr, float correction, int64_t tile_begin,
                              int64_t tile_end, void* ws, size_t ws_bytes, void* stream);
 
+/* Plain symmetric Gram G = X X^T (fp32 out; the same MFMA kernels, tiling and accuracy
+ * as the RDM, without centring or the correlation epilogue). The kernel matrix of the
+ * encoding score's ridge regression: replaces the SVD inside himalaya 0.4.9's
+ * RidgeCV(solver="svd") as called from visreps/analysis/encoding_score.py:47-62
+ * (kernel form: X_val X_tr^T and X_tr X_tr^T are blocks of one Gram of the stacked rows).
+ * Workspace: vr_rdm_pearson_workspace(n, d). G is exactly symmetric. */
+int vr_gram_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* G, int64_t ldg,
+                void* ws, size_t ws_bytes, void* stream);
+
+/* Encoding-score statistic (visreps/analysis/encoding_score.py:206-224): for each of
+ * `draws` row subsets (idx [dev] int32 draws x k; null = all n rows, draws = 1) the mean
+ * over the v columns of the per-column Pearson r between Y and P (himalaya 0.4.9
+ * correlation_score: zscore products, population std; zero variance -> NaN), in fp64.
+ * Y, P [dev] fp32 (n, v) row-major with leading dimension ld. voxel_r [dev] fp64
+ * (draws, v) or null. Workspace: vr_corr_score_workspace(v, draws). */
+size_t vr_corr_score_workspace(int64_t v, int64_t draws);
+int vr_corr_score_f32(const float* Y, const float* P, int64_t n, int64_t v, int64_t ld,
+                      const int32_t* idx, int64_t k, int64_t draws, double* scores,
+                      double* voxel_r, void* ws, size_t ws_bytes, void* stream);
+
 /* Row statistics of the same RDM (rsa.py:80-87): mean[i] (fp32) and
  * std[i] = sqrt(mean((x-mean)^2) + correction) with std < 10*correction -> 1.
  * Exposed so extraction can emit them alongside the feature rows. */

@@ -51,6 +51,15 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _c_i64, _c_i64, _vp, _c_sz, _vp],
     ),
+    "vr_gram_f32": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp, _c_sz, _vp],
+    ),
+    "vr_corr_score_workspace": (_c_sz, [_c_i64, _c_i64]),
+    "vr_corr_score_f32": (
+        ctypes.c_int,
+        [_vp, _vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_sz, _vp],
+    ),
     "vr_row_stats_f32": (
         ctypes.c_int,
         [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, ctypes.c_float, _vp],

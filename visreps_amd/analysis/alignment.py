@@ -77,7 +77,11 @@ def compute_traintest_alignment(cfg, train: AlignmentData, test: AlignmentData,
                            bootstrap=bootstrap, n_bootstrap=n_bootstrap, verbose=verbose,
                            re_extract_fn=re_extract_fn)
     if analysis == "encoding_score":
-        raise NotImplementedError("encoding_score is outside the MI355X RSA build (SURVEY.md §8(f))")
+        from .encoding_score import compute_encoding_score
+
+        pca_k = cfg.get("pca_k", 1) if cfg.get("reconstruct_from_pcs") else None
+        return compute_encoding_score(train, test, bootstrap=bootstrap, n_bootstrap=n_bootstrap,
+                                      verbose=verbose, reconstruct_pca_k=pca_k)
     raise ValueError(f"Unknown analysis method: {analysis}")
 
 

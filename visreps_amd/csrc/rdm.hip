@@ -119,6 +119,7 @@ struct GramParams {
   const uint16_t* planes;  // split Gram: bf16 hi/lo stage records (null: fp32 kernel)
   int64_t nstage;          // 32-k stages per plane row
   int blk0;                // first launch position of this generation (see gram_generation)
+  int raw;                 // 1: plain Gram X X^T (no centring, no correlation epilogue)
 };
 
 __device__ inline void tile_coords(int p, int T, int& bi, int& bj) {
@@ -252,6 +253,7 @@ __device__ inline void store_panel(const GramParams& P, float* lds, int64_t row0
 // reference's fp32 operation order; NaN propagates like torch.clamp.
 __device__ inline float rdm_value(float g, int64_t i, int64_t j, const GramParams& P,
                                   float si, float sj) {
+  if (P.raw) return g;  // vr_gram_f32
   float cov = g / (float)P.d;
   float c = cov / (si * sj + P.correction);
   c = (c < -1.f) ? -1.f : ((c > 1.f) ? 1.f : c);
@@ -746,7 +748,7 @@ int vr_row_stats_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* m
 
 static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm, int64_t ldr,
                       float correction, int64_t tile_begin, int64_t tile_end, void* ws,
-                      size_t ws_bytes, void* stream, size_t need) {
+                      size_t ws_bytes, void* stream, size_t need, bool raw = false) {
   if (ws_bytes < need || ws == nullptr) {
     set_error("vr_rdm_pearson: workspace %zu < %zu", ws_bytes, need);
     return VR_EWORKSPACE;
@@ -758,7 +760,13 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
   float *mean, *stdv;
   uint16_t* planes;
   gram_ws(n, d, tile_end - tile_begin, split3, ws, &mean, &stdv, &P.partial, &planes);
-  VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
+  P.raw = raw ? 1 : 0;
+  if (raw) {  // zero means: the panels stage X itself
+    VR_CHECK_HIP(hipMemsetAsync(mean, 0, (size_t)n * sizeof(float), st));
+    VR_CHECK_HIP(hipMemsetAsync(stdv, 0, (size_t)n * sizeof(float), st));
+  } else {
+    VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
+  }
   if (split3) {
     const int64_t rows = (int64_t)P.T * GT, nstage = (d + GK - 1) / GK;
     const int64_t threads = rows * nstage * 8;
@@ -834,6 +842,18 @@ int vr_rdm_pearson_tiles_f32(const float* X, int64_t n, int64_t d, int64_t ldx, 
   VR_REQUIRE(X && rdm, "vr_rdm_pearson_tiles_f32: null pointer");
   return rdm_launch(X, n, d, ldx, rdm, ldr, correction, tile_begin, tile_end, ws, ws_bytes,
                     stream, vr_rdm_tiles_workspace(n, d, tile_begin, tile_end));
+}
+
+int vr_gram_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* G, int64_t ldg,
+                void* ws, size_t ws_bytes, void* stream) {
+  VR_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldg >= n,
+             "vr_gram_f32: bad shape n=%lld d=%lld ldx=%lld ldg=%lld", (long long)n, (long long)d,
+             (long long)ldx, (long long)ldg);
+  if (n == 0) return VR_OK;
+  VR_REQUIRE(X && G, "vr_gram_f32: null pointer");
+  VR_REQUIRE(n <= (1 << 20), "vr_gram_f32: n=%lld too large", (long long)n);
+  return rdm_launch(X, n, d, ldx, G, ldg, 0.f, 0, gram_tiles(n), ws, ws_bytes, stream,
+                    vr_rdm_pearson_workspace(n, d), true);
 }
 
 }  // extern "C"
