@@ -94,3 +94,20 @@ def test_eval_end_to_end_matches_oracle(dev):
         point, scores, lo, hi = O.bootstrap_rsa(m_rdm, n_rdm, n_bootstrap=20, seed=42)
         assert abs(df.iloc[i]["score"] - point) < 1e-4
         assert np.max(np.abs(np.asarray(df.iloc[i]["bootstrap_scores"]) - scores)) < 1e-4
+
+
+@pytest.mark.gpu
+def test_eval_encoding_score_end_to_end(dev):
+    # evals._eval_encoding (evals.py:551-591): per (region, subject) train/test alignment on
+    # the SRP activations -> compute_encoding_score; record layout of the reference
+    from visreps_amd import evals
+
+    cfg = _cfg(analysis="encoding_score", bootstrap="true")
+    df = evals.eval(cfg)
+    assert len(df) == 2
+    for _, row in df.iterrows():
+        assert row["analysis"] == "encoding_score" and row["compare_method"] == "pearson"
+        sel = row["layer_selection_scores"]
+        assert len(sel) == 14 and row["layer"] in [s["layer"] for s in sel]
+        assert len(row["bootstrap_scores"]) == 20
+        assert row["ci_low"] <= row["ci_high"] and np.isfinite(row["score"])

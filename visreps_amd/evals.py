@@ -31,7 +31,8 @@ import numpy as np
 import pandas as pd
 import torch
 
-from .analysis.alignment import _align_stimulus_level
+from .analysis.alignment import (_align_stimulus_level, compute_traintest_alignment,
+                                 prepare_traintest_alignment)
 from .analysis.rsa import RankPlan, bootstrap_rsa, compute_rdm, compute_rdm_correlation
 from .analysis._random import LegacyRandomState
 from .dataloaders.neural import _make_loader, load_synthetic_data
@@ -81,8 +82,8 @@ def eval(cfg):  # noqa: A001  (reference name)
             "does not ship; use neural_dataset='synthetic' (NSD-shaped) or supply the arrays "
             "to visreps_amd.evals._eval_rsa directly")
     analysis = str(cfg.get("analysis", "rsa")).lower()
-    if analysis != "rsa":
-        raise NotImplementedError(f"analysis='{analysis}' is not on the MI355X RSA path")
+    if analysis not in ("rsa", "encoding_score"):
+        raise ValueError(f"Unknown analysis method: {analysis}")
 
     subjects = _listify(cfg.subject_idx)
     regions = _listify(cfg.region)
@@ -106,7 +107,10 @@ def eval(cfg):  # noqa: A001  (reference name)
                                        srp_cache_dir=cfg.get("srp_cache_dir", "model_checkpoints/srp_cache"))
     rprint("  Activations extracted once for all subjects/regions", style="success")
     del dl
-    results = _eval_rsa(cfg, model, acts, ids, all_data, subjects, regions, dev, verbose)
+    if analysis == "encoding_score":
+        results = _eval_encoding(cfg, model, acts, ids, all_data, subjects, regions, verbose)
+    else:
+        results = _eval_rsa(cfg, model, acts, ids, all_data, subjects, regions, dev, verbose)
     torch.cuda.empty_cache()
     return results
 
@@ -223,3 +227,22 @@ def _compare(layer_rdm, neural_rdm, neural_plan, method: str) -> float:
     if method in ("spearman", "kendall"):
         return float(bootstrap_rsa(RankPlan(layer_rdm), neural_plan, n_bootstrap=0, method=method)[0])
     return compute_rdm_correlation(layer_rdm, neural_rdm, correlation=method.capitalize())
+
+
+def _eval_encoding(cfg, model, acts, ids, all_data, subjects, regions, verbose):
+    """Per-(region, subject) encoding score on the SRP activations (evals.py:551-591):
+    train/test alignment, then compute_traintest_alignment -> compute_encoding_score."""
+    neural = all_data["neural"]
+    all_results: List[dict] = []
+    for region in regions:
+        rprint(f"\n  -- Region: {region} --", style="info")
+        for subj in subjects:
+            train_data, test_data = prepare_traintest_alignment(cfg, acts, neural[region][subj], ids)
+            scores = compute_traintest_alignment(cfg, train_data, test_data, verbose=verbose)
+            del train_data, test_data
+            if cfg.get("log_expdata"):
+                save_results(pd.DataFrame(scores), cfg.merge({"subject_idx": subj, "region": region}))
+            all_results.extend(scores)
+    del acts, model
+    torch.cuda.empty_cache()
+    return pd.DataFrame(all_results)
