@@ -218,6 +218,10 @@ def main():
                            "A-side rank walk of the neural plan + one B-side walk per unit)"),
                 "algorithmic_bytes_per_call": per_launch,
                 "avg_call_ms": round(times.engine_ms / max(1, times.engine_calls), 3)}
+        if traffic:  # bandwidth actually drawn: PMC bytes per unit / measured time per unit
+            drawn = traffic / (roof["avg_call_ms"] / 1e3) / 1e9
+            roof["traffic_gbs"] = round(drawn, 1)
+            roof["traffic_frac"] = round(drawn / HBM_PEAK_GBS, 4)
         if os.environ.get("VISREPS_GRAM") == "fp32":
             gpeak, gkern = FP32_MFMA_PEAK_TF, "k_gram (exact fp32, v_mfma_f32_32x32x2_f32)"
         else:  # 3 bf16 MFMA products per algorithmic FLOP: ceiling = bf16 dense peak / 3
