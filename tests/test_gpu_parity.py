@@ -389,3 +389,23 @@ def test_rdm_generation_tail_split(dev, mode, monkeypatch):
     assert float((tail - ref).abs().max()) <= bound
     assert float((whole - ref).abs().max()) <= bound
     assert torch.equal(tail, tail.T) and torch.all(torch.diagonal(tail) == 0)
+
+
+@pytest.mark.parametrize("wide", ["1", "0"])
+def test_rdm_wide_supertiles(dev, wide, monkeypatch):
+    # n = 6000: 24 x 25 / 2 = 300 super-tiles of 256; rows [0, 30 * 128) run on the wide
+    # 256 x 256 kernel (255 super-tiles = one generation), 128-tile rows 30..46 below on
+    # k_gram3 (generation + tail split). Both schemes against fp64; exact symmetry.
+    n, d = 6000, 1100
+    feats = O.synthetic_features(n, [d], seed=13, relu=[True])[0]
+    x = torch.from_numpy(feats).to(dev)
+    monkeypatch.setenv("VISREPS_GRAM", "split")
+    monkeypatch.setenv("VISREPS_GRAM_WIDE", wide)
+    got = R.compute_rdm(x).double()
+    xd = x.double()
+    xd = xd - xd.mean(1, keepdim=True)
+    s = torch.sqrt((xd * xd).mean(1) + 1e-12)
+    ref = 1.0 - ((xd @ xd.T / d) / (s[:, None] * s[None, :] + 1e-12)).clamp(-1.0, 1.0)
+    ref.fill_diagonal_(0.0)
+    assert float((got - ref).abs().max()) <= 5e-6
+    assert torch.equal(got, got.T) and torch.all(torch.diagonal(got) == 0)

@@ -558,6 +558,167 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram3(GramParams P) {
   gram_store(P, acc, row0, col0, diag, split, ltile);
 }
 
+// ------------------------------------------------------------------------------------
+// Wide split Gram: 256 x 256 super-tiles (2 x 2 of the 128-tiles), 8 waves as 2 x 4, each
+// wave 128 x 64 = 4 x 2 accumulators. Against k_gram3 it halves the global->LDS traffic
+// and the LDS writes per FLOP and cuts LDS fragment reads per MFMA from 2/3 to 1/2
+// (12 ds_read_b128 per 24 MFMAs per 16-k step). 147 KB of LDS: one block (8 waves) per CU.
+// Super-tile rows [0, R) of the upper triangle; a diagonal super-tile computes its lower
+// 128-tile too and writes only i <= j entries (mirrored), as the 128 kernel does.
+// ------------------------------------------------------------------------------------
+constexpr int WT = 256;               // super-tile edge
+constexpr int W_THREADS = 512;        // 8 waves
+constexpr int W_STAGE = WT * SROW;    // bf16 per panel per stage
+
+__device__ inline void load_rec_w(const GramParams& P, int64_t row0, int64_t st, u32x4 out[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int f = threadIdx.x + W_THREADS * s;
+    const int r = f >> 3, c = f & 7;
+    out[s] = *reinterpret_cast<const u32x4*>(P.planes + ((row0 + r) * P.nstage + st) * 64 + c * 8);
+  }
+}
+
+__device__ inline void store_rec_w(uint16_t* lds, const u32x4 v[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int f = threadIdx.x + W_THREADS * s;
+    const int r = f >> 3, c = f & 7;
+    *reinterpret_cast<u32x4*>(lds + r * SROW + c * 8) = v[s];
+  }
+}
+
+// Epilogue of one wave's 128 x 64 block (4 x 2 accumulators of 32 x 32).
+__device__ inline void gram_store_w(const GramParams& P, f32x16 (&acc)[4][2], int64_t row0,
+                                    int64_t col0, bool diag) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3, h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn) {
+      const int64_t j = col0 + wc * 64 + nn * 32 + l32;
+      const float sj = (j < P.n) ? P.stdv[j] : 1.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t ib = row0 + wr * 128 + m * 32 + 8 * g + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t i = ib + e;
+          const float si = (i < P.n) ? P.stdv[i] : 1.f;
+          v[e] = rdm_value(acc[m][nn][4 * g + e], i, j, P, si, sj);
+        }
+        if (diag) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t i = ib + e;
+            if (i <= j && j < P.n) {
+              P.rdm[i * P.ldr + j] = v[e];
+              if (i < j) P.rdm[j * P.ldr + i] = v[e];
+            }
+          }
+          continue;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t i = ib + e;
+          if (i < P.n && j < P.n) P.rdm[i * P.ldr + j] = v[e];
+        }
+        if (j < P.n) {
+          float* dst = P.rdm + j * P.ldr + ib;
+          if (P.vec && ib + 3 < P.n && ((P.ldr & 3) == 0)) {
+            f32x4 w = {v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<f32x4*>(dst) = w;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (ib + e < P.n) dst[e] = v[e];
+          }
+        }
+      }
+    }
+}
+
+// Super-tile position p (row-major over super rows [0, R) of a T2 x T2 triangle).
+__device__ inline void super_tile(int p, int T2, int& bi, int& bj) { tile_coords(p, T2, bi, bj); }
+
+__global__ __launch_bounds__(W_THREADS, 1) void k_gram3w(GramParams P) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * W_STAGE];  // [buf][A/B]
+  const int id = P.blk0 + (int)xcd_remap(blockIdx.x, (uint32_t)gridDim.x);
+  int bi, bj;
+  band_tile(id, 0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension here
+  const bool diag = (bi == bj);
+  const int64_t row0 = (int64_t)bi * WT, col0 = (int64_t)bj * WT;
+  const int ns = (int)P.nstage;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3, h = lane >> 5, l32 = lane & 31;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  u32x4 ga[4], gb[4];
+  load_rec_w(P, row0, 0, ga);
+  if (!diag) load_rec_w(P, col0, 0, gb);
+  store_rec_w(lds, ga);
+  if (!diag) store_rec_w(lds + W_STAGE, gb);
+  __syncthreads();
+  for (int kt = 0; kt < ns; ++kt) {
+    const int cur = kt & 1;
+    const uint16_t* As = lds + cur * 2 * W_STAGE;
+    const uint16_t* Bs = diag ? As : As + W_STAGE;
+    const bool more = kt + 1 < ns;
+    if (more) {
+      load_rec_w(P, row0, kt + 1, ga);
+      if (!diag) load_rec_w(P, col0, kt + 1, gb);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 aH[4], aL[4], bH[2], bL[2];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const uint16_t* ar = As + (wr * 128 + m * 32 + l32) * SROW + t * 16 + h * 8;
+        aH[m] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(ar));
+        aL[m] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(ar + 32));
+      }
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn) {
+        const uint16_t* br = Bs + (wc * 64 + nn * 32 + l32) * SROW + t * 16 + h * 8;
+        bH[nn] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(br));
+        bL[nn] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(br + 32));
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[m], bH[nn], acc[m][nn], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[m], bL[nn], acc[m][nn], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL[m], bH[nn], acc[m][nn], 0, 0, 0);
+    }
+    if (more) {
+      uint16_t* nxt = lds + (cur ^ 1) * 2 * W_STAGE;
+      store_rec_w(nxt, ga);
+      if (!diag) store_rec_w(nxt + W_STAGE, gb);
+    }
+    __syncthreads();
+  }
+  gram_store_w(P, acc, row0, col0, diag);
+}
+
 // Sums the split partials of one tile in split order and applies the epilogue; the
 // mirror half goes through an LDS transpose so both writes are row-coalesced.
 __global__ __launch_bounds__(256) void k_gram_reduce(GramParams P) {
@@ -661,10 +822,9 @@ static int64_t gram_tail(int64_t count) {
   return (tail > 0 && tail <= gen / 2) ? tail : 0;
 }
 
-// Scratch of one RDM launch over `count` tiles: row stats, split-K partial tiles, and the
-// bf16 plane records of the split kernel.
-static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* base, float** mean,
-                      float** stdv, float** partial, uint16_t** planes) {
+// Split-K partial floats of one tile range as run_split launches it (main + tail).
+static size_t range_partial(int64_t n, int64_t d, int64_t count) {
+  if (count <= 0) return 0;
   int T, ntiles, splits;
   int64_t kslice;
   const int64_t tail = gram_tail(count);
@@ -674,11 +834,42 @@ static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* ba
     gram_geometry(n, d, tail, T, ntiles, splits, kslice, true);
     if (splits > 1) part = std::max(part, (size_t)splits * tail);
   }
+  return part * GT * GT;
+}
+
+static int64_t tri_start(int64_t r, int64_t T) { return r * T - r * (r - 1) / 2; }
+
+// Super-tile rows [0, R) of the wide split kernel for a full-RDM launch (0: not used).
+// R is the largest whose super-tile count fits whole generations of one block per CU;
+// the 128-tile rows [2R, T) below them run on k_gram3 (generations + tail split).
+// VISREPS_GRAM_WIDE=0 turns the wide kernel off (A/B timing).
+static int gram_wide_rows(int64_t n, int64_t d, int64_t count, bool split3) {
+  if (!split3 || count != gram_tiles(n)) return 0;
+  if (const char* e = getenv("VISREPS_GRAM_WIDE"))
+    if (strcmp(e, "0") == 0) return 0;
+  const int64_t T2 = (n + WT - 1) / WT, gen = num_cus();
+  const int64_t full = (T2 * (T2 + 1) / 2) / gen * gen;
+  if (full < gen) return 0;
+  int64_t R = 0;
+  while (R + 1 <= T2 && tri_start(R + 1, T2) <= full) ++R;
+  (void)d;
+  return (int)R;
+}
+
+// Scratch of one RDM launch over `count` tiles: row stats, split-K partial tiles, and the
+// bf16 plane records of the split kernel (rows padded to the 256-row super-tile edge).
+static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* base, float** mean,
+                      float** stdv, float** partial, uint16_t** planes) {
+  const int64_t T = (n + GT - 1) / GT;
+  const int R = gram_wide_rows(n, d, count, split3);
+  const int64_t rest = R > 0 ? count - tri_start(2 * (int64_t)R, T) : count;
+  const size_t part = range_partial(n, d, rest);
   Carver c(base);
   float* m = c.take<float>((size_t)n);
   float* s = c.take<float>((size_t)n);
-  float* p = part ? c.take<float>(part * GT * GT) : nullptr;
-  uint16_t* pl = split3 ? c.take<uint16_t>((size_t)T * GT * (size_t)((d + GK - 1) / GK) * 64) : nullptr;
+  float* p = part ? c.take<float>(part) : nullptr;
+  const int64_t prow = (n + WT - 1) / WT * WT;
+  uint16_t* pl = split3 ? c.take<uint16_t>((size_t)prow * (size_t)((d + GK - 1) / GK) * 64) : nullptr;
   if (mean) *mean = m;
   if (stdv) *stdv = s;
   if (partial) *partial = p;
@@ -768,7 +959,7 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
     VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
   }
   if (split3) {
-    const int64_t rows = (int64_t)P.T * GT, nstage = (d + GK - 1) / GK;
+    const int64_t rows = (n + WT - 1) / WT * WT, nstage = (d + GK - 1) / GK;
     const int64_t threads = rows * nstage * 8;
     k_split3<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(X, n, d, ldx, mean, rows, nstage,
                                                                 planes);
@@ -810,10 +1001,28 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
     }
     return VR_OK;
   };
-  const int64_t count = tile_end - tile_begin, tail = gram_tail(count);
-  VR_TRY(run_range(tile_begin, count - tail, false));
-  VR_TRY(run_range(tile_end - tail, tail, true));
-  return VR_OK;
+  auto run_split = [&](int64_t t0, int64_t count) -> int {
+    const int64_t tail = gram_tail(count);
+    VR_TRY(run_range(t0, count - tail, false));
+    return run_range(t0 + count - tail, tail, true);
+  };
+  const int64_t count = tile_end - tile_begin;
+  const int R = gram_wide_rows(n, d, count, split3);
+  if (R == 0) return run_split(tile_begin, count);
+  // wide super-tiles over rows [0, 2R * 128), then the 128-tile rows below them
+  GramParams W = P;
+  W.T = (int)((n + WT - 1) / WT);
+  W.tile0 = 0;
+  W.tile_count = (int)tri_start(R, W.T);
+  W.splits = 1;
+  const int gen = num_cus();
+  for (int b0 = 0; b0 < W.tile_count; b0 += gen) {
+    W.blk0 = b0;
+    k_gram3w<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
+    VR_CHECK_LAUNCH();
+  }
+  const int64_t t0 = tri_start(2 * (int64_t)R, P.T);
+  return run_split(t0, gram_tiles(n) - t0);
 }
 
 int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
