@@ -113,15 +113,15 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
 // per-unit join and per-pass masks
 // ---------------------------------------------------------------------------------
 __global__ void k_join(const uint32_t* __restrict__ codesB, int64_t M, int64_t n,
-                       const uint32_t* __restrict__ posOfPairA,
-                       const uint32_t* __restrict__ chunkOfPairA,
+                       const uint2* __restrict__ pairMapA,
                        uint32_t* __restrict__ posA_byB, uint32_t* __restrict__ chunkA_byB) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M) return;
   const uint32_t cb = codesB[i];
   const uint64_t t = tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n);
-  posA_byB[i] = posOfPairA[t];
-  chunkA_byB[i] = chunkOfPairA[t];
+  const uint2 pc = pairMapA[t];
+  posA_byB[i] = pc.x;
+  chunkA_byB[i] = pc.y;
 }
 
 // bit w of masks[x] <- x in subset (set0 + w); subset 0 is "all stimuli" when full_first.
@@ -788,8 +788,8 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
   const bool narrow = (uint64_t)PLAN_L + h[0].max_group <= 32767u;
   const bool bigA = h[0].max_group >= 65536u;
   for (int64_t j = 0; j < nb; ++j) {
-    k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(Bs[j].codes, M, n, A.pos_of_pair,
-                                                       A.chunk_of_pair, joins[2 * j], joins[2 * j + 1]);
+    k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(Bs[j].codes, M, n, A.pair_map,
+                                                       joins[2 * j], joins[2 * j + 1]);
     VR_CHECK_LAUNCH();
   }
   return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {

@@ -33,8 +33,8 @@ struct PlanView {
   PlanHeader* hdr;
   uint32_t* codes;          // [M]    (a << 16) | b, sorted by value
   uint32_t* gstart;         // [M+1]  first G+1 valid: group start positions, gstart[G] = M
-  uint32_t* pos_of_pair;    // [M]    triangle index -> sorted position
-  uint32_t* chunk_of_pair;  // [M]    triangle index -> chunk of its sorted position
+  uint2* pair_map;          // [M]    triangle index -> (sorted position, chunk of it):
+                            //        one 8-B record, so a join gathers one sector per pair
   uint32_t* chunk_g;        // [nchunks+1] first group of each chunk
   uint32_t* gflag;          // [(M+31)/32 + 2] bit i = position i starts a tie group
 };
@@ -48,8 +48,7 @@ inline PlanView plan_layout(void* base, int64_t n, size_t* bytes = nullptr) {
   v.hdr = c.take<PlanHeader>(1);
   v.codes = c.take<uint32_t>((size_t)M);
   v.gstart = c.take<uint32_t>((size_t)M + 1);
-  v.pos_of_pair = c.take<uint32_t>((size_t)M);
-  v.chunk_of_pair = c.take<uint32_t>((size_t)M);
+  v.pair_map = c.take<uint2>((size_t)M);
   v.chunk_g = c.take<uint32_t>((size_t)plan_nchunks(M) + 1);
   v.gflag = c.take<uint32_t>((size_t)(M + 31) / 32 + 2);
   if (bytes) *bytes = c.bytes();
