@@ -823,10 +823,14 @@ static int64_t gram_tail(int64_t count) {
 }
 
 // Split-K partial floats of one tile range as run_split launches it (main + tail).
-static size_t range_partial(int64_t n, int64_t d, int64_t count) {
+static size_t range_partial(int64_t n, int64_t d, int64_t count, bool fit_one = false) {
   if (count <= 0) return 0;
   int T, ntiles, splits;
   int64_t kslice;
+  if (fit_one && count < 2 * num_cus()) {
+    gram_geometry(n, d, count, T, ntiles, splits, kslice, true);
+    return splits > 1 ? (size_t)splits * count * GT * GT : 0;
+  }
   const int64_t tail = gram_tail(count);
   gram_geometry(n, d, count - tail, T, ntiles, splits, kslice);
   size_t part = splits > 1 ? (size_t)splits * (count - tail) : 0;
@@ -863,7 +867,7 @@ static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* ba
   const int64_t T = (n + GT - 1) / GT;
   const int R = gram_wide_rows(n, d, count, split3);
   const int64_t rest = R > 0 ? count - tri_start(2 * (int64_t)R, T) : count;
-  const size_t part = range_partial(n, d, rest);
+  const size_t part = range_partial(n, d, rest, R > 0);
   Carver c(base);
   float* m = c.take<float>((size_t)n);
   float* s = c.take<float>((size_t)n);
@@ -1001,14 +1005,17 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
     }
     return VR_OK;
   };
-  auto run_split = [&](int64_t t0, int64_t count) -> int {
+  // fit_one: a range smaller than one generation splits over k into at most one
+  // generation (floor) instead of spilling a few blocks into a second one (ceil)
+  auto run_split = [&](int64_t t0, int64_t count, bool fit_one) -> int {
+    if (fit_one && count < 2 * num_cus()) return run_range(t0, count, true);
     const int64_t tail = gram_tail(count);
     VR_TRY(run_range(t0, count - tail, false));
     return run_range(t0 + count - tail, tail, true);
   };
   const int64_t count = tile_end - tile_begin;
   const int R = gram_wide_rows(n, d, count, split3);
-  if (R == 0) return run_split(tile_begin, count);
+  if (R == 0) return run_split(tile_begin, count, false);
   // wide super-tiles over rows [0, 2R * 128), then the 128-tile rows below them
   GramParams W = P;
   W.T = (int)((n + WT - 1) / WT);
@@ -1022,7 +1029,7 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
     VR_CHECK_LAUNCH();
   }
   const int64_t t0 = tri_start(2 * (int64_t)R, P.T);
-  return run_split(t0, gram_tiles(n) - t0);
+  return run_split(t0, gram_tiles(n) - t0, true);
 }
 
 int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
