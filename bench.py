@@ -43,7 +43,7 @@ sys.path.insert(0, ROOT)
 from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_responses, shard_rows
 from visreps_amd.models.custom_model import CustomCNN
 from visreps_amd.models.utils import FeatureExtractor
-from visreps_amd.pipeline import StepTimes, all_units_rsa, distributed_rdm, engine_bytes
+from visreps_amd.pipeline import PrefetchedRDMs, StepTimes, all_units_rsa, distributed_rdm, engine_bytes
 
 METRIC = "end-to-end RSA eval sec (extract→RDM→1000-bootstrap Spearman), N=10k stimuli"
 LAYERS = ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
@@ -174,7 +174,7 @@ def main():
         for p, f in feats.items():
             dims[p] = f.size(1)
         neural = {r: distributed_rdm(y, N, pg, times) for r, y in responses.items()}
-        res = all_units_rsa(lambda p: distributed_rdm(feats[p], N, pg, times), points, neural,
+        res = all_units_rsa(PrefetchedRDMs(feats, points, N, pg, times), points, neural,
                             N, n_boot=args.boot, seed=42, pg=pg, times=times)
         del feats
         return res, neural

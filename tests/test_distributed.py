@@ -73,6 +73,10 @@ def _worker(rank, world, port, n, d, n_boot, out_dir):
     y_local = torch.from_numpy(Y[rows.start:rows.stop])
     rdm_x = P.distributed_rdm(x_local, n, pg, tiles_into=_oracle_tiles_into)
     rdm_y = P.distributed_rdm(y_local, n, pg, tiles_into=_oracle_tiles_into)
+    # the prefetching source bench.py uses: next point's all-gather in flight (async)
+    src = P.PrefetchedRDMs({"x": x_local, "y": y_local}, ["x", "y"], n, pg,
+                           tiles_into=_oracle_tiles_into)
+    assert torch.equal(src("x"), rdm_x) and torch.equal(src("y"), rdm_y) and not src.pending
 
     def unit(pm, pn, idx, times):  # noqa: ARG001
         sets = [np.arange(n)] + ([] if idx is None else list(np.asarray(idx)))

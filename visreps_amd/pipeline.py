@@ -149,15 +149,36 @@ def gather_rows(x_local: torch.Tensor, n: int, pg) -> torch.Tensor:
     return torch.cat([full[r * per: r * per + sizes[r]] for r in range(world)], 0)
 
 
-def distributed_rdm(x_local: torch.Tensor, n: int, pg=None,
-                    times: Optional[StepTimes] = None, tiles_into=None) -> torch.Tensor:
-    """Full (n, n) RDM on every rank from each rank's stimulus rows: all-gather the rows,
-    each rank writes its balanced tile range (and mirrors) into a zeroed matrix, and a
-    sum all-reduce assembles it (every entry has exactly one writer, so the sum is exact).
-    tiles_into(x, out, t0, t1, times=...) defaults to the HIP Gram kernel."""
-    tiles_into = tiles_into or rdm_tiles_into
+def gather_rows_async(x_local: torch.Tensor, n: int, pg):
+    """Start the all-gather of gather_rows; returns a finish() -> (n, d) callable. The
+    collective runs on the communicator's stream, so work queued meanwhile on the
+    compute stream (the previous point's Gram) overlaps it."""
     rank, world = _world(pg)
-    x = gather_rows(x_local.float().contiguous(), n, pg)
+    x_local = x_local.float().contiguous()
+    if world == 1:
+        return lambda: x_local
+    sizes = [len(shard_rows(n, r, world)) for r in range(world)]
+    per = max(sizes)
+    d = x_local.size(1)
+    buf = torch.zeros((per, d), dtype=x_local.dtype, device=x_local.device)
+    buf[: x_local.size(0)] = x_local
+    full = torch.empty((world * per, d), dtype=x_local.dtype, device=x_local.device)
+    if dist.get_backend(pg) == "nccl":
+        work = dist.all_gather_into_tensor(full, buf, group=pg, async_op=True)
+    else:  # gloo (CPU tests of the orchestration)
+        work = dist.all_gather(list(full.chunk(world)), buf, group=pg, async_op=True)
+
+    def finish(_send=buf) -> torch.Tensor:  # _send keeps the source buffer alive until here
+        work.wait()  # the compute stream waits for the gather
+        if all(sz == per for sz in sizes):
+            return full
+        return torch.cat([full[r * per: r * per + sizes[r]] for r in range(world)], 0)
+
+    return finish
+
+
+def _rdm_from_rows(x: torch.Tensor, n: int, pg, times, tiles_into) -> torch.Tensor:
+    rank, world = _world(pg)
     if world == 1:
         out = torch.empty((n, n), dtype=torch.float32, device=x.device)
         tiles_into(x, out, 0, int(lib().vr_rdm_tile_count(n)), times=times)
@@ -165,9 +186,44 @@ def distributed_rdm(x_local: torch.Tensor, n: int, pg=None,
     out = torch.zeros((n, n), dtype=torch.float32, device=x.device)
     t0, t1 = tile_ranges(n, world)[rank]
     tiles_into(x, out, t0, t1, times=times)
-    del x
     dist.all_reduce(out, op=dist.ReduceOp.SUM, group=pg)
     return out
+
+
+class PrefetchedRDMs:
+    """RDM source for all_units_rsa over stimulus-sharded features: asking for point
+    points[i] first starts the all-gather of points[i + 1], so the exchange of the next
+    point's rows overlaps this point's Gram. Every rank asks for the points in the same
+    order (all_units_rsa walks `points`), so the collectives are issued in one order."""
+
+    def __init__(self, feats: Dict[str, torch.Tensor], points: Sequence[str], n: int, pg=None,
+                 times: Optional[StepTimes] = None, tiles_into=None):
+        self.feats, self.points, self.n, self.pg, self.times = feats, list(points), n, pg, times
+        self.tiles_into = tiles_into or rdm_tiles_into
+        self.pending: Dict[str, Callable[[], torch.Tensor]] = {}
+
+    def _start(self, p: str) -> None:
+        if p not in self.pending:
+            self.pending[p] = gather_rows_async(self.feats[p], self.n, self.pg)
+
+    def __call__(self, p: str) -> torch.Tensor:
+        self._start(p)
+        i = self.points.index(p)
+        if i + 1 < len(self.points):
+            self._start(self.points[i + 1])
+        x = self.pending.pop(p)()
+        return _rdm_from_rows(x, self.n, self.pg, self.times, self.tiles_into)
+
+
+def distributed_rdm(x_local: torch.Tensor, n: int, pg=None,
+                    times: Optional[StepTimes] = None, tiles_into=None) -> torch.Tensor:
+    """Full (n, n) RDM on every rank from each rank's stimulus rows: all-gather the rows,
+    each rank writes its balanced tile range (and mirrors) into a zeroed matrix, and a
+    sum all-reduce assembles it (every entry has exactly one writer, so the sum is exact).
+    tiles_into(x, out, t0, t1, times=...) defaults to the HIP Gram kernel."""
+    tiles_into = tiles_into or rdm_tiles_into
+    x = gather_rows(x_local.float().contiguous(), n, pg)
+    return _rdm_from_rows(x, n, pg, times, tiles_into)
 
 
 # ---------------------------------------------------------------------------------------
