@@ -651,6 +651,9 @@ __global__ void k_final_top(const uint64_t* __restrict__ fpart, uint32_t nblk,
                             const PlanHeader* __restrict__ hB, int nl, double* __restrict__ scores) {
   const int lane = threadIdx.x;
   u128 tA = 0, ab = 0, tB = 0;
+  // unrolled so the loads of several partial blocks are in flight at once (the loop is
+  // otherwise one L2 round trip per block)
+#pragma unroll 8
   for (uint32_t b = 0; b < nblk; ++b) {
     const uint64_t* f = fpart + (size_t)b * 6 * LANES + lane;
     tA += ((u128)f[1 * LANES] << 64) | f[0 * LANES];

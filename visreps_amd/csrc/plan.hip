@@ -87,16 +87,15 @@ __global__ void k_chunk_groups(const uint32_t* __restrict__ gstart,
   for (int64_t c = cp + 1; c <= cg; ++c) chunk_g[c] = (uint32_t)g;
 }
 
+// One flag per lane (coalesced reads), a wave ballot packs 64 of them into two words.
 __global__ void k_pack_flags(const uint32_t* __restrict__ flags, int64_t M,
                              uint32_t* __restrict__ gflag, int64_t words) {
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= words) return;
-  uint32_t v = 0;
-  for (int b = 0; b < 32; ++b) {
-    const int64_t i = w * 32 + b;
-    if (i < M && flags[i]) v |= 1u << b;
-  }
-  gflag[w] = v;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool bit = i < M && flags[i] != 0u;
+  const uint64_t b = __ballot(bit);
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (i - lane) / 32 + (lane >> 5);  // word of this lane's half-wave
+  if ((lane & 31) == 0 && w < words) gflag[w] = (uint32_t)(lane ? (b >> 32) : b);
 }
 
 int build_plan(const float* rdm, int64_t n, int64_t ld, const PlanView& P, const PlanBuildWs& W,
@@ -130,7 +129,7 @@ int build_plan(const float* rdm, int64_t n, int64_t ld, const PlanView& P, const
                                                                   PLAN_L, P.chunk_g);
   VR_CHECK_LAUNCH();
   const int64_t words = (M + 31) / 32 + 2;
-  k_pack_flags<<<(unsigned)((words + 255) / 256), 256, 0, st>>>(W.flags, M, P.gflag, words);
+  k_pack_flags<<<(unsigned)((words * 32 + 255) / 256), 256, 0, st>>>(W.flags, M, P.gflag, words);
   VR_CHECK_LAUNCH();
   return VR_OK;
 }
