@@ -19,6 +19,9 @@ torch.manual_seed(0)
 model = CustomCNN(num_classes=1000).to(dev).eval()
 ext = FeatureExtractor(model, bench.LAYERS, extract_pre_and_post=True)
 images = make_images(range(10000), device=dev)
+if os.environ.get("CL") == "1":  # channels_last (NHWC) convolutions
+    model = model.to(memory_format=torch.channels_last)
+    images = images.contiguous(memory_format=torch.channels_last)
 batch = int(os.environ.get("BATCH", "128"))
 with torch.no_grad():
     for it in range(3):
@@ -28,5 +31,5 @@ with torch.no_grad():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
         del f
-print(f"batch={batch} cudnn.benchmark={torch.backends.cudnn.benchmark} "
+print(f"CL={os.environ.get('CL', '0')} batch={batch} cudnn.benchmark={torch.backends.cudnn.benchmark} "
       f"find={os.environ.get('MIOPEN_FIND_MODE')}: {dt * 1e3:.1f} ms", flush=True)
