@@ -1,5 +1,5 @@
-"""Encoding-score timing at an NSD-like size on one MI355X: n_train=9000, n_test=1000,
-V=2000 voxels, layers of D=4096 and D=43264 (synthetic, seeded), 1000 bootstraps."""
+"""Encoding-score timing on one MI355X: n_train=NTR (9000), n_test=1000, V=2000 voxels,
+layers of D in DIMS (4096,43264), synthetic and seeded, 1000 bootstraps."""
 import os
 import sys
 import time
@@ -17,7 +17,7 @@ n = n_tr + n_te
 z = torch.randn(n, 64, device=dev, generator=g)
 acts = {f"d{d}": torch.relu(z @ (torch.randn(64, d, device=dev, generator=g) / 8)
                             + 2 * torch.randn(n, d, device=dev, generator=g))
-        for d in (4096, 43264)}
+        for d in [int(v) for v in os.environ.get("DIMS", "4096,43264").split(",")]}
 Y = z @ torch.randn(64, v, device=dev, generator=g) + 3 * torch.randn(n, v, device=dev, generator=g)
 tr = AlignmentData({k: a[:n_tr] for k, a in acts.items()}, Y[:n_tr])
 te = AlignmentData({k: a[n_tr:] for k, a in acts.items()}, Y[n_tr:])

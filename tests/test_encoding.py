@@ -139,6 +139,21 @@ def test_dual_ridge_cv_matches_primal_oracle(dev, n, p):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,p", [(150, 20), (300, 90)])
+def test_primal_ridge_cv_matches_primal_oracle(dev, n, p):
+    import torch
+    from visreps_amd.analysis.encoding_score import ridge_cv_predict_primal
+
+    X, Y = _data(n + 30, p, 5, n + 2 * p)
+    Y[:, 4] = np.random.RandomState(2).randn(n + 30)
+    pred, alphas = ridge_cv_predict_primal(torch.from_numpy(X[:n]).to(dev), torch.from_numpy(Y[:n]).to(dev),
+                                           torch.from_numpy(X[n:]).to(dev))
+    rp, ra = E.ridge_cv(X[:n], Y[:n], X[n:])
+    assert np.array_equal(alphas, ra)
+    assert np.max(np.abs(pred.cpu().numpy() - rp)) <= 1e-4 * max(1.0, np.abs(rp).max())
+
+
+@pytest.mark.gpu
 def test_compute_encoding_score_matches_oracle(dev):
     import torch
     from visreps_amd.analysis.alignment import AlignmentData

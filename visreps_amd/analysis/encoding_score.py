@@ -19,11 +19,12 @@ sklearn ``KFold(5)`` (contiguous folds, no shuffle) over the fit rows; per fold 
 the validation predictions of the ridge fit on the other folds; score per target =
 negative summed squared error (``l2_neg_loss``), averaged over folds; per-target best
 alpha = first argmax over alphas (``local_alpha=True``); refit on all fit rows with each
-target's alpha. It runs in kernel (dual) form: with K = X X^T = Q diag(lam) Q^T the fit
+target's alpha. Wide layers (p >= n) run in kernel (dual) form: with K = X X^T = Q diag(lam) Q^T the fit
 on rows T predicts rows V as K[V, T] Q diag(1 / (lam + alpha)) Q^T Y[T], which equals the
 primal SVD solution X_V V diag(s / (s^2 + alpha)) U^T Y with lam = s^2. Eigenvalues below
 n * eps_fp32 * lam_max are treated as the exact zeros of a rank-deficient X (the primal
-SVD has no such components). K comes from the MI355X Gram kernel (``vr_gram_f32``: the
+SVD has no such components). Narrow layers (p < n) run the primal form on the p x p
+Grams X_T^T X_T of each fold (``ridge_cv_predict_primal``). K comes from the MI355X Gram kernel (``vr_gram_f32``: the
 RDM's MFMA kernel without centring or epilogue; one Gram of the stacked fit + val rows
 holds both blocks); the eigendecomposition and the small dense products run in fp64
 through torch (rocSOLVER / rocBLAS); the statistic and its bootstrap run in
@@ -48,8 +49,8 @@ from ..utils import rprint
 from ._random import LegacyRandomState
 from .rsa import percentile
 
-__all__ = ["compute_encoding_score", "gram", "corr_score", "ridge_cv_predict", "kfold_splits",
-           "ALPHAS"]
+__all__ = ["compute_encoding_score", "gram", "corr_score", "ridge_cv_predict",
+           "ridge_cv_predict_primal", "kfold_splits", "ALPHAS"]
 
 ALPHAS = np.logspace(-10, 10, 20)
 
@@ -178,6 +179,41 @@ def ridge_cv_predict(K: torch.Tensor, fit: np.ndarray, new: np.ndarray, Y_fit: t
     return pred.float(), alpha_t.cpu().numpy()
 
 
+def ridge_cv_predict_primal(X_fit: torch.Tensor, Y_fit: torch.Tensor, X_new: torch.Tensor,
+                            alphas=ALPHAS, cv: int = 5):
+    """The same RidgeCV in primal form, for layers narrower than the fit set (p < n): per
+    fold the p x p Gram X_T^T X_T on the MFMA kernel (vr_gram_f32 of X_T^T), its
+    eigendecomposition V diag(lam) V^T, and predictions X_V V diag(1/(lam + alpha))
+    V^T X_T^T Y_T (= the SVD solution with lam = s^2). Returns (predictions fp32, alphas)."""
+    dev = X_fit.device
+    Xd = X_fit.to(torch.float32)
+    Yd = Y_fit.to(dev, torch.float64)
+    a = torch.as_tensor(np.asarray(alphas, dtype=np.float64), device=dev)
+    n_fit, v = Yd.shape
+
+    def solve(rows):
+        Xt = Xd[rows]
+        lam, V, keep = _eig(gram(Xt.T.contiguous()).double())
+        VtXtY = V.T @ (Xt.double().T @ Yd[rows])
+        return lam, V, keep, VtXtY
+
+    scores = torch.zeros((len(a), v), dtype=torch.float64, device=dev)
+    for tr, va in kfold_splits(n_fit, cv):
+        lam, V, keep, W0 = solve(torch.as_tensor(tr, device=dev))
+        XV = Xd[torch.as_tensor(va, device=dev)].double() @ V
+        Yva = Yd[torch.as_tensor(va, device=dev)]
+        for j in range(len(a)):
+            W = torch.where(keep[:, None], W0 / (lam[:, None] + a[j]), torch.zeros_like(W0))
+            err = Yva - XV @ W
+            scores[j] += -(err * err).sum(0)
+    scores /= cv
+    alpha_t = a[torch.argmax(scores, dim=0)]
+    lam, V, keep, W0 = solve(torch.arange(n_fit, device=dev))
+    W = torch.where(keep[:, None], W0 / (lam[:, None] + alpha_t[None, :]), torch.zeros_like(W0))
+    pred = (X_new.to(dev, torch.float64) @ V) @ W
+    return pred.float(), alpha_t.cpu().numpy()
+
+
 def _znorm(X, mean, std):
     """Z-normalise with precomputed statistics (encoding_score.py:28-30)."""
     return (X - mean) / std
@@ -203,7 +239,10 @@ def _fit_and_score(X_fit: torch.Tensor, Y_fit: torch.Tensor, X_new: torch.Tensor
     """RidgeCV on (X_fit, Y_fit), predictions for X_new and their mean Pearson r against
     Y_new (encoding_score.py:47-62). One MFMA Gram of the stacked rows gives both kernel
     blocks."""
-    n_fit = X_fit.size(0)
+    n_fit, p = X_fit.shape
+    if p < n_fit:  # narrow layer: p x p Grams per fold (primal)
+        pred, _ = ridge_cv_predict_primal(X_fit, Y_fit, X_new, alphas)
+        return pred, corr_score(Y_new, pred)
     K = gram(torch.cat([X_fit, X_new], dim=0))
     fit = np.arange(n_fit)
     new = np.arange(n_fit, K.size(0))
