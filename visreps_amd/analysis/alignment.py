@@ -1,14 +1,22 @@
-"""Stimulus alignment containers (reference: visreps/analysis/alignment.py).
+"""Stimulus alignment (reference: visreps/analysis/alignment.py).
 
-AlignmentData and the stimulus-ID join fix the row order every RDM is built in
-(alignment.py:23-39), so they are mirrored exactly; the encoding-score dispatch is out
-of scope for this build (OUT) and raises.
+The containers and the stimulus-ID joins fix the row order every RDM is built in, so
+their semantics follow the reference exactly:
+
+* stimulus level (alignment.py:23-39): rows of the activation dump whose key has a
+  response, in dump order;
+* train/test (alignment.py:42-71): the same join for each split;
+* concept level (alignment.py:117-162): per THINGS concept (dict order, concepts with no
+  extracted image dropped) the float mean of its images' activations, cast back to the
+  layer dtype, paired with the concept's embedding (float32);
+* dispatch (alignment.py:74-114): analysis=rsa -> compute_rsa, analysis=encoding_score ->
+  compute_encoding_score (refused for things-behavior).
 """
 from __future__ import annotations
 
 import logging
 from dataclasses import dataclass
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -28,7 +36,8 @@ __all__ = [
 
 @dataclass
 class AlignmentData:
-    """Activations and neural data for one split (alignment.py:14-20)."""
+    """One split: per-layer activations (rows = stimuli or concepts), the matching neural
+    or behavioural targets, and the IDs that fix the row order (alignment.py:14-20)."""
 
     activations: Dict[str, torch.Tensor]
     neural: torch.Tensor
@@ -36,72 +45,72 @@ class AlignmentData:
     concept_image_ids: Optional[Dict[str, List[str]]] = None
 
 
+def _take_rows(a, rows: Sequence[int]):
+    """a[rows] for a tensor (on its own device) or any numpy-indexable array."""
+    if isinstance(a, torch.Tensor):
+        return a.index_select(0, torch.as_tensor(list(rows), dtype=torch.long, device=a.device))
+    return a[list(rows)]
+
+
 def _align_stimulus_level(acts_raw, targets, keys):
-    """Rows of acts_raw whose key is in targets, in the order of keys (alignment.py:23-39).
-    Returns (acts, neural, matched_ids)."""
-    idx = [i for i, k in enumerate(keys) if str(k) in targets]
-    matched_ids = [str(keys[i]) for i in idx]
-    if not matched_ids:
-        neural = torch.empty(0, dtype=torch.float32)
-        acts = {l: a[:0] for l, a in acts_raw.items()}
-        return acts, neural, matched_ids
-    neural = torch.as_tensor(np.stack([targets[sid] for sid in matched_ids]), dtype=torch.float32)
-    acts = {}
-    for l, a in acts_raw.items():
-        acts[l] = a[torch.as_tensor(idx, dtype=torch.long, device=a.device)] if isinstance(
-            a, torch.Tensor) else a[idx]
-    return acts, neural, matched_ids
+    """(acts, neural, ids): the dump rows whose key is in `targets`, dump order."""
+    hits = [(row, str(key)) for row, key in enumerate(keys) if str(key) in targets]
+    ids = [sid for _, sid in hits]
+    if not hits:
+        return {name: a[:0] for name, a in acts_raw.items()}, torch.empty(0, dtype=torch.float32), ids
+    rows = [row for row, _ in hits]
+    neural = torch.as_tensor(np.stack([targets[sid] for sid in ids]), dtype=torch.float32)
+    return {name: _take_rows(a, rows) for name, a in acts_raw.items()}, neural, ids
 
 
-def prepare_traintest_alignment(cfg, acts_raw, neural_data_raw, keys) -> Tuple[AlignmentData, AlignmentData]:
-    """Train and test AlignmentData from one activation dump (alignment.py:42-71)."""
-    tr_a, tr_n, tr_ids = _align_stimulus_level(acts_raw, neural_data_raw["train"], keys)
-    te_a, te_n, te_ids = _align_stimulus_level(acts_raw, neural_data_raw["test"], keys)
-    return (AlignmentData(tr_a, tr_n, stimulus_ids=tr_ids),
-            AlignmentData(te_a, te_n, stimulus_ids=te_ids))
+def prepare_traintest_alignment(cfg, acts_raw, neural_data_raw, keys) -> Tuple[AlignmentData, AlignmentData]:  # noqa: ARG001
+    """Train and test AlignmentData from one activation dump."""
+    splits = []
+    for part in ("train", "test"):
+        acts, neural, ids = _align_stimulus_level(acts_raw, neural_data_raw[part], keys)
+        splits.append(AlignmentData(acts, neural, stimulus_ids=ids))
+    return splits[0], splits[1]
 
 
 def compute_traintest_alignment(cfg, train: AlignmentData, test: AlignmentData,
                                 verbose: bool = False, re_extract_fn=None) -> List[dict]:
-    """RSA dispatch (alignment.py:74-114). n_select defaults to None (all train)."""
-    analysis = cfg.get("analysis", "rsa").lower()
-    bootstrap = cfg.get("bootstrap", True)
-    n_bootstrap = cfg.get("n_bootstrap", 1000)
-    if analysis == "encoding_score" and cfg.get("neural_dataset", "").lower() == "things-behavior":
-        raise ValueError(
-            "Encoding score is not supported for things-behavior (behavioral embeddings "
-            "have no voxels to predict). Use analysis=rsa instead."
-        )
-    if analysis == "rsa":
-        return compute_rsa(cfg, train, test, n_select=cfg.get("n_select", None),
-                           bootstrap=bootstrap, n_bootstrap=n_bootstrap, verbose=verbose,
-                           re_extract_fn=re_extract_fn)
+    """Dispatch on cfg.analysis. n_select defaults to None (all train stimuli)."""
+    analysis = str(cfg.get("analysis", "rsa")).lower()
+    dataset = str(cfg.get("neural_dataset", "")).lower()
+    common = dict(bootstrap=cfg.get("bootstrap", True), n_bootstrap=cfg.get("n_bootstrap", 1000),
+                  verbose=verbose)
     if analysis == "encoding_score":
+        if dataset == "things-behavior":
+            raise ValueError(
+                "Encoding score is not supported for things-behavior (behavioral embeddings "
+                "have no voxels to predict). Use analysis=rsa instead."
+            )
         from .encoding_score import compute_encoding_score
 
         pca_k = cfg.get("pca_k", 1) if cfg.get("reconstruct_from_pcs") else None
-        return compute_encoding_score(train, test, bootstrap=bootstrap, n_bootstrap=n_bootstrap,
-                                      verbose=verbose, reconstruct_pca_k=pca_k)
+        return compute_encoding_score(train, test, reconstruct_pca_k=pca_k, **common)
+    if analysis == "rsa":
+        return compute_rsa(cfg, train, test, n_select=cfg.get("n_select", None),
+                           re_extract_fn=re_extract_fn, **common)
     raise ValueError(f"Unknown analysis method: {analysis}")
 
 
-def prepare_concept_alignment(cfg, acts_raw, neural_data_raw, keys) -> AlignmentData:
-    """Concept-mean activations paired with behavioural embeddings (alignment.py:117-162)."""
-    key_to_idx = {k: i for i, k in enumerate(keys)}
-    embeddings = neural_data_raw["embeddings"]
-    image_ids = neural_data_raw["image_ids"]
-    concepts, concept_image_ids = [], {}
-    concept_acts = {l: [] for l in acts_raw}
-    for concept, img_ids in image_ids.items():
-        indices = [key_to_idx[sid] for sid in img_ids if sid in key_to_idx]
-        if not indices:
-            continue
-        concepts.append(concept)
-        concept_image_ids[concept] = [sid for sid in img_ids if sid in key_to_idx]
-        for l, a in acts_raw.items():
-            sel = a[torch.as_tensor(indices, dtype=torch.long, device=a.device)]
-            concept_acts[l].append(sel.float().mean(0))
-    acts = {l: torch.stack(vs).to(acts_raw[l].dtype) for l, vs in concept_acts.items()}
-    neural = torch.as_tensor(np.stack([embeddings[c] for c in concepts], dtype=np.float32))
+def prepare_concept_alignment(cfg, acts_raw, neural_data_raw, keys) -> AlignmentData:  # noqa: ARG001
+    """Concept-mean activations paired with behavioural embeddings."""
+    where = {k: i for i, k in enumerate(keys)}
+    groups: Dict[str, List[str]] = {}
+    for concept, images in neural_data_raw["image_ids"].items():
+        present = [sid for sid in images if sid in where]
+        if present:  # a concept none of whose images was extracted has no row
+            groups[concept] = present
+    concepts = list(groups)
+
+    def concept_means(a):
+        rows = [_take_rows(a, [where[sid] for sid in groups[c]]).float().mean(0) for c in concepts]
+        return torch.stack(rows).to(a.dtype)
+
+    acts = {name: concept_means(a) for name, a in acts_raw.items()}
+    emb = neural_data_raw["embeddings"]
+    neural = torch.as_tensor(np.stack([emb[c] for c in concepts], dtype=np.float32))
     logger.info("Prepared concept alignment: %d concepts.", len(concepts))
-    return AlignmentData(acts, neural, stimulus_ids=concepts, concept_image_ids=concept_image_ids)
+    return AlignmentData(acts, neural, stimulus_ids=concepts, concept_image_ids=groups)
