@@ -73,6 +73,18 @@ int vr_rdm_pearson_tiles_f32(const float* X, int64_t n, int64_t d, int64_t ldx, 
                              int64_t ldr, float correction, int64_t tile_begin,
                              int64_t tile_end, void* ws, size_t ws_bytes, void* stream);
 
+/* bf16 features (X holds the 16-bit patterns of torch.bfloat16, row-major with leading
+ * dimension ldx): the same RDM as vr_rdm_pearson_f32 of X.float() (rsa.py:76 widens any
+ * dtype to fp32), computed on the split bf16 MFMA Gram without an fp32 copy of X; the
+ * row statistics and the centring read the bf16 values directly (cfg5: ViT / CLIP
+ * features at N = 50k). Tile ranges as vr_rdm_pearson_tiles_f32. */
+size_t vr_rdm_bf16_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end);
+int vr_rdm_pearson_bf16(const uint16_t* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
+                        int64_t ldr, float correction, void* ws, size_t ws_bytes, void* stream);
+int vr_rdm_pearson_tiles_bf16(const uint16_t* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
+                              int64_t ldr, float correction, int64_t tile_begin, int64_t tile_end,
+                              void* ws, size_t ws_bytes, void* stream);
+
 /* Plain symmetric Gram G = X X^T (fp32 out; the same MFMA kernels, tiling and accuracy
  * as the RDM, without centring or the correlation epilogue). The kernel matrix of the
  * encoding score's ridge regression: replaces the SVD inside himalaya 0.4.9's
@@ -163,6 +175,13 @@ int vr_bootstrap_spearman_multi(const void* plan_a, const void* const* planBs, i
                                 int64_t n, const int32_t* idx, int64_t k, int64_t n_sets,
                                 int full_first, double* scores, int64_t ld_scores, void* ws,
                                 size_t ws_bytes, void* stream);
+
+/* Passes of the bootstrap engines run in a one-gather-per-pair form (absolute ranks kept
+ * modulo 2^16 and recovered against an interpolated count table). A pass whose ranks the
+ * table cannot recover (very large tie groups, adversarial orders) is re-run in the
+ * exact chunk-base form; this counter is the number of such re-runs in the process so
+ * far (scores never depend on it). VISREPS_ENGINE_EST=0 forces the chunk-base form. */
+int64_t vr_engine_est_reruns(void);
 
 /* One-shot form: builds both plans in the workspace, then runs the engine. */
 size_t vr_bootstrap_spearman_workspace(int64_t n);

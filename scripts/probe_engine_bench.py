@@ -1,0 +1,39 @@
+"""Engine probe on the bench's own RDMs: the 14 CustomCNN points (random init, seed 0) of
+10k synthetic images against the V1 neural RDM, one vr_bootstrap_spearman_multi call
+(14 units x 1001 subsets), timed REPS times. ALT_LIB=path selects another library build."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+import torch
+if os.environ.get("ALT_LIB"):
+    import visreps_amd._lib as _L
+    _L.LIB_PATH = os.environ["ALT_LIB"]
+from bench import LAYERS, extract
+from visreps_amd.analysis import rsa as R
+from visreps_amd.analysis._random import bootstrap_indices
+from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_responses
+from visreps_amd.models.custom_model import CustomCNN
+from visreps_amd.models.utils import FeatureExtractor
+
+dev = torch.device("cuda", 0)
+N = 10000
+torch.manual_seed(0)
+model = CustomCNN(num_classes=1000).to(dev).eval()
+ex = FeatureExtractor(model, LAYERS, extract_pre_and_post=True)
+images = make_images(range(N), device=dev)
+y = make_responses(images, range(N), {"V1": NSD_ROIS_4["V1"]})["V1"]
+feats = extract(ex, images, 128)
+del images
+neural = R.RankPlan(R.compute_rdm(y))
+models = []
+for p in list(feats):
+    models.append(R.RankPlan(R.compute_rdm(feats.pop(p))))
+torch.cuda.empty_cache()
+idx = torch.from_numpy(bootstrap_indices(42, N, int(0.9 * N), 1000).copy()).to(dev)
+ts = []
+for _ in range(int(os.environ.get("REPS", 2))):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(); s = R.bootstrap_spearman_multi(neural, models, idx); b.record(); torch.cuda.synchronize()
+    ts.append(a.elapsed_time(b))
+print(f"engine bench-RDMs NB={len(models)}: {min(ts) / len(models):.2f} ms/unit  "
+      f"checksum={float(s.double().sum()):.15g}", flush=True)

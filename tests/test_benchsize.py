@@ -1,0 +1,220 @@
+"""Parity at the bench's own sizes and precision (BASELINE.json configs[1], [2], [4]).
+
+The bench builds every Gram with the bf16x3 split kernel (n^2 d >= 1e10), so these tests
+check that kernel on the bench's own inputs against float64 ground truth:
+
+* configs[1] (N = 10k): the 14 CustomCNN points of the bench (random-init weights,
+  synthetic images: exactly bench.py's features, D = 290,400 ... 4,096) and the §8(d)
+  synthetic features at D = 290,400 / 186,624 / 43,264:
+    - RDM rows vs a float64 recomputation on 64 sampled rows, <= 5e-6;
+    - point + all 1000 bootstrap Spearman scores (RandomState(42) subsets, evals.py:355-373)
+      of the split RDMs vs the same scores of the float64 RDMs rounded to fp32 (the RDM
+      an exact reference would produce), and of the exact-fp32 kernel's RDMs
+      (VISREPS_GRAM=fp32): |dSpearman| < 1e-5, the north-star tolerance.
+* configs[2]: the 73k x 43,264 RDM (one GPU), float64 rows, exact symmetry, zero diagonal.
+* configs[4]: ViT-B/16 block tokens (D = 151,296) and the CLS embedding in bf16 at
+  N = 50k, RDM straight from the bf16 features (no fp32 copy), float64 rows.
+
+Reference semantics: rsa.py:59-93 (RDM), rsa.py:96-129 (Spearman), evals.py:341-373.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from visreps_amd.analysis import rsa as R
+from visreps_amd.analysis._random import bootstrap_indices
+
+pytestmark = pytest.mark.gpu
+
+N, NB = 10000, 1000
+SPEARMAN_TOL = 1e-5  # BASELINE.json north_star: |dSpearman| < 1e-5 vs CPU
+ROW_TOL = 5e-6
+
+
+class gram_mode:
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        self.old = os.environ.get("VISREPS_GRAM")
+        os.environ["VISREPS_GRAM"] = self.mode
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("VISREPS_GRAM", None)
+        else:
+            os.environ["VISREPS_GRAM"] = self.old
+
+
+def _centred_f64(x):
+    xd = x.double()
+    xd -= xd.mean(1, keepdim=True)
+    s = torch.sqrt((xd * xd).mean(1) + 1e-12)
+    return xd, s
+
+
+def rdm_f64_rows(x, rows):
+    """float64 RDM rows `rows` of x (rsa.py:76-92 in exact arithmetic)."""
+    xd, s = _centred_f64(x)
+    g = xd[rows] @ xd.T / x.size(1)
+    out = 1.0 - (g / (s[rows, None] * s[None, :] + 1e-12)).clamp(-1, 1)
+    out[torch.arange(len(rows), device=x.device), rows] = 0.0
+    return out
+
+
+def rdm_f64(x, block=2048):
+    """Whole float64 RDM of x, rounded to fp32 (what an exact-arithmetic reference
+    compute_rdm would return)."""
+    xd, s = _centred_f64(x)
+    n = x.size(0)
+    out = torch.empty((n, n), dtype=torch.float32, device=x.device)
+    for r0 in range(0, n, block):
+        r1 = min(n, r0 + block)
+        g = xd[r0:r1] @ xd.T / x.size(1)
+        c = (g / (s[r0:r1, None] * s[None, :] + 1e-12)).clamp(-1, 1)
+        c[torch.arange(r1 - r0, device=x.device), torch.arange(r0, r1, device=x.device)] = 1.0
+        out[r0:r1] = (1.0 - c).float()
+    del xd
+    return out
+
+
+def _rows(dev, n, seed=1):
+    return torch.randperm(n, device=dev, generator=torch.Generator(device=dev).manual_seed(seed))[:64]
+
+
+def _scores(a, b, idx):
+    return R.bootstrap_spearman(R.RankPlan(a), R.RankPlan(b), idx, full_first=True).cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def idx():
+    return bootstrap_indices(42, N, int(0.9 * N), NB)
+
+
+# ------------------------------------------------------------------------ bench features
+@pytest.fixture(scope="module")
+def bench(dev):
+    """bench.py's inputs: random-init CustomCNN (seed 0), 10k synthetic images, the 14
+    flattened points, and the V1 responses."""
+    from bench import LAYERS, extract
+    from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_responses
+    from visreps_amd.models.custom_model import CustomCNN
+    from visreps_amd.models.utils import FeatureExtractor
+
+    torch.manual_seed(0)
+    model = CustomCNN(num_classes=1000).to(dev).eval()
+    ex = FeatureExtractor(model, LAYERS, extract_pre_and_post=True)
+    images = make_images(range(N), device=dev)
+    y = make_responses(images, range(N), {"V1": NSD_ROIS_4["V1"]})["V1"]
+    feats = extract(ex, images, 128)
+    del images
+    neural_split = R.compute_rdm(y)
+    neural_64 = rdm_f64(y)
+    with gram_mode("fp32"):
+        neural_32 = R.compute_rdm(y)
+    return feats, neural_split, neural_64, neural_32
+
+
+POINTS = [f"{l}_{s}" for l in ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
+          for s in ("pre", "post")]
+
+
+@pytest.mark.parametrize("point", POINTS)
+def test_bench_point_split_gram_parity(dev, bench, idx, point):
+    feats, neural_split, neural_64, neural_32 = bench
+    x = feats[point]
+    assert x.size(0) == N
+    rdm = R.compute_rdm(x)
+    rows = _rows(dev, N)
+    err = float((rdm[rows].double() - rdm_f64_rows(x, rows)).abs().max())
+    assert err <= ROW_TOL, (point, x.size(1), err)
+    assert torch.all(torch.diagonal(rdm) == 0)
+    ref64 = rdm_f64(x)
+    with gram_mode("fp32"):
+        rdm32 = R.compute_rdm(x)
+    s_split = _scores(rdm, neural_split, idx)
+    s_64 = _scores(ref64, neural_64, idx)
+    s_32 = _scores(rdm32, neural_32, idx)
+    d64 = float(np.max(np.abs(s_split - s_64)))
+    d32 = float(np.max(np.abs(s_split - s_32)))
+    assert d64 < SPEARMAN_TOL, (point, d64)
+    assert d32 < SPEARMAN_TOL, (point, d32)
+    assert float(np.max(np.abs(s_32 - s_64))) < SPEARMAN_TOL
+
+
+# ------------------------------------------------------------------ §8(d) synthetic widths
+@pytest.mark.parametrize("d", [290400, 186624, 43264])
+def test_synthetic_width_split_gram_parity(dev, idx, d):
+    g = torch.Generator(device=dev).manual_seed(20260306)
+    z = torch.randn(N, 64, device=dev, generator=g)
+    x = z @ (torch.randn(64, d, device=dev, generator=g) / 8)
+    x += 2 * torch.randn(N, d, device=dev, generator=g)
+    x.relu_()
+    y = z @ torch.randn(64, 2000, device=dev, generator=g) + 3 * torch.randn(N, 2000, device=dev, generator=g)
+    rdm = R.compute_rdm(x)
+    rows = _rows(dev, N, 3)
+    err = float((rdm[rows].double() - rdm_f64_rows(x, rows)).abs().max())
+    assert err <= ROW_TOL, (d, err)
+    s_split = _scores(rdm, R.compute_rdm(y), idx)
+    s_64 = _scores(rdm_f64(x), rdm_f64(y), idx)
+    assert float(np.max(np.abs(s_split - s_64))) < SPEARMAN_TOL
+
+
+# ----------------------------------------------------------------------------- configs[2]
+def test_cfg3_73k_rdm(dev):
+    n, d = 73000, 43264
+    g = torch.Generator(device=dev).manual_seed(7)
+    z = torch.randn(n, 64, device=dev, generator=g)
+    x = z @ (torch.randn(64, d, device=dev, generator=g) / 8)
+    x += 2 * torch.randn(n, d, device=dev, generator=g)
+    x.relu_()
+    del z
+    rdm = R.compute_rdm(x)
+    rows = _rows(dev, n, 5)
+    err = float((rdm[rows].double() - rdm_f64_rows(x, rows)).abs().max())
+    assert err <= ROW_TOL, err
+    assert torch.all(torch.diagonal(rdm) == 0)
+    cols = _rows(dev, n, 6)
+    assert torch.equal(rdm[rows][:, cols], rdm[cols][:, rows].T)  # exact symmetry, sampled
+    assert torch.all(rdm[rows] >= 0) and torch.all(rdm[rows] <= 2)
+
+
+# ----------------------------------------------------------------------------- configs[4]
+@pytest.fixture(scope="module")
+def vit_tokens(dev):
+    """ViT-B/16 (random init, torchvision layout) on 50k synthetic images in bf16: the
+    tokens of encoder block 6 (197 x 768 = 151,296 features) and the final CLS."""
+    from visreps_amd.dataloaders.synthetic import make_images
+    from visreps_amd.models.standard_model import ViTBase
+    from visreps_amd.models.utils import FeatureExtractor
+
+    n = 50000
+    torch.manual_seed(0)
+    model = ViTBase("none").to(dev).eval().to(torch.bfloat16)
+    ex = FeatureExtractor(model, ["block6"], extract_pre_and_post=False)
+    block = torch.empty((n, 197 * 768), dtype=torch.bfloat16, device=dev)
+    cls = torch.empty((n, 768), dtype=torch.bfloat16, device=dev)
+    with torch.no_grad():
+        for b0 in range(0, n, 1000):
+            imgs = make_images(range(b0, b0 + 1000), device=dev, dtype=torch.bfloat16)
+            ex.features = {}
+            tokens = model.forward_features(imgs)  # fires the block6 hook
+            block[b0:b0 + 1000] = ex.features["block6"].reshape(1000, -1)
+            cls[b0:b0 + 1000] = tokens[:, 0]
+    return block, cls
+
+
+@pytest.mark.parametrize("which", ["block6", "cls"])
+def test_cfg5_vit_bf16_rdm(dev, vit_tokens, which):
+    x = vit_tokens[0] if which == "block6" else vit_tokens[1]
+    assert x.dtype == torch.bfloat16
+    rdm = R.compute_rdm(x)  # bf16 kernels: no fp32 copy of the features
+    assert rdm.dtype == torch.float32 and rdm.shape == (x.size(0), x.size(0))
+    rows = _rows(dev, x.size(0), 9)
+    err = float((rdm[rows].double() - rdm_f64_rows(x.float(), rows)).abs().max())
+    assert err <= ROW_TOL, (which, err)
+    assert torch.all(torch.diagonal(rdm) == 0)
+    cols = _rows(dev, x.size(0), 10)
+    assert torch.equal(rdm[rows][:, cols], rdm[cols][:, rows].T)

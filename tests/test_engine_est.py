@@ -1,0 +1,118 @@
+"""The bootstrap engine's one-gather-per-pair (EST) pass form against its exact chunk-base
+form and the CPU oracle.
+
+EST keeps each pair's absolute doubled A rank modulo 2^16 and recovers it on the B side
+from an interpolated count table; a pass whose ranks cannot be recovered is re-run in the
+exact form. Both forms are exact integer arithmetic, so scores must agree bit for bit
+(VISREPS_ENGINE_EST=1 selects the EST form, =0 the exact form, for every pass).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import rsa_oracle as O
+from visreps_amd._lib import lib
+from visreps_amd.analysis import rsa as R
+from visreps_amd.analysis._random import bootstrap_indices
+
+pytestmark = pytest.mark.gpu
+
+
+class _engine_form:
+    def __init__(self, value):
+        self.value = value
+
+    def __enter__(self):
+        self.old = os.environ.get("VISREPS_ENGINE_EST")
+        os.environ["VISREPS_ENGINE_EST"] = self.value
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("VISREPS_ENGINE_EST", None)
+        else:
+            os.environ["VISREPS_ENGINE_EST"] = self.old
+
+
+def exact_engine():
+    """Context: every engine pass in the exact chunk-base form."""
+    return _engine_form("0")
+
+
+@pytest.fixture(autouse=True)
+def est_engine():
+    """Every test of this module runs the EST form unless it asks for the exact one."""
+    with _engine_form("1"):
+        yield
+
+
+def _rdm(dev, n, d, seed, relu=False):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.randn(n, d, device=dev, generator=g)
+    return R.compute_rdm(torch.relu(x) if relu else x)
+
+
+@pytest.mark.parametrize("n,nb", [(40, 70), (700, 200), (3000, 130)])
+def test_est_equals_exact_form(dev, n, nb):
+    a, b = _rdm(dev, n, 64, 1, relu=True), _rdm(dev, n, 300, 2)
+    idx = bootstrap_indices(42, n, int(0.9 * n), nb)
+    pa, pb = R.RankPlan(a), R.RankPlan(b)
+    r0 = int(lib().vr_engine_est_reruns())
+    est = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    assert int(lib().vr_engine_est_reruns()) == r0, "continuous RDMs must not need the exact re-run"
+    with exact_engine():
+        ref = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    assert np.array_equal(est, ref)
+
+
+def test_est_multi_equals_exact_form(dev):
+    n = 1500
+    neural = R.RankPlan(_rdm(dev, n, 200, 3))
+    models = [R.RankPlan(_rdm(dev, n, 50 * (i + 1), 10 + i, relu=i % 2 == 0)) for i in range(4)]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 100)
+    est = R.bootstrap_spearman_multi(neural, models, idx, full_first=True).cpu().numpy()
+    with exact_engine():
+        ref = R.bootstrap_spearman_multi(neural, models, idx, full_first=True).cpu().numpy()
+    assert np.array_equal(est, ref)
+    for j, pm in enumerate(models):  # and each row equals the per-unit call
+        one = R.bootstrap_spearman(pm, neural, idx, full_first=True).cpu().numpy()
+        assert np.array_equal(est[j], one)
+
+
+def test_est_triangle_entry_point_matches_oracle(dev):
+    # vr_spearman_triu_f32 runs one lane (lw = 1, FULL = false) in the EST form
+    n = 900
+    a, b = _rdm(dev, n, 40, 5), _rdm(dev, n, 70, 6, relu=True)
+    got = R.compute_rdm_correlation(a, b, correlation="Spearman")
+    ref = O.compute_rdm_correlation(a.cpu().numpy(), b.cpu().numpy(), "Spearman")
+    assert abs(got - ref) <= 1e-12
+
+
+def test_est_giant_tie_groups_fall_back_to_exact(dev):
+    # Five distinct RDM values over 499,500 pairs: tie groups of ~100k positions, whose
+    # shared midrank is ~80k counts from the interpolated estimate at the group ends, so
+    # EST flags the passes and they are re-run in the exact form (u32 chunk ranks, 128-bit
+    # tie sums). Scores must equal the exact form and the oracle.
+    n = 1000
+    rs = np.random.RandomState(0)
+    vals = rs.randint(0, 5, size=(n, n)).astype(np.float32) / 4.0
+    a = np.triu(vals, 1)
+    a = a + a.T
+    b = np.triu(rs.rand(n, n).astype(np.float32), 1)
+    b = b + b.T
+    ta, tb = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+    idx = bootstrap_indices(42, n, int(0.9 * n), 70)
+    pa, pb = R.RankPlan(ta), R.RankPlan(tb)
+    r0 = int(lib().vr_engine_est_reruns())
+    est = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    assert int(lib().vr_engine_est_reruns()) > r0, "giant tie groups must trigger the exact re-run"
+    with exact_engine():
+        ref = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    assert np.array_equal(est, ref)
+    # oracle: point + the first 3 subsets (scipy on the explicit sub-RDMs)
+    assert abs(est[0] - O.compute_rdm_correlation(a, b, "Spearman")) <= 1e-12
+    for s in range(3):
+        i = np.asarray(idx[s])
+        ref_s = O.compute_rdm_correlation(a[np.ix_(i, i)], b[np.ix_(i, i)], "Spearman")
+        assert abs(est[1 + s] - ref_s) <= 1e-12

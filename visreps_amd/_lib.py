@@ -23,7 +23,9 @@ __all__ = [
     "EXPORTED_SYMBOLS",
 ]
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvisreps_hip.so")
+# VISREPS_AMD_LIB selects another build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("VISREPS_AMD_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libvisreps_hip.so")
 
 
 class VisrepsHipError(RuntimeError):
@@ -48,6 +50,15 @@ _PROTOTYPES = {
     "vr_rdm_tile_rect": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "vr_rdm_tiles_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64]),
     "vr_rdm_pearson_tiles_f32": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _c_i64, _c_i64, _vp, _c_sz, _vp],
+    ),
+    "vr_rdm_bf16_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64]),
+    "vr_rdm_pearson_bf16": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _vp, _c_sz, _vp],
+    ),
+    "vr_rdm_pearson_tiles_bf16": (
         ctypes.c_int,
         [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _c_i64, _c_i64, _vp, _c_sz, _vp],
     ),
@@ -90,6 +101,7 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _c_sz, _vp],
     ),
+    "vr_engine_est_reruns": (_c_i64, []),
     "vr_bootstrap_spearman_workspace": (_c_sz, [_c_i64]),
     "vr_bootstrap_spearman_f32": (
         ctypes.c_int,

@@ -14,7 +14,7 @@ import numpy as np
 
 from .._lib import check, lib
 
-__all__ = ["LegacyRandomState", "bootstrap_indices"]
+__all__ = ["LegacyRandomState", "bootstrap_indices", "draw_bootstrap_indices"]
 
 
 class LegacyRandomState:
@@ -54,10 +54,17 @@ class LegacyRandomState:
         return out
 
 
+def draw_bootstrap_indices(seed: int, n: int, k: int, n_draws: int) -> np.ndarray:
+    """``[RandomState(seed).choice(n, k, replace=False) for _ in range(n_draws)]`` as an
+    int32 (n_draws, k) array, drawn now (host MT19937, no cache)."""
+    out = np.empty((int(n_draws), int(k)), dtype=np.int32)
+    check(lib().vr_legacy_choice(int(seed), int(n), int(k), int(n_draws), out.ctypes.data), "vr_legacy_choice")
+    return out
+
+
 @functools.lru_cache(maxsize=8)
 def _cached_bootstrap_indices(seed: int, n: int, k: int, n_draws: int) -> np.ndarray:
-    out = np.empty((n_draws, k), dtype=np.int32)
-    check(lib().vr_legacy_choice(seed, n, k, n_draws, out.ctypes.data), "vr_legacy_choice")
+    out = draw_bootstrap_indices(seed, n, k, n_draws)
     out.setflags(write=False)
     return out
 

@@ -104,6 +104,22 @@ def compute_rdm(
     if representations.ndim != 2:
         raise ValueError("representations must be a 2-D (n_samples, n_features) tensor")
     dev = _device_for(representations)
+    if (corr == "pearson" and representations.dtype == torch.bfloat16 and representations.size(0) > 0
+            and representations.size(1) > 0):
+        # bf16 features (ViT / CLIP, cfg5): the kernels widen them on the fly (rsa.py:76's
+        # X.float()); no fp32 copy of the (n, d) features is made
+        x = representations.to(dev)
+        if x.stride(1) != 1 or x.stride(0) < x.size(1):
+            x = x.contiguous()
+        n, d = x.shape
+        out = torch.empty((n, n), dtype=torch.float32, device=dev)
+        L = lib()
+        t = int(L.vr_rdm_tile_count(n))
+        ws = workspace.get(dev, L.vr_rdm_bf16_workspace(n, d, 0, t), "rdm")
+        with torch.cuda.device(dev):
+            check(L.vr_rdm_pearson_bf16(_ptr(x), n, d, x.stride(0), _ptr(out), n, float(correction),
+                                        _ptr(ws), ws.numel(), stream_of(dev)), "vr_rdm_pearson_bf16")
+        return out if representations.is_cuda else out.cpu()
     x = _as_device_f32(representations, dev)
     if corr == "spearman":
         x = _rank(x)

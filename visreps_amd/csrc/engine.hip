@@ -27,6 +27,9 @@
 //            row per pair); per B group S = sum of included yA; sums S y'_B, S, k y'_B,
 //            k y'_B^2 (segment-relative)
 //  scan + k_final_part + k_final_top   combine segments with their bases -> rho per lane
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -41,22 +44,73 @@ constexpr int ENG_THREADS = VR_ENG_THREADS;  // waves per workgroup share one LD
 constexpr int WAVES_PER_WG = ENG_THREADS / 64;
 constexpr int SCAN_SEGS = 256;     // segments per block in the segment scans / final fold
 
+// ---------------------------------------------------------------------------------
+// Count-estimate table (EST mode, the default pass form).
+// The A side stores each pair's ABSOLUTE doubled rank y_A modulo 2^16 (one u16 per subset,
+// a 128-byte row per pair). The B side recovers y_A exactly from those 16 bits and the low
+// end lo of a 2^16-wide window known to hold it: y_A = lo + (u16)(t - lo). lo interpolates
+// the doubled included count between coarse boundaries q_c = c 2^b in 4096 steps per
+// interval: lo = L_c + D_c * step (one v_mad_u32_u24 per pair and lane; {L_c, D_c} per
+// interval and lane, <= EST_NC rows of 64 lanes staged in LDS), so the only per-pair
+// global access of the B walk is the TB row. Measured on N=10k RDMs the interpolation error is a few hundred counts
+// (profiles/r2_est_deviation.log) against the 2^14 the 16 bits allow; the A walk checks
+// every stored value against the same estimate and flags the pass, and flagged passes
+// are re-run in the exact chunk-base form (baseA rows), so scores never depend on it.
+// ---------------------------------------------------------------------------------
+constexpr int EST_NC = 256;
+constexpr int EST_STEP_BITS = 12;  // interpolation steps per interval: 2^12
+#ifndef VR_EST_CHECK
+#define VR_EST_CHECK 1  // 0: timing probe only (no A-side recoverability checks: unsafe)
+#endif
+static std::atomic<int64_t> g_est_reruns{0};  // passes re-run in the exact form (vr_engine_est_reruns)  // coarse intervals at most: table <= 128 x 256 B = 32 KB
+
+// log2 of the coarse interval: the smallest b >= 12 (windows of 64 never straddle a
+// boundary; the 4096 steps are whole positions) with ceil(M / 2^b) <= 96, or, for larger
+// triangles, <= EST_NC (a step of 2^(b-12) positions moves lo by <= 2^(b-11): b <= 23
+// keeps that at a few thousand of the 2^15 of slack).
+static int est_bits(int64_t M) {
+  int b = 12;
+  while (((M + ((int64_t)1 << b) - 1) >> b) > 96 && b < 23) ++b;
+  while (((M + ((int64_t)1 << b) - 1) >> b) > EST_NC) ++b;
+  return b;
+}
+static uint32_t est_intervals(int64_t M, int b) { return (uint32_t)((M + ((int64_t)1 << b) - 1) >> b); }
+static size_t est_table_bytes(int64_t M) {
+  return M > 0 ? (size_t)est_intervals(M, est_bits(M)) * LANES * sizeof(uint2) : 0;
+}
+
+// EST form only with VISREPS_ENGINE_EST=1. Measured in the bench (profiles/r2_engine_ab.log):
+// the exact form's k_rankB runs 1.90 ms per pass at two workgroups per CU; the EST form's
+// 1.94-2.04 ms (its saved chunk-base gather is paid back in per-pair VALU/SALU work and in
+// the L2 mask reads it needs for the same occupancy), so the exact form is the default.
+static bool engine_est() {
+  const char* e = getenv("VISREPS_ENGINE_EST");
+  return e && strcmp(e, "1") == 0;
+}
+
+// Launch shape. The walks are bound by the latency of their random TB gathers, so they run
+// two 16-wave workgroups per CU (32 waves): the exact-form kernels and the EST count
+// pre-pass keep the masks in LDS while two copies fit (N <= 10176), the EST rank walks
+// read them from L2 (80 KB at N = 10k) and hold only the interval table in LDS.
 struct EngineCfg {
   int grid;      // workgroups
   int nwaves;    // grid * WAVES_PER_WG = number of chunk segments (A and B each)
-  size_t lds;    // dynamic LDS for the masks (0: masks read from global)
-  bool use_lds;
+  bool use_lds;  // exact kernels, k_countA: masks in LDS
+  size_t lds;    // their dynamic LDS (the masks, or 0)
+  size_t tab;    // EST rank walks: dynamic LDS = the interval table
 };
 
 static EngineCfg engine_cfg(int64_t n) {
   EngineCfg c;
   const size_t need = (size_t)n * sizeof(uint64_t);
+  c.tab = est_table_bytes(pairs_of(n));
   const size_t cap = 160 * 1024 - 1024;
-  c.use_lds = need <= cap;
-  const int per_cu = c.use_lds ? std::max<int>(1, std::min<int>(2, (int)(cap / std::max<size_t>(need, 1)))) : 2;
+  const char* e = getenv("VISREPS_ENGINE_MASKS");  // "global": masks from L2 (A/B timing)
+  c.use_lds = need <= cap && !(e && strcmp(e, "global") == 0);
+  c.lds = c.use_lds ? need : 0;
+  const int per_cu = std::max<int>(1, std::min<int>(2048 / ENG_THREADS, (int)(cap / std::max<size_t>(c.lds, 1))));
   c.grid = num_cus() * per_cu;
   c.nwaves = c.grid * WAVES_PER_WG;
-  c.lds = c.use_lds ? need : 0;
   return c;
 }
 
@@ -82,7 +136,13 @@ struct EngineWs {
   uint32_t* bsum;       // [scan_blocks * 64] scan scratch
   uint64_t* fpart;      // [scan_blocks][6][64] final-fold partials
   uint32_t* totA;       // [64] included pairs per subset
+  uint32_t* c0rel;      // [EST_NC][64]     EST: that count relative to its segment
+  uint32_t* c0seg;      // [EST_NC]         EST: the segment holding each boundary
+  uint2* ftab;          // [EST_NC][64]     EST: {L_c, D_c} per interval (window low end, step)
+  uint32_t* viol;       // [EST_MAX_PASSES] EST: pass flagged for the exact re-run
 };
+
+constexpr int EST_MAX_PASSES = 512;  // passes between two checks of the EST flags
 
 static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t* bytes) {
   const int64_t M = pairs_of(n);
@@ -90,6 +150,10 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
   const size_t nsb = scan_blocks((uint32_t)nwaves);
   Carver c(base);
   EngineWs e;
+  e.c0rel = c.take<uint32_t>((size_t)EST_NC * LANES);
+  e.c0seg = c.take<uint32_t>((size_t)EST_NC);
+  e.ftab = c.take<uint2>((size_t)EST_NC * LANES);
+  e.viol = c.take<uint32_t>((size_t)EST_MAX_PASSES);
   e.masks = c.take<uint64_t>((size_t)n);
   e.posA_byB = c.take<uint32_t>((size_t)M);
   e.chunkA_byB = c.take<uint32_t>((size_t)M);
@@ -121,7 +185,7 @@ __global__ void k_join(const uint32_t* __restrict__ codesB, int64_t M, int64_t n
   const uint64_t t = tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n);
   const uint2 pc = pairMapA[t];
   posA_byB[i] = pc.x;
-  chunkA_byB[i] = pc.y;
+  if (chunkA_byB) chunkA_byB[i] = pc.y;  // only the exact (chunk-base) form reads it
 }
 
 // bit w of masks[x] <- x in subset (set0 + w); subset 0 is "all stimuli" when full_first.
@@ -212,35 +276,160 @@ int build_pass_masks(const int32_t* idx, int64_t k, int64_t set0, int nl, int fu
   return VR_OK;
 }
 
+// EST: the copy of the interval table in LDS (the rank walks read the masks from L2)
+__device__ inline const uint2* stage_table(const uint2* __restrict__ gtab, uint32_t rows, uint2* smem) {
+  for (uint32_t i = threadIdx.x; i < rows * LANES; i += blockDim.x) smem[i] = gtab[i];
+  __syncthreads();
+  return smem;
+}
+
+// EST: low end of the 2^16-wide window holding the doubled rank of A position pos for this
+// lane's subset: L_c + D_c * step, step = the position's 1/4096th of interval c. Monotone
+// non-decreasing in pos, over interval boundaries too (L_c + D_c 4095 <= L_{c+1}).
+__device__ inline uint32_t est_lo(const uint2* tab, uint32_t pos, int lane, int bits) {
+  const uint2 e = tab[(pos >> bits) * LANES + lane];
+  const uint32_t step = (pos & ((1u << bits) - 1u)) >> (bits - EST_STEP_BITS);
+  return e.x + __umul24(e.y, step);  // v_mad_u32_u24 (D_c <= 2^(b-11) < 2^24)
+}
+
+// EST: the doubled rank whose low 16 bits are v, in the window [lo, lo + 2^16)
+__device__ inline uint32_t est_recover(uint32_t v, uint32_t lo) { return lo + (uint32_t)(uint16_t)(v - lo); }
+
+// EST: true if y is outside the window [lo, lo + 2^16)
+__device__ inline bool est_bad(uint32_t y, uint32_t lo) { return y - lo > 65535u; }
+
+// ---------------------------------------------------------------------------------
+// EST pre-pass: included pairs per A segment (for the absolute ranks of k_rankA<EST>)
+// and the segment-relative count at every coarse boundary inside the segment
+// ---------------------------------------------------------------------------------
+template <bool LDS, bool FULL>
+__global__ __launch_bounds__(ENG_THREADS, 8) void k_countA(
+    const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
+    const uint32_t* __restrict__ chunk_g, uint32_t nchunks, const uint64_t* __restrict__ gmask,
+    int64_t n, int lw, int bits, uint32_t* __restrict__ c0rel, uint32_t* __restrict__ c0seg,
+    uint32_t* __restrict__ seg_tot, uint32_t nseg) {
+  extern __shared__ uint64_t smask[];
+  const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
+  const int lane = threadIdx.x & 63;
+  const bool active = FULL || lane < lw;
+  const uint32_t wave = wave_uniform(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
+  const Segment sg = my_segment(nchunks, nseg, wave);
+  uint32_t cw = 0;
+  if (sg.c0 < sg.c1) {
+    const uint32_t P0 = chunk_start(gstart, chunk_g, sg.c0);
+    const uint32_t P1 = chunk_start(gstart, chunk_g, sg.c1);
+    const uint32_t bmask = (1u << bits) - 1u;
+    uint32_t w0 = P0 & ~63u;
+    uint32_t cd = (w0 + lane >= P0 && w0 + lane < P1) ? codes[w0 + lane] : 0u;
+    for (; w0 < P1; w0 += 64) {
+      const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+      if (w0 + 64 < P1) {
+        const uint32_t q = w0 + 64 + lane;
+        cd = q < P1 ? codes[q] : 0u;
+      }
+      if ((w0 & bmask) == 0 && w0 >= P0) {  // boundary q = w0: count before it
+        c0rel[(size_t)(w0 >> bits) * LANES + lane] = cw;
+        if (lane == 0) c0seg[w0 >> bits] = wave;
+      }
+      cw += popc64(x);
+    }
+  }
+  seg_tot[(size_t)wave * LANES + lane] = cw;
+}
+
+// Interval c of the EST table from the included counts at its two boundaries: c0 = segment
+// base + relative count (k_countA); the end of the last, possibly partial, interval is
+// extrapolated to a full 2^b span so the step keeps its meaning. L_c is 2^15 below the
+// doubled rank 2 c0 + 1 at the boundary (modulo 2^32); D_c = floor(2 (c0' - c0) / 4096).
+__device__ inline uint32_t c0_at(uint32_t c, int lane, const uint32_t* c0rel, const uint32_t* c0seg,
+                                 const uint32_t* segpre) {
+  return segpre[(size_t)c0seg[c] * LANES + lane] + c0rel[(size_t)c * LANES + lane];
+}
+
+__global__ void k_c0(const uint32_t* __restrict__ c0rel, const uint32_t* __restrict__ c0seg,
+                     const uint32_t* __restrict__ segpre, const uint32_t* __restrict__ total,
+                     uint32_t nc, int bits, int64_t M, uint2* __restrict__ ftab) {
+  const uint32_t c = blockIdx.x;
+  const int lane = threadIdx.x;
+  const uint32_t a = c0_at(c, lane, c0rel, c0seg, segpre);
+  uint64_t d;  // included pairs over the (extrapolated) interval
+  if (c + 1 < nc) {
+    d = c0_at(c + 1, lane, c0rel, c0seg, segpre) - a;
+  } else {
+    const uint64_t span = (uint64_t)M - ((uint64_t)c << bits);
+    d = ((uint64_t)(total[lane] - a) << bits) / span;
+  }
+  ftab[(size_t)c * LANES + lane] = make_uint2(2u * a + 1u - 32768u, (uint32_t)((2 * d) >> EST_STEP_BITS));
+}
+
 // ---------------------------------------------------------------------------------
 // A pass
 // ---------------------------------------------------------------------------------
-template <bool LDS, bool FULL, typename TBT, bool BIGT>
+// EST: the k_rankA outputs besides TB
+struct EstA {
+  const uint32_t* segpre;  // [nseg][64] included pairs before each A segment (k_countA scan)
+  const uint2* ftab;       // interval table (k_c0), tabrows rows
+  uint32_t tabrows;
+  int bits;
+  uint32_t* viol;          // this pass's flag: some stored rank is not recoverable
+};
+
+// rows [r0, r0 + cnt) of TB get y mod 2^16 (EST); bad |= some row's y is not recoverable.
+// lo is monotone in the position, so the group's two end rows bound the rest.
+__device__ inline void store_rows_est(uint16_t* __restrict__ TB, uint32_t stride, uint32_t r0,
+                                      uint32_t cnt, int lane, uint32_t y, const uint2* tab,
+                                      int bits, bool& bad) {
+  if (cnt == 0) return;
+  // a group inside one 64-position window is covered by that window's check (k_rankA)
+  if (VR_EST_CHECK && (r0 >> 6) != ((r0 + cnt - 1u) >> 6))
+    bad |= est_bad(y, est_lo(tab, r0, lane, bits)) || est_bad(y, est_lo(tab, r0 + cnt - 1u, lane, bits));
+  uint16_t* row = TB + (size_t)r0 * stride + lane;
+  uint32_t i = 0;
+  for (; i + 4 <= cnt; i += 4, row += 4 * (size_t)stride) {
+    __builtin_nontemporal_store((uint16_t)y, row);
+    __builtin_nontemporal_store((uint16_t)y, row + stride);
+    __builtin_nontemporal_store((uint16_t)y, row + 2 * stride);
+    __builtin_nontemporal_store((uint16_t)y, row + 3 * stride);
+  }
+  for (; i < cnt; ++i, row += stride) __builtin_nontemporal_store((uint16_t)y, row);
+}
+
+// A side. Exact form (EST false): chunk-relative doubled ranks y - 2 lp (u16 or u32) and
+// the chunk-start counts lpA for baseA. EST form: absolute doubled ranks modulo 2^16,
+// each checked against the count estimate the B side will use.
+template <bool LDS, bool FULL, typename TBT, bool BIGT, bool EST>
 __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
     const uint64_t* __restrict__ gmask, int64_t n, TBT* __restrict__ TB, int lw,
     uint32_t* __restrict__ lpA, uint32_t* __restrict__ seg_tot, uint64_t* __restrict__ seg_part,
-    uint32_t nseg) {
+    uint32_t nseg, EstA est) {
+  static_assert(!EST || sizeof(TBT) == 2, "EST ranks are u16");
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
+  const uint2* tab = nullptr;
+  if constexpr (EST) tab = stage_table(est.ftab, est.tabrows, reinterpret_cast<uint2*>(smask + (LDS ? n : 0)));
   const int lane = threadIdx.x & 63;
   const bool active = FULL || lane < lw;
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
   const uint32_t wave = wave_uniform(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
   const Segment sg = my_segment(nchunks, nseg, wave);
+  const int bits = EST ? est.bits : 0;
 
   uint64_t tie = 0;  // sum over groups of k^3 - k (k < 2^16)
   u128 tie_big = 0;  //   (k >= 2^16)
   uint32_t cw = 0;   // included count before the window (segment-relative)
+  bool bad = false;  // EST: a stored rank is not recoverable from its 16 bits
   if (sg.c0 < sg.c1) {
+    // EST: 2 x (included pairs before this segment); exact form: 0
+    const uint32_t y0 = EST ? 2u * est.segpre[(size_t)wave * LANES + lane] : 0u;
     const uint32_t P0 = chunk_start(gstart, chunk_g, sg.c0);
     const uint32_t P1 = chunk_start(gstart, chunk_g, sg.c1);
     uint32_t cn = sg.c0;  // next chunk whose start is not yet recorded
     uint32_t pn = P0;
-    uint32_t lp = 0;      // count at the current chunk's start
+    uint32_t lp = 0;      // count at the current chunk's start (exact form)
     while (cn < sg.c1 && pn == P0) {
-      lpA[(size_t)cn * LANES + lane] = 0;
+      if (!EST) lpA[(size_t)cn * LANES + lane] = 0;
       ++cn;
       pn = cn < sg.c1 ? chunk_start(gstart, chunk_g, cn) : P1;
     }
@@ -248,11 +437,17 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
     // close the open group [gs, xe) given ce = included count before xe
     auto close = [&](uint32_t xe, uint32_t ce) {
       tie_add<BIGT>(tie, tie_big, ce - cgs);
-      if (active) store_rows<FULL, TBT>(TB, stride, gs, xe - gs, lane, (TBT)(cgs + ce + 1u - 2u * lp));
+      if (active) {
+        if constexpr (EST)
+          store_rows_est(reinterpret_cast<uint16_t*>(TB), stride, gs, xe - gs, lane, y0 + cgs + ce + 1u,
+                         tab, bits, bad);
+        else
+          store_rows<FULL, TBT>(TB, stride, gs, xe - gs, lane, (TBT)(cgs + ce + 1u - 2u * lp));
+      }
       gs = xe;
       cgs = ce;
       while (cn < sg.c1 && pn == xe) {  // chunk boundaries are group starts
-        lpA[(size_t)cn * LANES + lane] = ce;
+        if (!EST) lpA[(size_t)cn * LANES + lane] = ce;
         lp = ce;
         ++cn;
         pn = cn < sg.c1 ? chunk_start(gstart, chunk_g, cn) : P1;
@@ -266,6 +461,16 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
       const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
       uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
       asm volatile("" ::"v"(x) : "memory");
+      if constexpr (EST) {
+        // Every group that starts and ends in this window has y = y0 + cgs + ce + 1 in
+        // [Y0, Y0 + 128] (Y0 = y0 + 2 cw + 1: cw <= cgs <= ce <= cw + 64), and lo is monotone,
+        // in [lo(w0), lo(w0 + 63)]: these two checks make all of them recoverable. Longer
+        // groups are checked where they close.
+        if (VR_EST_CHECK) {
+          const uint32_t Y0 = y0 + 2u * cw + 1u;
+          bad |= est_bad(Y0, est_lo(tab, w0 + 63u, lane, bits)) || est_bad(Y0 + 128u, est_lo(tab, w0, lane, bits));
+        }
+      }
       if (w0 + 64 < P1) {
         const uint32_t q = w0 + 64 + lane;
         cd = q < P1 ? codes[q] : 0u;
@@ -275,7 +480,7 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
       if (F == ~0ull) {  // every position starts a group: close the carried one, then
         close(w0, cw);   // 63 singletons need only a running count
         if (cn >= sg.c1 || pn > w0 + 63u) {
-          uint32_t t = 2u * (cw - lp) + 1u;
+          uint32_t t = EST ? y0 + 2u * cw + 1u : 2u * (cw - lp) + 1u;
           TBT* row = TB + (size_t)w0 * stride + lane;
 #pragma unroll
           for (int j = 0; j < 63; ++j) {
@@ -305,6 +510,9 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
   seg_tot[o] = cw;
   seg_part[PA_TIEL * fs + o] = (uint64_t)t;
   seg_part[PA_TIEH * fs + o] = (uint64_t)(t >> 64);
+  if constexpr (EST) {
+    if (__ballot(bad) != 0 && lane == 0) *est.viol = 1u;  // benign race: every writer stores 1
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -393,6 +601,9 @@ __global__ void k_add_base(const uint32_t* __restrict__ lpA, const uint32_t* __r
 #ifndef VR_RANKB_MINW
 #define VR_RANKB_MINW 8  // waves per SIMD the B pass is compiled for (8: 64 VGPRs)
 #endif
+#ifndef VR_RANKB_EST_MINW
+#define VR_RANKB_EST_MINW 8  // EST B walk: 8 waves per SIMD (two 1024-thread workgroups per CU)
+#endif
 #ifndef VR_RANKB_PIPE
 #define VR_RANKB_PIPE 0  // 1: gather batch h+1 in flight while batch h is consumed
 #endif
@@ -451,6 +662,90 @@ __device__ inline void gather_wait(uint32_t t[BB], uint32_t b[BB]) {
                  : "memory");
 }
 
+#ifndef VR_EST_BB
+#define VR_EST_BB 8  // EST: pairs per gather batch (8, 16 or 32 loads in flight per wave)
+#endif
+#ifndef VR_EST_ASM
+#define VR_EST_ASM 1  // 0: plain loads (the compiler places the waits)
+#endif
+constexpr int EBB = VR_EST_BB;
+static_assert(EBB == 4 || EBB == 8 || EBB == 16 || EBB == 32, "EST batch");
+
+// EST: EBB pairs' TB entries only (absolute doubled ranks modulo 2^16), same load form
+__device__ inline void gather_issue_t(const uint16_t* __restrict__ TB, uint32_t stride, uint32_t pa,
+                                      uint32_t j0, uint32_t lane_bt, uint32_t t[EBB]) {
+#pragma unroll
+  for (int q = 0; q < EBB; ++q) {
+    const char* trow = reinterpret_cast<const char*>(TB) + (size_t)readlane_u32(pa, j0 + q) * (stride * 2);
+    asm volatile("global_load_ushort %0, %1, %2" VR_TB_CACHE : "=v"(t[q]) : "v"(lane_bt), "s"(trow) : "memory");
+  }
+}
+
+// wait for all of this wave's loads; ties the EBB results (16 per asm statement: the first
+// waits, the others only tell the compiler the registers are defined from here on)
+__device__ inline void wait_tie16(uint32_t* t, bool wait) {
+  if (wait)
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+                   "+v"(t[7]), "+v"(t[8]), "+v"(t[9]), "+v"(t[10]), "+v"(t[11]), "+v"(t[12]), "+v"(t[13]),
+                   "+v"(t[14]), "+v"(t[15])
+                 :
+                 : "memory");
+  else
+    asm volatile(""
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+                   "+v"(t[7]), "+v"(t[8]), "+v"(t[9]), "+v"(t[10]), "+v"(t[11]), "+v"(t[12]), "+v"(t[13]),
+                   "+v"(t[14]), "+v"(t[15])
+                 :
+                 : "memory");
+}
+
+__device__ inline void gather_wait_t(uint32_t t[EBB]) {
+  if constexpr (EBB == 4) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]) : : "memory");
+  } else if constexpr (EBB == 8) {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+                   "+v"(t[7])
+                 :
+                 : "memory");
+  } else {
+#pragma unroll
+    for (int g = 0; g < EBB / 16; ++g) wait_tie16(t + 16 * g, g == 0);
+  }
+}
+
+#ifndef VR_EST_ASM
+#define VR_EST_ASM 1  // 0: plain loads (the compiler places the waits)
+#endif
+
+// EST: yA of the window's 64 pairs (TB row entry + the window low end from the LDS table),
+// EBB pairs per batch, handed to fn(h, ya[EBB]). The batch's loads are waited for right
+// after they are issued (no compiler code between the asm issue and the asm wait, which
+// could otherwise read the destination registers before the data lands); the window
+// low ends are computed after the wait.
+template <typename Fn>
+__device__ inline void gather_window_est(const uint16_t* __restrict__ TB, uint32_t stride, const uint2* tab,
+                                         int bits, uint32_t pa, uint32_t lane_bt, int lane, Fn&& fn) {
+#pragma unroll
+  for (int h = 0; h < 64 / EBB; ++h) {
+    uint32_t t[EBB];
+    if constexpr (VR_EST_ASM) {
+      gather_issue_t(TB, stride, pa, h * EBB, lane_bt, t);
+      gather_wait_t(t);
+    } else {
+#pragma unroll
+      for (int q = 0; q < EBB; ++q) {
+        const char* row = reinterpret_cast<const char*>(TB) + (size_t)readlane_u32(pa, h * EBB + q) * (stride * 2u);
+        t[q] = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(row + lane_bt));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < EBB; ++q) t[q] = est_recover(t[q], est_lo(tab, readlane_u32(pa, h * EBB + q), lane, bits));
+    fn(h, t);
+  }
+}
+
 // yA of the window's 64 pairs, batch by batch, handed to fn(h, ya[BB])
 template <typename TBT, typename Fn>
 __device__ inline void gather_window(const TBT* __restrict__ TB, const uint32_t* __restrict__ baseA,
@@ -486,16 +781,23 @@ __device__ inline void gather_window(const TBT* __restrict__ TB, const uint32_t*
   }
 }
 
-template <bool LDS, bool FULL, typename TBT, bool BIGT>
-__global__ __launch_bounds__(ENG_THREADS, VR_RANKB_MINW) void k_rankB(
+// B side. Exact form: yA = 2 baseA[chunkA] + TB[posA] (two gathers per pair). EST form:
+// yA recovered from TB[posA] (absolute, modulo 2^16) and the LDS count table (one gather).
+template <bool LDS, bool FULL, typename TBT, bool BIGT, bool EST>
+__global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MINW) void k_rankB(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
     const uint64_t* __restrict__ gmask, int64_t n, const TBT* __restrict__ TB, int lw,
     const uint32_t* __restrict__ posA_byB, const uint32_t* __restrict__ chunkA_byB,
     const uint32_t* __restrict__ baseA, uint32_t* __restrict__ seg_tot,
-    uint64_t* __restrict__ seg_part, uint32_t nseg) {
+    uint64_t* __restrict__ seg_part, uint32_t nseg, const uint2* __restrict__ ftab,
+    uint32_t tabrows, int bits) {
+  static_assert(!EST || sizeof(TBT) == 2, "EST ranks are u16");
+  constexpr int NB = EST ? EBB : BB;  // pairs per gather batch
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
+  const uint2* tab = nullptr;
+  if constexpr (EST) tab = stage_table(ftab, tabrows, reinterpret_cast<uint2*>(smask + (LDS ? n : 0)));
   const int lane = threadIdx.x & 63;
   const bool active = FULL || lane < lw;
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
@@ -525,7 +827,7 @@ __global__ __launch_bounds__(ENG_THREADS, VR_RANKB_MINW) void k_rankB(
       const uint32_t pos = w + (uint32_t)lane;
       const bool valid = pos >= P0 && pos < P1;
       pa = valid ? posA_byB[pos] : 0u;
-      ca = valid ? chunkA_byB[pos] : 0u;
+      ca = (!EST && valid) ? chunkA_byB[pos] : 0u;
       cd = valid ? codes[pos] : 0u;
       f0 = sload(gflag + (w >> 5));
       f1 = sload(gflag + (w >> 5) + 1);
@@ -540,6 +842,12 @@ __global__ __launch_bounds__(ENG_THREADS, VR_RANKB_MINW) void k_rankB(
       const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
       const uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
       if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
+      auto gather = [&](auto&& fn) {
+        if constexpr (EST)
+          gather_window_est(reinterpret_cast<const uint16_t*>(TB), stride, tab, bits, pa_c, lane_bt, lane, fn);
+        else
+          gather_window<TBT>(TB, baseA, stride, pa_c, ca_c, lane_bt, lane_b4, fn);
+      };
       if (F == ~0ull) {
         // Every position starts a group (the normal case for continuous RDMs): after
         // closing the carried group, positions 0..62 are singletons, whose tie term is 0
@@ -549,10 +857,10 @@ __global__ __launch_bounds__(ENG_THREADS, VR_RANKB_MINW) void k_rankB(
         close(cw);
         uint64_t a64 = 0;
         uint32_t c = cw;
-        gather_window<TBT>(TB, baseA, stride, pa_c, ca_c, lane_bt, lane_b4, [&](int h, uint32_t* ya) {
+        gather([&](int h, uint32_t* ya) {
 #pragma unroll
-          for (int q = 0; q < BB; ++q) {
-            const uint32_t j = h * BB + q;
+          for (int q = 0; q < NB; ++q) {
+            const uint32_t j = h * NB + q;
             const uint32_t b = (uint32_t)(x >> j) & 1u;
             const uint32_t yb = b ? ya[q] : 0u;  // x is 0 on inactive lanes
             if (j < 63) {
@@ -567,10 +875,10 @@ __global__ __launch_bounds__(ENG_THREADS, VR_RANKB_MINW) void k_rankB(
         });
         acc += (u128)a64 * 2u;
       } else {
-        gather_window<TBT>(TB, baseA, stride, pa_c, ca_c, lane_bt, lane_b4, [&](int h, uint32_t* ya) {
+        gather([&](int h, uint32_t* ya) {
 #pragma unroll
-          for (int q = 0; q < BB; ++q) {
-            const uint32_t j = h * BB + q;
+          for (int q = 0; q < NB; ++q) {
+            const uint32_t j = h * NB + q;
             if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
             S += ((x >> j) & 1ull) ? (uint64_t)ya[q] : 0ull;  // x is 0 on inactive lanes
           }
@@ -692,22 +1000,22 @@ static int allow_big_lds(K kernel) {
   return VR_OK;
 }
 
-// A side of a pass (shared by every B plan of the call): TB rows in A order, chunk bases
-// baseA, A segment tie sums and the included-pair totals totA.
+// A side of a pass (shared by every B plan of the call), exact form: TB rows in A order,
+// chunk bases baseA, A segment tie sums and the included-pair totals totA.
 template <bool LDS, bool FULL, typename TBT, bool BTA>
 static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const EngineCfg& cfg,
                   hipStream_t st) {
   static bool attr = false;
-  if (LDS && !attr) {
-    VR_TRY(allow_big_lds(k_rankA<LDS, FULL, TBT, BTA>));
+  if (!attr) {
+    VR_TRY(allow_big_lds(k_rankA<LDS, FULL, TBT, BTA, false>));
     attr = true;
   }
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = (uint32_t)cfg.nwaves;
-  k_rankA<LDS, FULL, TBT, BTA><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
+  k_rankA<LDS, FULL, TBT, BTA, false><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
       A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<TBT*>(E.TB), lw, E.lpA,
-      E.segA_tot, E.segA_part, nseg);
+      E.segA_tot, E.segA_part, nseg, EstA{});
   VR_CHECK_LAUNCH();
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
   const size_t nb = ((size_t)nch * LANES + 255) / 256;
@@ -716,23 +1024,56 @@ static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const
   return VR_OK;
 }
 
-// B side of a pass for one B plan, joined to A by (posA_byB, chunkA_byB): the nl scores
-// of the pass.
-template <bool LDS, bool FULL, typename TBT, bool BTB>
-static int pass_b(const PlanView& A, const PlanView& B, const uint32_t* posA_byB,
-                  const uint32_t* chunkA_byB, int64_t n, const EngineWs& E, int lw, int nl,
-                  double* scores_out, const EngineCfg& cfg, hipStream_t st) {
+// A side of a pass, EST form: count pre-pass -> segment bases and the interval table ->
+// absolute u16 ranks in A order (flagging *viol when one is not recoverable). The count
+// pre-pass reads the masks from LDS when they fit (CL), the rank walk from L2.
+template <bool CL, bool FULL, bool BTA>
+static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, const EngineCfg& cfg,
+                      uint32_t* viol, hipStream_t st) {
   static bool attr = false;
-  if (LDS && !attr) {
-    VR_TRY(allow_big_lds(k_rankB<LDS, FULL, TBT, BTB>));
+  if (!attr) {
+    VR_TRY(allow_big_lds(k_countA<CL, FULL>));
+    VR_TRY(allow_big_lds(k_rankA<false, FULL, uint16_t, BTA, true>));
     attr = true;
   }
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = (uint32_t)cfg.nwaves;
-  k_rankB<LDS, FULL, TBT, BTB><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
+  const int bits = est_bits(M);
+  const uint32_t nc = est_intervals(M, bits);
+  k_countA<CL, FULL><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(A.codes, A.gstart, A.chunk_g, nch, E.masks,
+                                                              n, lw, bits, E.c0rel, E.c0seg, E.segA_tot, nseg);
+  VR_CHECK_LAUNCH();
+  VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
+  k_c0<<<nc, LANES, 0, st>>>(E.c0rel, E.c0seg, E.segA_pre, E.totA, nc, bits, M, E.ftab);
+  VR_CHECK_LAUNCH();
+  const EstA est{E.segA_pre, E.ftab, nc, bits, viol};
+  k_rankA<false, FULL, uint16_t, BTA, true><<<cfg.grid, ENG_THREADS, cfg.tab, st>>>(
+      A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<uint16_t*>(E.TB), lw, E.lpA,
+      E.segA_tot, E.segA_part, nseg, est);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+// B side of a pass for one B plan, joined to A by posA_byB (and chunkA_byB in the exact
+// form): the nl scores of the pass.
+template <bool LDS, bool FULL, typename TBT, bool BTB, bool EST>
+static int pass_b(const PlanView& A, const PlanView& B, const uint32_t* posA_byB,
+                  const uint32_t* chunkA_byB, int64_t n, const EngineWs& E, int lw, int nl,
+                  double* scores_out, const EngineCfg& cfg, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    VR_TRY(allow_big_lds(k_rankB<LDS, FULL, TBT, BTB, EST>));
+    attr = true;
+  }
+  const int64_t M = pairs_of(n);
+  const uint32_t nch = plan_nchunks(M);
+  const uint32_t nseg = (uint32_t)cfg.nwaves;
+  const int bits = EST ? est_bits(M) : 0;
+  const uint32_t rows = EST ? est_intervals(M, bits) : 0;
+  k_rankB<LDS, FULL, TBT, BTB, EST><<<cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
       B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
-      posA_byB, chunkA_byB, E.baseA, E.segB_tot, E.segB_part, nseg);
+      posA_byB, chunkA_byB, E.baseA, E.segB_tot, E.segB_part, nseg, E.ftab, rows, bits);
   VR_CHECK_LAUNCH();
   VR_TRY(lane_scan(E.segB_tot, nseg, E.bsum, E.segB_pre, nullptr, st));
   const uint32_t nsb = scan_blocks(nseg);
@@ -766,6 +1107,8 @@ static int with_pass_tag(bool lds, bool full, bool narrow, Fn&& fn) {
 // so scores equal the per-unit calls bit for bit.
 // Scores of B j: scores[j * score_ld + s] for the `total` subsets (full set first if
 // full_first), 64 per pass. joins: nb pairs of M-element (posA_byB, chunkA_byB) arrays.
+// Passes run in the EST form; the few it flags (and every pass, with VISREPS_ENGINE_EST=0)
+// run in the exact chunk-base form, which needs the chunkA joins too.
 static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, int64_t n,
                             const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
                             double* scores, int64_t score_ld, uint32_t* const* joins,
@@ -790,30 +1133,80 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
   VR_CHECK_HIP(hipStreamSynchronize(st));
   const bool narrow = (uint64_t)PLAN_L + h[0].max_group <= 32767u;
   const bool bigA = h[0].max_group >= 65536u;
-  for (int64_t j = 0; j < nb; ++j) {
-    k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(Bs[j].codes, M, n, A.pair_map,
-                                                       joins[2 * j], joins[2 * j + 1]);
-    VR_CHECK_LAUNCH();
-  }
-  return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
-    using Tg = decltype(tag);
-    using TBT = typename Tg::tbt;
-    for (int64_t set0 = 0; set0 < total; set0 += lw) {
-      const int nl = (int)std::min<int64_t>(lw, total - set0);
-      VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
-      VR_TRY((bigA ? pass_a<Tg::lds, Tg::full, TBT, true>(A, n, E, lw, cfg, st)
-                   : pass_a<Tg::lds, Tg::full, TBT, false>(A, n, E, lw, cfg, st)));
-      for (int64_t j = 0; j < nb; ++j) {
-        double* out = scores + j * score_ld + set0;
-        const uint32_t* pj = joins[2 * j];
-        const uint32_t* cj = joins[2 * j + 1];
-        VR_TRY((h[(size_t)j + 1].max_group >= 65536u
-                    ? pass_b<Tg::lds, Tg::full, TBT, true>(A, Bs[j], pj, cj, n, E, lw, nl, out, cfg, st)
-                    : pass_b<Tg::lds, Tg::full, TBT, false>(A, Bs[j], pj, cj, n, E, lw, nl, out, cfg, st)));
-      }
+  const bool est = engine_est();
+  auto join = [&](bool chunks) -> int {
+    for (int64_t j = 0; j < nb; ++j) {
+      k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(Bs[j].codes, M, n, A.pair_map, joins[2 * j],
+                                                         chunks ? joins[2 * j + 1] : nullptr);
+      VR_CHECK_LAUNCH();
     }
     return VR_OK;
-  });
+  };
+  VR_TRY(join(!est));
+  // the exact chunk-base form of the pass starting at subset set0
+  auto exact_pass = [&](auto tag, int64_t set0) -> int {
+    using Tg = decltype(tag);
+    using TBT = typename Tg::tbt;
+    const int nl = (int)std::min<int64_t>(lw, total - set0);
+    VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
+    VR_TRY((bigA ? pass_a<Tg::lds, Tg::full, TBT, true>(A, n, E, lw, cfg, st)
+                 : pass_a<Tg::lds, Tg::full, TBT, false>(A, n, E, lw, cfg, st)));
+    for (int64_t j = 0; j < nb; ++j) {
+      double* out = scores + j * score_ld + set0;
+      const uint32_t* pj = joins[2 * j];
+      const uint32_t* cj = joins[2 * j + 1];
+      VR_TRY((h[(size_t)j + 1].max_group >= 65536u
+                  ? pass_b<Tg::lds, Tg::full, TBT, true, false>(A, Bs[j], pj, cj, n, E, lw, nl, out, cfg, st)
+                  : pass_b<Tg::lds, Tg::full, TBT, false, false>(A, Bs[j], pj, cj, n, E, lw, nl, out, cfg, st)));
+    }
+    return VR_OK;
+  };
+  if (!est) {
+    return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
+      for (int64_t set0 = 0; set0 < total; set0 += lw) VR_TRY(exact_pass(tag, set0));
+      return VR_OK;
+    });
+  }
+  const int64_t npass = (total + lw - 1) / lw;
+  bool chunk_joins = false;
+  for (int64_t p0 = 0; p0 < npass; p0 += EST_MAX_PASSES) {
+    const int64_t p1 = std::min<int64_t>(npass, p0 + EST_MAX_PASSES);
+    VR_CHECK_HIP(hipMemsetAsync(E.viol, 0, (size_t)(p1 - p0) * sizeof(uint32_t), st));
+    VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, true, [&](auto tag) -> int {
+      using Tg = decltype(tag);
+      if constexpr (sizeof(typename Tg::tbt) == 2) {
+        for (int64_t p = p0; p < p1; ++p) {
+          const int64_t set0 = p * lw;
+          const int nl = (int)std::min<int64_t>(lw, total - set0);
+          VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
+          uint32_t* viol = E.viol + (p - p0);
+          VR_TRY((bigA ? pass_a_est<Tg::lds, Tg::full, true>(A, n, E, lw, cfg, viol, st)
+                       : pass_a_est<Tg::lds, Tg::full, false>(A, n, E, lw, cfg, viol, st)));
+          for (int64_t j = 0; j < nb; ++j) {
+            double* out = scores + j * score_ld + set0;
+            const uint32_t* pj = joins[2 * j];
+            VR_TRY((h[(size_t)j + 1].max_group >= 65536u
+                        ? pass_b<false, Tg::full, uint16_t, true, true>(A, Bs[j], pj, nullptr, n, E, lw, nl, out, cfg, st)
+                        : pass_b<false, Tg::full, uint16_t, false, true>(A, Bs[j], pj, nullptr, n, E, lw, nl, out, cfg, st)));
+          }
+        }
+      }
+      return VR_OK;
+    }));
+    std::vector<uint32_t> flags((size_t)(p1 - p0));
+    VR_CHECK_HIP(hipMemcpyAsync(flags.data(), E.viol, flags.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    VR_CHECK_HIP(hipStreamSynchronize(st));
+    for (int64_t p = p0; p < p1; ++p) {
+      if (!flags[(size_t)(p - p0)]) continue;
+      if (!chunk_joins) {
+        VR_TRY(join(true));
+        chunk_joins = true;
+      }
+      g_est_reruns.fetch_add(1);
+      VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) { return exact_pass(tag, p * lw); }));
+    }
+  }
+  return VR_OK;
 }
 
 // Scores for `total` subsets (full set first if full_first), 64 per pass.
@@ -873,6 +1266,8 @@ static size_t oneshot_bytes(int64_t n, int lw, int nwaves, void* base, PlanView*
 using namespace vr;
 
 extern "C" {
+
+int64_t vr_engine_est_reruns(void) { return g_est_reruns.load(); }
 
 size_t vr_bootstrap_workspace(int64_t n) {
   size_t b = 0;

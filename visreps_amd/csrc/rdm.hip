@@ -43,42 +43,52 @@ __device__ inline double block_sum_f64(double v, double* lds) {
   return s;
 }
 
-__global__ __launch_bounds__(RSTAT_BS) void k_row_stats(const float* __restrict__ X, int64_t d,
+// Input elements as fp32: float as is, bf16 (stored as its 16-bit pattern) exactly widened,
+// which is the reference's X.float() (rsa.py:76) without materialising an fp32 copy.
+__device__ inline float in_f32(float v) { return v; }
+__device__ inline float in_f32(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ inline f32x4 in_f32x4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ inline f32x4 in_f32x4(const uint16_t* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+}
+
+template <typename T>
+__global__ __launch_bounds__(RSTAT_BS) void k_row_stats(const T* __restrict__ X, int64_t d,
                                                         int64_t ldx, float* __restrict__ mean,
                                                         float* __restrict__ stdv,
                                                         float correction, int vec) {
   __shared__ double lds[RSTAT_BS / 64 + 1];
-  const float* row = X + (int64_t)blockIdx.x * ldx;
+  const T* row = X + (int64_t)blockIdx.x * ldx;
   double s = 0;
   if (vec) {
-    const f32x4* r4 = reinterpret_cast<const f32x4*>(row);
     const int64_t d4 = d / 4;
     for (int64_t i = threadIdx.x; i < d4; i += RSTAT_BS) {
-      f32x4 v = r4[i];
+      f32x4 v = in_f32x4(row + 4 * i);
       s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
     }
-    for (int64_t i = d4 * 4 + threadIdx.x; i < d; i += RSTAT_BS) s += (double)row[i];
+    for (int64_t i = d4 * 4 + threadIdx.x; i < d; i += RSTAT_BS) s += (double)in_f32(row[i]);
   } else {
-    for (int64_t i = threadIdx.x; i < d; i += RSTAT_BS) s += (double)row[i];
+    for (int64_t i = threadIdx.x; i < d; i += RSTAT_BS) s += (double)in_f32(row[i]);
   }
   s = block_sum_f64(s, lds);
   const float m = (float)(s / (double)d);
   double q = 0;
   if (vec) {
-    const f32x4* r4 = reinterpret_cast<const f32x4*>(row);
     const int64_t d4 = d / 4;
     for (int64_t i = threadIdx.x; i < d4; i += RSTAT_BS) {
-      f32x4 v = r4[i];
+      f32x4 v = in_f32x4(row + 4 * i);
       float a = v.x - m, b = v.y - m, c = v.z - m, e = v.w - m;
       q += (double)(a * a) + (double)(b * b) + (double)(c * c) + (double)(e * e);
     }
     for (int64_t i = d4 * 4 + threadIdx.x; i < d; i += RSTAT_BS) {
-      float a = row[i] - m;
+      float a = in_f32(row[i]) - m;
       q += (double)(a * a);
     }
   } else {
     for (int64_t i = threadIdx.x; i < d; i += RSTAT_BS) {
-      float a = row[i] - m;
+      float a = in_f32(row[i]) - m;
       q += (double)(a * a);
     }
   }
@@ -427,7 +437,8 @@ constexpr int S_STAGE = GT * SROW;    // bf16 per panel per stage
 
 // Planes: per row and 32-k stage one 128-byte record [hi k0..31 | lo k0..31]; rows padded
 // to the tile edge and k to the stage with exact zeros (so the Gram kernel has no edges).
-__global__ void k_split3(const float* __restrict__ X, int64_t n, int64_t d, int64_t ldx,
+template <typename T>
+__global__ void k_split3(const T* __restrict__ X, int64_t n, int64_t d, int64_t ldx,
                          const float* __restrict__ mean, int64_t rows, int64_t nstage,
                          uint16_t* __restrict__ planes) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (row, stage, 4-k group)
@@ -440,10 +451,10 @@ __global__ void k_split3(const float* __restrict__ X, int64_t n, int64_t d, int6
   float v[4] = {0.f, 0.f, 0.f, 0.f};
   if (r < n) {
     const float m = mean[r];
-    const float* src = X + r * ldx + k;
+    const T* src = X + r * ldx + k;
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      if (k + e < d) v[e] = src[e] - m;
+      if (k + e < d) v[e] = in_f32(src[e]) - m;
   }
   uint32_t hw[2], lw[2];
 #pragma unroll
@@ -935,15 +946,27 @@ int vr_row_stats_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* m
   VR_REQUIRE(X && mean && stdv, "vr_row_stats_f32: null pointer");
   VR_REQUIRE(n <= INT32_MAX, "vr_row_stats_f32: n too large");
   const int vec = ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && ((ldx & 3) == 0);
-  k_row_stats<<<(unsigned)n, RSTAT_BS, 0, as_stream(stream)>>>(X, d, ldx, mean, stdv,
-                                                                correction, vec);
+  k_row_stats<float><<<(unsigned)n, RSTAT_BS, 0, as_stream(stream)>>>(X, d, ldx, mean, stdv,
+                                                                       correction, vec);
   VR_CHECK_LAUNCH();
   return VR_OK;
 }
 
-static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm, int64_t ldr,
+// bf16 rows (16-bit patterns): the same statistics of the exactly widened values
+static int row_stats_bf16(const uint16_t* X, int64_t n, int64_t d, int64_t ldx, float* mean,
+                          float* stdv, float correction, hipStream_t st) {
+  const int vec = ((reinterpret_cast<uintptr_t>(X) & 7) == 0) && ((ldx & 3) == 0);
+  k_row_stats<uint16_t><<<(unsigned)n, RSTAT_BS, 0, st>>>(X, d, ldx, mean, stdv, correction, vec);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+// bf16 input always takes the split kernel: only the row statistics and the split prepass
+// read X, so no fp32 copy of the features is ever made (the exact-fp32 kernel stages X).
+static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* rdm, int64_t ldr,
                       float correction, int64_t tile_begin, int64_t tile_end, void* ws,
-                      size_t ws_bytes, void* stream, size_t need, bool raw = false) {
+                      size_t ws_bytes, void* stream, size_t need, bool raw = false, bool bf16 = false) {
+  const float* X = static_cast<const float*>(Xv);
   if (ws_bytes < need || ws == nullptr) {
     set_error("vr_rdm_pearson: workspace %zu < %zu", ws_bytes, need);
     return VR_EWORKSPACE;
@@ -951,7 +974,7 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
   hipStream_t st = as_stream(stream);
   GramParams P{};
   gram_geometry(n, d, tile_end - tile_begin, P.T, P.ntiles, P.splits, P.kslice);
-  const bool split3 = gram_split(n, d);
+  const bool split3 = bf16 || gram_split(n, d);
   float *mean, *stdv;
   uint16_t* planes;
   gram_ws(n, d, tile_end - tile_begin, split3, ws, &mean, &stdv, &P.partial, &planes);
@@ -959,14 +982,20 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
   if (raw) {  // zero means: the panels stage X itself
     VR_CHECK_HIP(hipMemsetAsync(mean, 0, (size_t)n * sizeof(float), st));
     VR_CHECK_HIP(hipMemsetAsync(stdv, 0, (size_t)n * sizeof(float), st));
+  } else if (bf16) {
+    VR_TRY(row_stats_bf16(static_cast<const uint16_t*>(Xv), n, d, ldx, mean, stdv, correction, st));
   } else {
     VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
   }
   if (split3) {
     const int64_t rows = (n + WT - 1) / WT * WT, nstage = (d + GK - 1) / GK;
     const int64_t threads = rows * nstage * 8;
-    k_split3<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(X, n, d, ldx, mean, rows, nstage,
-                                                                planes);
+    if (bf16)
+      k_split3<uint16_t><<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(
+          static_cast<const uint16_t*>(Xv), n, d, ldx, mean, rows, nstage, planes);
+    else
+      k_split3<float><<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(X, n, d, ldx, mean, rows, nstage,
+                                                                         planes);
     VR_CHECK_LAUNCH();
     P.planes = planes;
     P.nstage = nstage;
@@ -980,7 +1009,7 @@ static int rdm_launch(const float* X, int64_t n, int64_t d, int64_t ldx, float* 
   P.ldx = ldx;
   P.ldr = ldr;
   P.correction = correction;
-  P.vec = ((reinterpret_cast<uintptr_t>(X) & 15) == 0) && ((ldx & 3) == 0) &&
+  P.vec = ((reinterpret_cast<uintptr_t>(Xv) & 15) == 0) && ((ldx & 3) == 0) &&
           ((reinterpret_cast<uintptr_t>(rdm) & 15) == 0);
   // tile range [t0, t0 + count): its own split-K geometry, generations, reduction
   auto run_range = [&](int64_t t0, int64_t count, bool fit) -> int {
@@ -1058,6 +1087,32 @@ int vr_rdm_pearson_tiles_f32(const float* X, int64_t n, int64_t d, int64_t ldx, 
   VR_REQUIRE(X && rdm, "vr_rdm_pearson_tiles_f32: null pointer");
   return rdm_launch(X, n, d, ldx, rdm, ldr, correction, tile_begin, tile_end, ws, ws_bytes,
                     stream, vr_rdm_tiles_workspace(n, d, tile_begin, tile_end));
+}
+
+size_t vr_rdm_bf16_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
+  if (n <= 0 || d <= 0 || tile_end <= tile_begin) return 256;
+  return gram_ws(n, d, tile_end - tile_begin, true, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+
+int vr_rdm_pearson_tiles_bf16(const uint16_t* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
+                              int64_t ldr, float correction, int64_t tile_begin, int64_t tile_end,
+                              void* ws, size_t ws_bytes, void* stream) {
+  VR_REQUIRE(n >= 0 && d > 0 && ldx >= d && ldr >= n,
+             "vr_rdm_pearson_tiles_bf16: bad shape n=%lld d=%lld", (long long)n, (long long)d);
+  VR_REQUIRE(n <= (1 << 20), "vr_rdm_pearson_tiles_bf16: n too large");
+  VR_REQUIRE(tile_begin >= 0 && tile_end >= tile_begin && tile_end <= gram_tiles(n),
+             "vr_rdm_pearson_tiles_bf16: tile range [%lld, %lld) outside [0, %lld)",
+             (long long)tile_begin, (long long)tile_end, (long long)gram_tiles(n));
+  if (n == 0 || tile_end == tile_begin) return VR_OK;
+  VR_REQUIRE(X && rdm, "vr_rdm_pearson_tiles_bf16: null pointer");
+  return rdm_launch(X, n, d, ldx, rdm, ldr, correction, tile_begin, tile_end, ws, ws_bytes, stream,
+                    vr_rdm_bf16_workspace(n, d, tile_begin, tile_end), false, true);
+}
+
+int vr_rdm_pearson_bf16(const uint16_t* X, int64_t n, int64_t d, int64_t ldx, float* rdm, int64_t ldr,
+                        float correction, void* ws, size_t ws_bytes, void* stream) {
+  return vr_rdm_pearson_tiles_bf16(X, n, d, ldx, rdm, ldr, correction, 0, n > 0 ? gram_tiles(n) : 0, ws,
+                                   ws_bytes, stream);
 }
 
 int vr_gram_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* G, int64_t ldg,

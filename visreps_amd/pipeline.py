@@ -31,7 +31,7 @@ import torch.distributed as dist
 
 from ._lib import check, lib, stream_of, workspace
 from .analysis import rsa as R
-from .analysis._random import bootstrap_indices
+from .analysis._random import LegacyRandomState, bootstrap_indices, draw_bootstrap_indices
 from .dataloaders.synthetic import shard_rows
 
 
@@ -42,15 +42,16 @@ class StepTimes:
     gram_ms: float = 0.0
     gram_flops: float = 0.0
     engine_ms: float = 0.0
-    engine_bytes: float = 0.0
-    engine_calls: int = 0
+    engine_bytes: float = 0.0      # the engine's own algorithmic bytes (engine_call_bytes)
+    engine_ref_bytes: float = 0.0  # reference-equivalent bytes (engine_bytes(), §8(d))
+    engine_calls: int = 0          # units
     _pending: list = field(default_factory=list)
 
-    def record(self, kind: str, start, end, work: float, calls: int = 1):
-        self._pending.append((kind, start, end, work, calls))
+    def record(self, kind: str, start, end, work: float, calls: int = 1, ref: float = 0.0):
+        self._pending.append((kind, start, end, work, calls, ref))
 
     def resolve(self):
-        for kind, s, e, w, c in self._pending:
+        for kind, s, e, w, c, ref in self._pending:
             ms = s.elapsed_time(e)
             if kind == "gram":
                 self.gram_ms += ms
@@ -58,6 +59,7 @@ class StepTimes:
             else:
                 self.engine_ms += ms
                 self.engine_bytes += w
+                self.engine_ref_bytes += ref
                 self.engine_calls += c
         self._pending.clear()
 
@@ -230,9 +232,29 @@ def distributed_rdm(x_local: torch.Tensor, n: int, pg=None,
 # units
 # ---------------------------------------------------------------------------------------
 def engine_bytes(n: int, n_boot: int) -> float:
-    """Algorithmic bytes of one unit: 8 * [M(N) + n_boot * M(int(0.9 N))]."""
+    """Reference-equivalent bytes of one unit: 8 * [M(N) + n_boot * M(int(0.9 N))]
+    (both fp32 triangles read once per Spearman evaluation). The engine
+    never streams these; it is the yardstick of the reference's algorithm."""
     k = int(0.9 * n)
     return 8.0 * (n * (n - 1) // 2 + n_boot * (k * (k - 1) // 2))
+
+
+# Bytes per pair of the engine's own passes (engine.hip, EST form): the A side streams its
+# codes twice (count pre-pass, rank walk) and writes one 128-byte TB row per pair; each B
+# side streams its codes and the join (4 + 4 B) and gathers one TB row per pair. k_join
+# reads B codes and one 8-B pair-map record and writes posA, once per unit.
+ENGINE_A_BYTES_PER_PAIR = 4 + 4 + 128
+ENGINE_B_BYTES_PER_PAIR = 4 + 4 + 128
+ENGINE_JOIN_BYTES_PER_PAIR = 4 + 8 + 4
+
+
+def engine_call_bytes(n: int, subsets: int, units: int) -> float:
+    """Algorithmic HBM bytes of one engine call: `units` B plans against one A plan over
+    `subsets` subsets (64 per pass)."""
+    M = n * (n - 1) // 2
+    passes = -(-subsets // 64)
+    return float(M) * (passes * (ENGINE_A_BYTES_PER_PAIR + units * ENGINE_B_BYTES_PER_PAIR)
+                       + units * ENGINE_JOIN_BYTES_PER_PAIR)
 
 
 def run_unit(plan_m: R.RankPlan, plan_n: R.RankPlan, idx: Optional[np.ndarray],
@@ -244,7 +266,9 @@ def run_unit(plan_m: R.RankPlan, plan_n: R.RankPlan, idx: Optional[np.ndarray],
     scores = R.bootstrap_spearman(plan_m, plan_n, idx, full_first=True)
     if times is not None:
         ev[1].record()
-        times.record("engine", ev[0], ev[1], engine_bytes(plan_m.n, 0 if idx is None else len(idx)))
+        nb = 0 if idx is None else len(idx)
+        times.record("engine", ev[0], ev[1], engine_call_bytes(plan_m.n, nb + 1, 1),
+                     ref=engine_bytes(plan_m.n, nb))
     return scores
 
 
@@ -260,8 +284,8 @@ def run_group(plan_n: R.RankPlan, plans_m: Sequence[R.RankPlan], idx: Optional[n
     if times is not None:
         ev[1].record()
         nb = 0 if idx is None else len(idx)
-        times.record("engine", ev[0], ev[1], engine_bytes(plan_n.n, nb) * len(plans_m),
-                     calls=len(plans_m))
+        times.record("engine", ev[0], ev[1], engine_call_bytes(plan_n.n, nb + 1, len(plans_m)),
+                     calls=len(plans_m), ref=engine_bytes(plan_n.n, nb) * len(plans_m))
     return scores
 
 
@@ -270,6 +294,56 @@ def unit_split(units: Sequence, world: int) -> List[Tuple[int, int]]:
     u = len(units)
     b = [round(r * u / world) for r in range(world + 1)]
     return [(b[r], b[r + 1]) for r in range(world)]
+
+
+def phase1_select(feats: Dict[str, torch.Tensor], projectors: Dict, responses: Dict[str, torch.Tensor],
+                  points: Sequence[str], n: int, *, n_select: int = 1000, seed: int = 42,
+                  pg=None, times: Optional[StepTimes] = None) -> Dict[str, Tuple[str, List[Dict]]]:
+    """Phase-1 layer selection of the reference eval (evals.py:249-287) on stimulus-sharded
+    features: every local row of every point is projected by its SRP matrix (the bulk
+    extraction's torch.sparse.mm, models/utils.py:297-344, here vr_srp_csr_f32);
+    RandomState(seed).choice(n, n_select) picks the selection stimuli (re-created per
+    (region, subject); the regions share one subject's stimuli, so one draw serves them
+    all); selection RDMs of the projected points and of each region's responses; Spearman
+    of every point against every region; best = first strict maximum.
+    Returns {region: (best point, [{"layer", "score"} per point])} on every rank."""
+    rank, world = _world(pg)
+    rows = shard_rows(n, rank, world)
+    k = min(int(n_select), n) if n_select is not None else n
+    sel = (LegacyRandomState(seed).choice(n, k, replace=False) if k < n else np.arange(n))
+    mine = np.flatnonzero((sel >= rows.start) & (sel < rows.stop))
+    dev = next(iter(responses.values())).device
+    pos_t = torch.as_tensor(mine, dtype=torch.long, device=dev)
+    src_t = torch.as_tensor(sel[mine] - rows.start, dtype=torch.long, device=dev)
+
+    def selected(x_local: torch.Tensor) -> torch.Tensor:  # (n_local, d) -> (k, d), every rank
+        out = torch.zeros((k, x_local.size(1)), dtype=torch.float32, device=dev)
+        out[pos_t] = x_local[src_t].float()
+        if world > 1:  # disjoint rows: the sum is exact
+            dist.all_reduce(out, op=dist.ReduceOp.SUM, group=pg)
+        return out
+
+    def timed_rdm(x: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((x.size(0), x.size(0)), dtype=torch.float32, device=dev)
+        rdm_tiles_into(x, out, 0, int(lib().vr_rdm_tile_count(x.size(0))), times=times)
+        return out
+
+    mplans = []
+    for p in points:
+        proj = projectors[p](feats[p])  # SRP of every local stimulus, as get_activations
+        mplans.append(R.RankPlan(timed_rdm(selected(proj))))
+        del proj
+    out = {}
+    for r, y in responses.items():
+        pn = R.RankPlan(timed_rdm(selected(y)))
+        sc = R.bootstrap_spearman_multi(pn, mplans, None, full_first=True)[:, 0].cpu().numpy()
+        best, best_score, scores = None, -float("inf"), []
+        for p, v in zip(points, sc):
+            scores.append({"layer": p, "score": float(v)})
+            if v > best_score:  # strict: the first maximal point wins (evals.py:273-275)
+                best, best_score = p, float(v)
+        out[r] = (best, scores)
+    return out
 
 
 def summarize(scores: np.ndarray, bootstrap: bool) -> Dict:
@@ -310,9 +384,11 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
     mine = units[lo:hi]
     k = int(0.9 * n)
     idx = None
-    if n_boot > 0:  # one upload of the (n_boot, k) index sets, shared by every unit
+    if n_boot > 0:
+        # RandomState(seed) is re-created per (region, subject) (evals.py:356), so every unit
+        # draws the same (n_boot, k) index sets: drawn once per call (host MT19937), one upload
         dev = next(iter(neural_rdms.values())).device
-        idx = torch.from_numpy(np.array(bootstrap_indices(seed, n, k, n_boot))).to(dev)
+        idx = torch.from_numpy(draw_bootstrap_indices(seed, n, k, n_boot)).to(dev)
     local: Dict[Tuple[str, str], np.ndarray] = {}
     need = {p for p, _ in mine}
     mplans = {}
