@@ -39,9 +39,8 @@ def _svd_predict(X_tr, Y_tr, X_new, alphas_per_target):
     U, s, Vt = np.linalg.svd(X_tr, full_matrices=False)
     UTY = U.T @ Y_tr
     XV = X_new @ Vt.T
-    # the product's kernel-form cut (lam = s^2 <= n eps_fp32 lam_max are exact zeros)
-    keep = s ** 2 > s.max() ** 2 * X_tr.shape[0] * np.finfo(np.float32).eps
-    f = np.where(keep[:, None], s[:, None] / (s[:, None] ** 2 + alphas_per_target[None, :]), 0.0)
+    # himalaya solve_ridge_cv_svd: every singular value, s / (s^2 + alpha)
+    f = s[:, None] / (s[:, None] ** 2 + alphas_per_target[None, :])
     return XV @ (f * UTY)
 
 

@@ -126,11 +126,11 @@ def test_corr_score_constant_column_is_nan(dev):
 @pytest.mark.parametrize("n,p", [(150, 20), (120, 400)])  # primal n > p and dual p > n
 def test_dual_ridge_cv_matches_primal_oracle(dev, n, p):
     import torch
-    from visreps_amd.analysis.encoding_score import gram, ridge_cv_predict
+    from visreps_amd.analysis.encoding_score import gram64, ridge_cv_predict
 
     X, Y = _data(n + 30, p, 5, n + p)
     Y[:, 4] = np.random.RandomState(1).randn(n + 30)  # one pure-noise target
-    K = gram(torch.from_numpy(X).to(dev))
+    K = gram64(torch.from_numpy(X).to(dev))
     pred, alphas = ridge_cv_predict(K, np.arange(n), np.arange(n, n + 30),
                                     torch.from_numpy(Y[:n]).to(dev))
     rp, ra = E.ridge_cv(X[:n], Y[:n], X[n:])
@@ -151,6 +151,57 @@ def test_primal_ridge_cv_matches_primal_oracle(dev, n, p):
     rp, ra = E.ridge_cv(X[:n], Y[:n], X[n:])
     assert np.array_equal(alphas, ra)
     assert np.max(np.abs(pred.cpu().numpy() - rp)) <= 1e-4 * max(1.0, np.abs(rp).max())
+
+
+def _decaying(n, p, v, cond, seed):
+    """X = U diag(s) V^T with s log-spaced over `cond` (condition number), Y = X w + noise."""
+    rs = np.random.RandomState(seed)
+    r = min(n, p)
+    U = np.linalg.qr(rs.randn(n, r))[0]
+    Vt = np.linalg.qr(rs.randn(p, r))[0].T
+    s = np.logspace(0, -np.log10(cond), r) * 30.0
+    X = (U * s) @ Vt
+    Y = X @ rs.randn(p, v) + 0.01 * rs.randn(n, v)
+    return X.astype(np.float32), Y.astype(np.float32)
+
+
+def _closed_form(X, Y, X_new, alphas):
+    """fp64 ridge per target: X_new (X^T X + a I)^-1 X^T y."""
+    X, Y, X_new = (np.asarray(a, np.float64) for a in (X, Y, X_new))
+    out = np.empty((X_new.shape[0], Y.shape[1]))
+    for t, a in enumerate(alphas):
+        w = np.linalg.solve(X.T @ X + a * np.eye(X.shape[1]), X.T @ Y[:, t])
+        out[:, t] = X_new @ w
+    return out
+
+
+def test_oracle_ridge_keeps_small_singular_values():
+    # himalaya's SVD solver keeps every singular value: on a spectrum decaying over 1e5 the
+    # oracle's refit equals the closed-form ridge at its chosen alphas
+    X, Y = _decaying(160, 40, 4, 1e5, 3)
+    pred, alphas = E.ridge_cv(X[:130], Y[:130], X[130:])
+    ref = _closed_form(X[:130], Y[:130], X[130:], alphas)
+    assert np.max(np.abs(pred - ref)) <= 1e-8 * np.abs(ref).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,p", [(130, 40), (90, 200)])  # primal and dual
+def test_ridge_cv_decaying_spectrum_matches_closed_form(dev, n, p):
+    # condition number 1e5: no component above the fp64 floor may be dropped
+    import torch
+    from visreps_amd.analysis.encoding_score import gram64, ridge_cv_predict, ridge_cv_predict_primal
+
+    X, Y = _decaying(n + 30, p, 4, 1e5, n + p)
+    Xt = torch.from_numpy(X).to(dev)
+    Yt = torch.from_numpy(Y[:n]).to(dev)
+    if p < n:
+        pred, alphas = ridge_cv_predict_primal(Xt[:n], Yt, Xt[n:])
+    else:
+        pred, alphas = ridge_cv_predict(gram64(Xt), np.arange(n), np.arange(n, n + 30), Yt)
+    ref = _closed_form(X[:n], Y[:n], X[n:], alphas)
+    assert np.max(np.abs(pred.cpu().numpy() - ref)) <= 1e-5 * np.abs(ref).max()
+    _, ra = E.ridge_cv(X[:n], Y[:n], X[n:])
+    assert np.array_equal(alphas, ra)
 
 
 @pytest.mark.gpu

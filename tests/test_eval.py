@@ -3,8 +3,8 @@
 CPU: CLI argument handling, config validation, loader ordering (string order for phase
 1, int order for shared test IDs, as neural.py:170/:474).
 GPU: eval() end to end at small size; the phase-2 point estimate and bootstrap are then
-re-derived with the CPU oracle from the same exact activations (|d rho| < 1e-4: the GPU
-and numpy RDMs differ in the last fp32 bits, which can move individual ranks)."""
+re-derived with the CPU oracle from the same exact activations: bit-level (1e-12) on the
+eval's own RDMs, and within 1e-5 on the oracle's numpy RDMs."""
 import numpy as np
 import pytest
 import torch
@@ -89,11 +89,22 @@ def test_eval_end_to_end_matches_oracle(dev):
                                                     data["shared_test_ids"])
         assert got_ids == data["shared_test_ids"]
         resp = np.stack([data["neural"][region][0]["test"][s] for s in data["shared_test_ids"]])
+        # (a) the eval's own RDMs (same kernel, same rows) through the oracle's scipy
+        #     Spearman + RandomState bootstrap: the Spearman path is exact
+        from visreps_amd.analysis import rsa as R
+        g_m = R.compute_rdm(acts.to(dev)).cpu().numpy()
+        g_n = R.compute_rdm(torch.from_numpy(resp.astype(np.float32)).to(dev)).cpu().numpy()
+        point, scores, lo, hi = O.bootstrap_rsa(g_m, g_n, n_bootstrap=20, seed=42)
+        assert abs(df.iloc[i]["score"] - point) <= 1e-12
+        assert np.max(np.abs(np.asarray(df.iloc[i]["bootstrap_scores"]) - scores)) <= 1e-12
+        assert df.iloc[i]["ci_low"] == lo and df.iloc[i]["ci_high"] == hi
+        # (b) fully oracle RDMs: within the north-star tolerance 1e-5
         m_rdm = O.compute_rdm(acts.numpy())
         n_rdm = O.compute_rdm(resp.astype(np.float32))
+        assert np.max(np.abs(m_rdm - g_m)) < 1e-5 and np.max(np.abs(n_rdm - g_n)) < 1e-5
         point, scores, lo, hi = O.bootstrap_rsa(m_rdm, n_rdm, n_bootstrap=20, seed=42)
-        assert abs(df.iloc[i]["score"] - point) < 1e-4
-        assert np.max(np.abs(np.asarray(df.iloc[i]["bootstrap_scores"]) - scores)) < 1e-4
+        assert abs(df.iloc[i]["score"] - point) < 1e-5
+        assert np.max(np.abs(np.asarray(df.iloc[i]["bootstrap_scores"]) - scores)) < 1e-5
 
 
 @pytest.mark.gpu

@@ -279,6 +279,26 @@ def test_rdm_tile_ranges_assemble_full_rdm(dev, n, d, world, mode, monkeypatch):
     assert torch.equal(full, full.T)
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_rdm_tile_ranges_wide_d_match_within_rounding(dev, world):
+    # at d = 4096 split-K engages and the one-launch RDM uses the wide kernel, so a tile
+    # range may sum in another order: entries agree to fp32 rounding, not bit for bit
+    from visreps_amd import pipeline as P
+
+    n, d = 3000, 4096
+    g = torch.Generator(device=dev).manual_seed(world)
+    x = torch.relu(torch.randn(n, d, device=dev, generator=g))
+    full = R.compute_rdm(x)
+    acc = torch.zeros(n, n, device=dev)
+    for t0, t1 in P.tile_ranges(n, world):
+        part = torch.zeros(n, n, device=dev)
+        P.rdm_tiles_into(x, part, t0, t1)
+        acc += part
+        del part
+    assert torch.equal(acc, acc.T)
+    assert (acc - full).abs().max().item() <= 2e-6
+
+
 @pytest.mark.parametrize("n,nb,levels_a",[(64, 70, None), (200, 130, None), (150, 64, 6)])
 def test_bootstrap_multi_equals_per_unit(dev, n, nb, levels_a):
     # one shared (neural) plan against several model plans: every row bit-equal to the

@@ -135,10 +135,21 @@ def kfold_splits(n: int, n_splits: int = 5):
 
 
 def _eig(K: torch.Tensor):
+    """Eigendecomposition of an fp64 Gram. Every component with lam above the fp64
+    rounding floor of the decomposition (n eps_64 lam_max) is kept, as himalaya's SVD
+    solver keeps every singular value: below that floor lam is rounding noise whose
+    1/(lam + alpha) would only amplify it."""
     lam, Q = torch.linalg.eigh(K)
-    tol = lam.abs().max() * K.size(0) * float(np.finfo(np.float32).eps)
+    tol = lam.abs().max() * K.size(0) * float(np.finfo(np.float64).eps)
     keep = lam > tol
     return lam, Q, keep
+
+
+def gram64(x: torch.Tensor) -> torch.Tensor:
+    """x x^T in fp64 (the ridge solves are conditioning-sensitive; the RSA Grams use
+    vr_gram_f32)."""
+    xd = x.double()
+    return xd @ xd.T
 
 
 def _dual_predict(K_new: torch.Tensor, lam, Q, keep, Y: torch.Tensor, alphas: torch.Tensor):
@@ -182,7 +193,7 @@ def ridge_cv_predict(K: torch.Tensor, fit: np.ndarray, new: np.ndarray, Y_fit: t
 def ridge_cv_predict_primal(X_fit: torch.Tensor, Y_fit: torch.Tensor, X_new: torch.Tensor,
                             alphas=ALPHAS, cv: int = 5):
     """The same RidgeCV in primal form, for layers narrower than the fit set (p < n): per
-    fold the p x p Gram X_T^T X_T on the MFMA kernel (vr_gram_f32 of X_T^T), its
+    fold the fp64 p x p Gram X_T^T X_T (gram64), its
     eigendecomposition V diag(lam) V^T, and predictions X_V V diag(1/(lam + alpha))
     V^T X_T^T Y_T (= the SVD solution with lam = s^2). Returns (predictions fp32, alphas)."""
     dev = X_fit.device
@@ -193,7 +204,7 @@ def ridge_cv_predict_primal(X_fit: torch.Tensor, Y_fit: torch.Tensor, X_new: tor
 
     def solve(rows):
         Xt = Xd[rows]
-        lam, V, keep = _eig(gram(Xt.T.contiguous()).double())
+        lam, V, keep = _eig(gram64(Xt.T))
         VtXtY = V.T @ (Xt.double().T @ Yd[rows])
         return lam, V, keep, VtXtY
 
@@ -237,13 +248,13 @@ def _flatten(acts, dev) -> Dict[str, torch.Tensor]:
 def _fit_and_score(X_fit: torch.Tensor, Y_fit: torch.Tensor, X_new: torch.Tensor,
                    Y_new: torch.Tensor, alphas):
     """RidgeCV on (X_fit, Y_fit), predictions for X_new and their mean Pearson r against
-    Y_new (encoding_score.py:47-62). One MFMA Gram of the stacked rows gives both kernel
+    Y_new (encoding_score.py:47-62). One fp64 Gram of the stacked rows gives both kernel
     blocks."""
     n_fit, p = X_fit.shape
     if p < n_fit:  # narrow layer: p x p Grams per fold (primal)
         pred, _ = ridge_cv_predict_primal(X_fit, Y_fit, X_new, alphas)
         return pred, corr_score(Y_new, pred)
-    K = gram(torch.cat([X_fit, X_new], dim=0))
+    K = gram64(torch.cat([X_fit, X_new], dim=0))
     fit = np.arange(n_fit)
     new = np.arange(n_fit, K.size(0))
     pred, _ = ridge_cv_predict(K, fit, new, Y_fit, alphas)

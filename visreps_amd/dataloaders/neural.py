@@ -9,6 +9,12 @@ with a deterministic NSD-shaped synthetic source:
       "shared_test_ids": [sid, ...]  sorted by int (neural.py:170),
       "stimuli": {sid: row},         images generated on demand
   }
+  load_things_synthetic(cfg) -> (targets, stimuli), the THINGS-behaviour contract
+      (neural.py:313-336): targets = {"embeddings": {concept: (66,) float32},
+      "image_ids": {concept: [sid, ...]}}, stimuli = {sid: image}
+  load_nsd_synthetic_test_data(cfg, subjects, regions) -> {"neural": {region: {subj:
+      {sid: (V,)}}}, "stimuli", "test_ids" (sorted names), "regions", "subjects"}
+      (neural.py:192-241; 220 stimuli)
   _make_loader(stimuli, transform, batch, workers) iterates (images, ids) in the
   lexicographic ID order of the reference's _StimuliDataset (neural.py:474, :513-523).
 
@@ -26,7 +32,8 @@ import torch
 
 from . import synthetic as syn
 
-__all__ = ["SyntheticStimuli", "load_synthetic_data", "_make_loader", "StimulusLoader"]
+__all__ = ["SyntheticStimuli", "load_synthetic_data", "load_things_synthetic",
+           "load_nsd_synthetic_test_data", "_make_loader", "StimulusLoader"]
 
 
 class SyntheticStimuli(dict):
@@ -72,8 +79,71 @@ class StimulusLoader:
             yield self.stimuli.images([self.stimuli[s] for s in ids]), ids
 
 
-def _make_loader(stimuli, transform, batch, workers):  # noqa: ARG001  (tensors need no transform)
+def _make_loader(stimuli, transform, batch, workers):  # noqa: ARG001
+    """Synthetic stimuli are generated as normalised tensors (no transform applies);
+    image files go through dataloaders.obj_cls.ImageFolderLoader with get_transform."""
     return StimulusLoader(stimuli, batch)
+
+
+def _device():
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+        else torch.device("cpu")
+
+
+def _responses(stimuli: SyntheticStimuli, n: int, voxels: Dict[str, int], seed: int,
+               noise: float = 3.0) -> Dict[str, np.ndarray]:
+    """make_responses for rows 0..n-1 of `stimuli`, in 4096-row chunks, on the host."""
+    out = {r: np.empty((n, v), np.float32) for r, v in voxels.items()}
+    for c0 in range(0, n, 4096):
+        rr = range(c0, min(n, c0 + 4096))
+        imgs = syn.make_images(rr, seed=stimuli.seed, device=stimuli.device)
+        resp = syn.make_responses(imgs, rr, voxels, seed=seed, noise=noise)
+        for r in voxels:
+            out[r][rr.start:rr.stop] = resp[r].cpu().numpy()
+        del imgs, resp
+    return out
+
+
+def load_things_synthetic(cfg) -> Tuple[Dict, SyntheticStimuli]:
+    """THINGS-shaped behavioural data: cfg.synthetic.things_concepts concepts (default
+    1854) with things_images images each (default 2); a concept's 66-d embedding is the
+    non-negative (SPoSE-like) mean over its images of a response to their latent."""
+    sc = cfg.get("synthetic", {}) or {}
+    n_c = int(sc.get("things_concepts", 1854))
+    per = int(sc.get("things_images", 2))
+    seed = int(sc.get("seed", 20260306)) + 17
+    concepts = [f"concept{c:04d}" for c in range(n_c)]
+    rows: Dict[str, int] = {}
+    image_ids: Dict[str, List[str]] = {}
+    for c, name in enumerate(concepts):
+        sids = [f"{name}_{j:02d}s" for j in range(per)]
+        image_ids[name] = sids
+        for j, sid in enumerate(sids):
+            rows[sid] = c * per + j
+    stimuli = SyntheticStimuli(rows, seed, _device())
+    emb = _responses(stimuli, n_c * per, {"things": 66}, seed + 3, noise=1.0)["things"]
+    embeddings = {name: np.maximum(emb[c * per:(c + 1) * per].mean(0), 0.0).astype(np.float32)
+                  for c, name in enumerate(concepts)}
+    return {"embeddings": embeddings, "image_ids": image_ids}, stimuli
+
+
+def load_nsd_synthetic_test_data(cfg, subjects: Sequence[int], regions: Sequence[str]) -> Dict:
+    """NSD-Synthetic-shaped test data: cfg.synthetic.nsd_synthetic_n stimuli (default 220,
+    names sorted), per-subject responses with the NSD source's voxel counts."""
+    sc = cfg.get("synthetic", {}) or {}
+    n = int(sc.get("nsd_synthetic_n", 220))
+    seed = int(sc.get("seed", 20260306)) + 29
+    vox_cfg = dict(sc.get("voxels", {}) or {})
+    voxels = {r: int(vox_cfg.get(r, syn.NSD_ROIS_4.get(r, 1000))) for r in regions}
+    names = [f"synth{i:03d}" for i in range(n)]
+    stimuli = SyntheticStimuli({s: i for i, s in enumerate(names)}, seed, _device())
+    neural: Dict = {r: {} for r in regions}
+    for subj in subjects:
+        resp = _responses(stimuli, n, voxels, seed + 7 * (int(subj) + 1))
+        for r in regions:
+            neural[r][subj] = {s: resp[r][i] for i, s in enumerate(names)}
+    return {"regions": list(regions), "subjects": list(subjects), "neural": neural,
+            "stimuli": stimuli, "test_ids": sorted(names)}
 
 
 def load_synthetic_data(cfg, subjects: Sequence[int], regions: Sequence[str]) -> Dict:

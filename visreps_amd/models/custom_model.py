@@ -44,9 +44,10 @@ class BaseCNN(nn.Module):
         self.num_classes = num_classes
         self.dropout = dropout
         self.pooling_type = pooling_type
+        # trainable_layers (custom_model.py:36-68) only freezes parameters for training;
+        # it is accepted for signature parity and has no effect on the eval path
+        del trainable_layers
         self._build_architecture()
-        if trainable_layers is not None:
-            self._set_trainable_layers(trainable_layers)
         self._initialize_weights()
 
     def _pool(self, kernel_size=3, stride=2):
@@ -72,29 +73,6 @@ class BaseCNN(nn.Module):
             nn.ReLU(inplace=True), nn.Dropout(p=self.dropout), nn.Linear(self.hidden, self.hidden),
             nn.BatchNorm1d(self.hidden), nn.ReLU(inplace=True), nn.Linear(self.hidden, n_cls),
         )
-
-    def _set_trainable_layers(self, trainable_layers: Dict[str, str]):
-        convs = [m for m in self.features.modules() if isinstance(m, nn.Conv2d)]
-        fcs = [m for m in self.classifier.modules() if isinstance(m, nn.Linear)]
-        conv_bns = [m for m in self.features.modules() if isinstance(m, (nn.BatchNorm2d, nn.BatchNorm1d))]
-        fc_bns = [m for m in self.classifier.modules() if isinstance(m, (nn.BatchNorm2d, nn.BatchNorm1d))]
-        conv_mask = [c == "1" for c in trainable_layers.get("conv", "1" * len(convs))]
-        fc_mask = [c == "1" for c in trainable_layers.get("fc", "1" * len(fcs))]
-        for layer, on in zip(convs + fcs, conv_mask + fc_mask):
-            for prm in layer.parameters():
-                prm.requires_grad = on
-        self._frozen_bns = []
-        for bn, on in zip(conv_bns + fc_bns, conv_mask + fc_mask):
-            if not on:
-                for prm in bn.parameters():
-                    prm.requires_grad = False
-                self._frozen_bns.append(bn)
-
-    def train(self, mode=True):
-        super().train(mode)
-        for bn in getattr(self, "_frozen_bns", []):
-            bn.eval()
-        return self
 
     def _initialize_weights(self):
         n_cls = self.num_classes if self.num_classes is not None else 1000

@@ -15,7 +15,11 @@ Per step (BASELINE.json configs[1]: CustomCNN points x NSD ROIs, N stimuli, 1000
                   is the point estimate + n_boot subsets (evals.py:341-373 semantics,
                   RandomState(seed) per unit);
   5. gather       per-unit score vectors are gathered to every rank.
-Scores are exact-integer Spearman values, so they do not depend on the world size.
+Given the RDMs, scores are exact-integer Spearman values and do not depend on how units
+are split over ranks. The RDM entries themselves can differ in the last fp32 bits between
+world sizes: the Gram's split-K factor and the wide 256x256 kernel are chosen per launched
+tile range (csrc/rdm.hip), so a rank's range may sum a tile in another order than the
+one-GPU launch (tests/test_gpu_parity.py::test_rdm_tile_ranges_wide_d_match_within_rounding).
 """
 from __future__ import annotations
 
