@@ -224,6 +224,19 @@ int vr_srp_csr_f32(const int32_t* indptr, const int32_t* indices, const float* v
                    int64_t ldo, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------
+ * Image preprocessing: the eval loaders' get_transform (visreps/dataloaders/obj_cls.py:
+ * 27-45) = torchvision Resize(resize, BILINEAR) on a PIL image (Pillow's ImagingResample:
+ * antialiased separable bilinear, 22-bit fixed point, uint8 intermediate) ->
+ * CenterCrop(crop) -> ToTensor -> Normalize(mean, std), bit-exact.
+ * src [device] B x H x W x 3 uint8 (RGB, same size images); out [device] B x 3 x crop x
+ * crop float32; mean, std [host] 3 floats each. crop must not exceed the resized image.
+ * -------------------------------------------------------------------------- */
+size_t vr_transform_workspace(int64_t B, int64_t H, int64_t W, int64_t resize, int64_t crop);
+int vr_transform_u8(const uint8_t* src, int64_t B, int64_t H, int64_t W, int64_t resize,
+                    int64_t crop, const float* mean, const float* std, float* out, void* ws,
+                    size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------
  * Host: legacy numpy RandomState (MT19937) index streams, bit-exact.
  * Replaces np.random.RandomState(seed) + .choice(n, k, replace=False) / .permutation(n)
  * (evals.py:260-261,356,362-364; rsa.py:169,176,248-250; evals.py:111-113).

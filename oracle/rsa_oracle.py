@@ -146,9 +146,12 @@ def bootstrap_rsa(model_rdm, neural_rdm, n_bootstrap: int = 1000, seed: int = 42
 def compute_rsa(cfg: Dict, sel_acts: Dict[str, np.ndarray], sel_neural: np.ndarray,
                 eval_acts: Dict[str, np.ndarray], eval_neural: np.ndarray,
                 n_select: Optional[int] = None, bootstrap: bool = True,
-                n_bootstrap: int = 1000, seed: int = 42) -> List[Dict]:
+                n_bootstrap: int = 1000, seed: int = 42, rdm_fn=None) -> List[Dict]:
     """rsa.py:132-281 without the printing: one RandomState(seed) shared by the
-    n_select draw and the bootstrap draws; first strict maximum wins the selection."""
+    n_select draw and the bootstrap draws; first strict maximum wins the selection.
+    rdm_fn replaces compute_rdm (a test hands in the product's RDM kernel to check the
+    selection / Spearman / bootstrap logic on bit-identical RDMs)."""
+    compute_rdm_ = rdm_fn or compute_rdm
     method = cfg.get("compare_method", "spearman").lower()
     rng = np.random.RandomState(seed)
     n_train = sel_neural.shape[0]
@@ -157,20 +160,20 @@ def compute_rsa(cfg: Dict, sel_acts: Dict[str, np.ndarray], sel_neural: np.ndarr
         sel_idx = rng.choice(n_train, size=n_select, replace=False)
     else:
         sel_idx = np.arange(n_train)
-    neural_rdm_sel = compute_rdm(sel_neural[sel_idx])
+    neural_rdm_sel = compute_rdm_(sel_neural[sel_idx])
     selection_scores = []
     best_layer, best_score = None, -float("inf")
     for layer, acts in sel_acts.items():
         a = acts[sel_idx]
         flat = a.reshape(a.shape[0], -1)
-        score = compute_rdm_correlation(compute_rdm(flat), neural_rdm_sel,
+        score = compute_rdm_correlation(compute_rdm_(flat), neural_rdm_sel,
                                         correlation=method.capitalize())
         selection_scores.append({"layer": layer, "score": score})
         if score > best_score:
             best_score, best_layer = score, layer
     t = eval_acts[best_layer]
-    test_model_rdm = compute_rdm(t.reshape(t.shape[0], -1))
-    test_neural_rdm = compute_rdm(eval_neural)
+    test_model_rdm = compute_rdm_(t.reshape(t.shape[0], -1))
+    test_neural_rdm = compute_rdm_(eval_neural)
     point = compute_rdm_correlation(test_model_rdm, test_neural_rdm,
                                     correlation=method.capitalize())
     ci_low = ci_high = None

@@ -3,9 +3,9 @@
 seeded synthetic stand-ins, re-derived with the CPU oracle from the same exact
 activations.
 
-Tolerances: the layer choice must match exactly; scores to 1e-4, because the oracle
-builds its RDMs in numpy float32 whose last bits differ from the MFMA Gram's and can move
-individual ranks (the engine itself is checked at 1e-12 on identical RDMs elsewhere)."""
+Tolerances: the oracle is run on the product's own RDMs (rdm_fn = the HIP Gram), so
+layer choice, selection scores, point estimate and bootstrap must agree to 1e-12; the
+RDM kernel itself is checked against numpy's RDMs entry-wise (1e-5)."""
 import numpy as np
 import pytest
 import torch
@@ -30,6 +30,17 @@ def _model(cfg, dev):
     return mutils.configure_feature_extractor(cfg, mutils.load_model(cfg, dev))
 
 
+def _gpu_rdm(dev):
+    from visreps_amd.analysis import rsa as R
+
+    def fn(x):
+        x = np.asarray(x, np.float32)
+        g = R.compute_rdm(torch.from_numpy(x.reshape(x.shape[0], -1)).to(dev)).cpu().numpy()
+        assert np.max(np.abs(g - O.compute_rdm(x.reshape(x.shape[0], -1)))) < 1e-5
+        return g
+    return fn
+
+
 def _exact(model, stimuli, dev, layer, ids=None):
     from visreps_amd.dataloaders.neural import _make_loader
     from visreps_amd.models import utils as mutils
@@ -41,7 +52,8 @@ def _exact(model, stimuli, dev, layer, ids=None):
 # --------------------------------------------------------------------------- THINGS
 def test_things_behavior_end_to_end_matches_oracle(dev):
     from visreps_amd import evals
-    from visreps_amd.analysis.alignment import prepare_concept_alignment
+    from visreps_amd.analysis.alignment import AlignmentData, prepare_concept_alignment
+    from visreps_amd.analysis.rsa import _concept_average_exact
     from visreps_amd.dataloaders.neural import _make_loader, load_things_synthetic
     from visreps_amd.models import utils as mutils
 
@@ -58,30 +70,33 @@ def test_things_behavior_end_to_end_matches_oracle(dev):
     model = _model(cfg, dev)
     targets, stimuli = load_things_synthetic(cfg)
     acts, ids = mutils.get_activations(model, _make_loader(stimuli, None, 64, 0), dev,
-                                       srp_seed=cfg.srp_seed)
+                                       keep_on_device=True, srp_seed=cfg.srp_seed)
     conc = prepare_concept_alignment(cfg, acts, targets, ids)
     perm = np.random.RandomState(42).permutation(60)
     sel, ev = perm[:12], perm[12:]
     concepts = conc.stimulus_ids
-    sel_acts = {l: a.numpy()[sel] for l, a in conc.activations.items()}
+    sel_acts = {l: a.cpu().numpy()[sel] for l, a in conc.activations.items()}
     neural = conc.neural.numpy()
+    evaluation = AlignmentData({}, conc.neural[ev], stimulus_ids=[concepts[i] for i in ev],
+                               concept_image_ids={concepts[i]: targets["image_ids"][concepts[i]] for i in ev})
 
     class ExactMeans(dict):  # the oracle asks only for its best layer
         def __missing__(self, layer):
+            # concept means of the exact activations on the device, as the eval forms them
+            # (their arithmetic: tests/test_concepts.py)
             raw, raw_ids = _exact(model, stimuli, dev, layer)
-            pos = {s: i for i, s in enumerate(raw_ids)}
-            out = np.stack([raw[[pos[s] for s in targets["image_ids"][concepts[i]]]].astype(np.float32).mean(0)
-                            for i in ev])
+            out = _concept_average_exact(torch.from_numpy(raw).to(dev), raw_ids, evaluation).cpu().numpy()
             self[layer] = out
             return out
 
     ref = O.compute_rsa({"compare_method": "spearman"}, sel_acts, neural[sel], ExactMeans(),
-                        neural[ev], n_select=None, bootstrap=True, n_bootstrap=15, seed=42)[0]
+                        neural[ev], n_select=None, bootstrap=True, n_bootstrap=15, seed=42,
+                        rdm_fn=_gpu_rdm(dev))[0]
     assert row["layer"] == ref["layer"]
     for g, r in zip(row["layer_selection_scores"], ref["layer_selection_scores"]):
-        assert g["layer"] == r["layer"] and abs(g["score"] - r["score"]) < 1e-4
-    assert abs(row["score"] - ref["score"]) < 1e-4
-    assert np.max(np.abs(np.asarray(row["bootstrap_scores"]) - ref["bootstrap_scores"])) < 1e-4
+        assert g["layer"] == r["layer"] and abs(g["score"] - r["score"]) <= 1e-12
+    assert abs(row["score"] - ref["score"]) <= 1e-12
+    assert np.max(np.abs(np.asarray(row["bootstrap_scores"]) - ref["bootstrap_scores"])) <= 1e-12
 
 
 def test_things_behavior_encoding_refused(dev):
@@ -122,9 +137,10 @@ def test_nsd_synthetic_reuses_nsd_layers_and_matches_oracle(dev, tmp_path, monke
             acts, got = _exact(model, data["stimuli"], dev, row["layer"], data["test_ids"])
             assert got == data["test_ids"]
             resp = np.stack([data["neural"][region][subj][s] for s in data["test_ids"]])
-            point, scores, _, _ = O.bootstrap_rsa(O.compute_rdm(acts), O.compute_rdm(resp), 12, 42)
-            assert abs(row["score"] - point) < 1e-4
-            assert np.max(np.abs(np.asarray(row["bootstrap_scores"]) - scores)) < 1e-4
+            rdm = _gpu_rdm(dev)
+            point, scores, _, _ = O.bootstrap_rsa(rdm(acts), rdm(resp), 12, 42)
+            assert abs(row["score"] - point) <= 1e-12
+            assert np.max(np.abs(np.asarray(row["bootstrap_scores"]) - scores)) <= 1e-12
 
 
 # --------------------------------------------------------------------------- PCA reconstruction
@@ -147,5 +163,6 @@ def test_rsa_phase2_reconstruct_from_pcs_matches_oracle(dev):
     rec = P.reconstruct_from_pcs(acts, 3).astype(np.float32)
     resp = np.stack([data["neural"]["V1"][0]["test"][s] for s in data["shared_test_ids"]])
     point, scores, _, _ = O.bootstrap_rsa(O.compute_rdm(rec), O.compute_rdm(resp), 10, 42)
+    # the reconstruction is fp64 on both sides; the RDMs are float32 numpy vs MFMA
     assert abs(df.iloc[0]["score"] - point) < 1e-4
     assert np.max(np.abs(np.asarray(df.iloc[0]["bootstrap_scores"]) - scores)) < 1e-4

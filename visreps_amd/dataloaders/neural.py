@@ -80,9 +80,14 @@ class StimulusLoader:
 
 
 def _make_loader(stimuli, transform, batch, workers):  # noqa: ARG001
-    """Synthetic stimuli are generated as normalised tensors (no transform applies);
-    image files go through dataloaders.obj_cls.ImageFolderLoader with get_transform."""
-    return StimulusLoader(stimuli, batch)
+    """Synthetic stimuli are generated as normalised tensors (no transform applies); any
+    other {key: path | uint8 array | PIL image} mapping is read and transformed on the
+    device by dataloaders.obj_cls.ImageLoader (get_transform, vr_transform_u8)."""
+    if isinstance(stimuli, SyntheticStimuli):
+        return StimulusLoader(stimuli, batch)
+    from .obj_cls import ImageLoader
+
+    return ImageLoader(stimuli, transform, batch)
 
 
 def _device():

@@ -61,8 +61,9 @@ def _load_cfg(cfg):
     """Merge the training config of a checkpoint run under the runtime cfg (evals.py:31-41)."""
     path = f"{cfg.checkpoint_dir}/cfg{cfg.cfg_id}{get_seed_letter(cfg.seed)}/config.json"
     if not os.path.exists(path):
-        if cfg.get("random_init", False):
+        if cfg.get("random_init", False):  # no training run: its config fields default
             cfg.epoch = cfg.get("epoch", 0)
+            cfg.model_name = cfg.get("model_name") or "CustomCNN"
             return cfg
         raise FileNotFoundError(f"training config not found: {path}")
     with open(path) as f:
