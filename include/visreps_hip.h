@@ -231,10 +231,13 @@ int vr_srp_csr_f32(const int32_t* indptr, const int32_t* indices, const float* v
  * src [device] B x H x W x 3 uint8 (RGB, same size images); out [device] B x 3 x crop x
  * crop float32; mean, std [host] 3 floats each. crop must not exceed the resized image.
  * -------------------------------------------------------------------------- */
-size_t vr_transform_workspace(int64_t B, int64_t H, int64_t W, int64_t resize, int64_t crop);
+size_t vr_transform_workspace(int64_t B, int64_t H, int64_t W, int64_t resize, int64_t crop,
+                              int filter);
+/* filter: 0 = BILINEAR (get_transform), 1 = BICUBIC (the CLIP and timm DINOv3 loaders,
+ * clip_representations.py:27, dino_representations.py:31-32) */
 int vr_transform_u8(const uint8_t* src, int64_t B, int64_t H, int64_t W, int64_t resize,
-                    int64_t crop, const float* mean, const float* std, float* out, void* ws,
-                    size_t ws_bytes, void* stream);
+                    int64_t crop, int filter, const float* mean, const float* std, float* out,
+                    void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------
  * Host: legacy numpy RandomState (MT19937) index streams, bit-exact.

@@ -16,11 +16,24 @@ import numpy as np
 PREC = 22  # PRECISION_BITS = 32 - 8 - 2
 
 
-def _coeffs(in_size: int, out_size: int):
-    """(bounds (out, 2) int, kk (out, ksize) int32) of Pillow's bilinear filter."""
+def _filter(kind: str, x: float) -> float:
+    """Resample.c bilinear_filter / bicubic_filter (a = -0.5)."""
+    x = -x if x < 0.0 else x
+    if kind == "bicubic":
+        a = -0.5
+        if x < 1.0:
+            return ((a + 2.0) * x - (a + 3.0)) * x * x + 1
+        if x < 2.0:
+            return (((x - 5) * x + 8) * x - 4) * a
+        return 0.0
+    return 1.0 - x if x < 1.0 else 0.0
+
+
+def _coeffs(in_size: int, out_size: int, kind: str = "bilinear"):
+    """(bounds (out, 2) int, kk (out, ksize) int32) of Pillow's filter."""
     scale = float(np.float32(in_size) - np.float32(0.0)) / out_size
     filterscale = max(scale, 1.0)
-    support = 1.0 * filterscale
+    support = (2.0 if kind == "bicubic" else 1.0) * filterscale
     ksize = int(math.ceil(support)) * 2 + 1
     bounds = np.zeros((out_size, 2), np.int64)
     kk = np.zeros((out_size, ksize), np.int64)
@@ -32,8 +45,7 @@ def _coeffs(in_size: int, out_size: int):
         xmax = min(int(center + support + 0.5), in_size) - xmin
         w = []
         for x in range(xmax):
-            t = abs((x + xmin - center + 0.5) * ss)
-            w.append(1.0 - t if t < 1.0 else 0.0)
+            w.append(_filter(kind, (x + xmin - center + 0.5) * ss))
         ww = sum(w)  # left-to-right double sum, as the C loop
         k = [v / ww if ww != 0.0 else v for v in w]
         for x, v in enumerate(k):
@@ -55,15 +67,15 @@ def _pass(a: np.ndarray, bounds, kk, axis: int) -> np.ndarray:
     return np.moveaxis(out, 0, axis)
 
 
-def resample(img: np.ndarray, new_w: int, new_h: int) -> np.ndarray:
-    """Pillow Image.resize((new_w, new_h), BILINEAR) of an H x W x 3 uint8 image."""
+def resample(img: np.ndarray, new_w: int, new_h: int, kind: str = "bilinear") -> np.ndarray:
+    """Pillow Image.resize((new_w, new_h), BILINEAR | BICUBIC) of an H x W x 3 uint8 image."""
     H, W, _ = img.shape
     out = img
     if new_w != W:
-        b, k = _coeffs(W, new_w)
+        b, k = _coeffs(W, new_w, kind)
         out = _pass(out, b, k, 1)
     if new_h != H:
-        b, k = _coeffs(H, new_h)
+        b, k = _coeffs(H, new_h, kind)
         out = _pass(out, b, k, 0)
     return out
 
@@ -75,11 +87,11 @@ def resize_size(H: int, W: int, size: int):
     return (new_long, new_short) if W <= H else (new_short, new_long)
 
 
-def transform(img: np.ndarray, resize: int, crop: int, mean, std) -> np.ndarray:
+def transform(img: np.ndarray, resize: int, crop: int, mean, std, kind: str = "bilinear") -> np.ndarray:
     """get_transform on one H x W x 3 uint8 image -> 3 x crop x crop float32."""
     H, W, _ = img.shape
     nh, nw = resize_size(H, W, resize)
-    r = resample(img, nw, nh)
+    r = resample(img, nw, nh, kind)
     top = int(round((nh - crop) / 2.0))
     left = int(round((nw - crop) / 2.0))
     c = r[top:top + crop, left:left + crop]

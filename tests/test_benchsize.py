@@ -251,3 +251,44 @@ def test_cfg5_vit_bf16_rdm(dev, vit_tokens, which):
     assert torch.all(torch.diagonal(rdm) == 0)
     cols = _rows(dev, x.size(0), 10)
     assert torch.equal(rdm[rows][:, cols], rdm[cols][:, rows].T)
+
+
+def _foundation_feats(dev, model, extract_fn, n=50000, batch=500):
+    from visreps_amd.dataloaders.synthetic import make_images
+
+    feats = None
+    with torch.no_grad():
+        for b0 in range(0, n, batch):
+            imgs = make_images(range(b0, b0 + batch), device=dev, dtype=torch.bfloat16)
+            f = extract_fn(model, imgs)
+            if feats is None:
+                feats = torch.empty((n, f.size(1)), dtype=torch.bfloat16, device=dev)
+            feats[b0:b0 + batch] = f
+    return feats
+
+
+@pytest.mark.parametrize("which", ["clip", "dino"])
+def test_cfg5_foundation_bf16_rdm(dev, which):
+    """configs[4]'s CLIP ViT-L/14 image embedding (encode_image / its norm) and the DINOv3
+    ViT-L/16 CLS (random init, bf16) on 50k synthetic images: bf16 RDM, fp64 rows."""
+    from visreps_amd import extract_representations as X
+    from visreps_amd.models.foundation import clip_vit_l14, dinov3_vit_l16
+
+    torch.manual_seed(0)
+    if which == "clip":
+        model, fn = X.clip_image(clip_vit_l14().to(dev).eval().to(torch.bfloat16))
+    else:
+        model, fn = X.dino_cls(dinov3_vit_l16().to(dev).eval().to(torch.bfloat16))
+    x = _foundation_feats(dev, model, fn)
+    del model
+    torch.cuda.empty_cache()
+    assert x.dtype == torch.bfloat16 and x.shape == (50000, 768 if which == "clip" else 1024)
+    assert torch.isfinite(x).all()
+    rdm = R.compute_rdm(x)
+    rows = _rows(dev, x.size(0), 11)
+    err = _row_err(rdm, x.float(), rows)
+    err32 = _row_err(_fp32_rdm(x), x.float(), rows)
+    assert err <= max(ROW_TOL, err32), (which, err, err32)
+    assert torch.all(torch.diagonal(rdm) == 0)
+    cols = _rows(dev, x.size(0), 12)
+    assert torch.equal(rdm[rows][:, cols], rdm[cols][:, rows].T)

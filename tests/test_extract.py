@@ -61,3 +61,54 @@ def test_name_mismatch_raises():
     loader = torch.utils.data.DataLoader(_DS(2, 64, named=False), batch_size=2)
     with pytest.raises(ValueError, match="Mismatch"):
         X.extract_features(model, [loader], fn, torch.device("cpu"))
+
+
+def test_clip_visual_structure_and_unit_rows():
+    # clip/model.py VisionTransformer at a tiny width: token layout, ln_post on the class
+    # token, projection, and the dump's row normalisation
+    from visreps_amd.models.foundation import CLIPImageModel, CLIPVisual
+
+    torch.manual_seed(0)
+    m = CLIPImageModel(input_resolution=28, patch_size=14, width=32, layers=2, heads=4, output_dim=16).eval()
+    v = m.visual
+    assert v.positional_embedding.shape == (5, 32) and v.conv1.bias is None
+    assert isinstance(v.transformer[0].mlp.gelu, torch.nn.Module)
+    x = torch.randn(3, 3, 28, 28)
+    model, fn = X.clip_image(m)
+    with torch.no_grad():
+        f = fn(model, x)
+        # manual forward of the tower
+        t = v.conv1(x).reshape(3, 32, -1).permute(0, 2, 1)
+        t = torch.cat([v.class_embedding + torch.zeros(3, 1, 32), t], 1) + v.positional_embedding
+        t = v.transformer(v.ln_pre(t).permute(1, 0, 2)).permute(1, 0, 2)
+        ref = v.ln_post(t[:, 0]) @ v.proj
+    assert torch.allclose(f, ref / ref.norm(dim=-1, keepdim=True), atol=1e-6)
+    assert torch.allclose(f.norm(dim=-1), torch.ones(3), atol=1e-6)
+
+
+def test_clip_vit_l14_dimensions():
+    from visreps_amd.models.foundation import clip_vit_l14
+
+    v = clip_vit_l14().visual
+    assert v.conv1.weight.shape == (1024, 3, 14, 14)
+    assert v.positional_embedding.shape == (257, 1024) and v.proj.shape == (1024, 768)
+    assert len(v.transformer) == 24 and v.transformer[0].attn.num_heads == 16
+
+
+def test_dino_structure_and_cls_rows():
+    from visreps_amd.models.foundation import DINOv3ViT, _apply_rope, _rope_tables
+
+    torch.manual_seed(0)
+    m = DINOv3ViT(img_size=32, patch_size=16, embed_dim=32, depth=2, num_heads=4, num_registers=4).eval()
+    x = torch.randn(2, 3, 32, 32)
+    with torch.no_grad():
+        tok = m.forward_features(x)
+    assert tok.shape == (2, 1 + 4 + 4, 32)
+    model, fn = X.dino_cls(m)
+    with torch.no_grad():
+        f = fn(model, x)
+    assert torch.allclose(f, F.normalize(tok[:, 0], dim=-1), atol=1e-6)
+    # the rotary embedding is a rotation: norms of q/k rows are preserved
+    cos, sin = _rope_tables(2, 8)
+    q = torch.randn(1, 1, 4, 8)
+    assert torch.allclose(_apply_rope(q, cos, sin).norm(dim=-1), q.norm(dim=-1), atol=1e-5)

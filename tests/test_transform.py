@@ -21,12 +21,13 @@ def _img(h, w, seed):
     return np.clip(smooth * 255 + rs.randn(h, w, 3) * 20, 0, 255).astype(np.uint8)
 
 
-def _pil_ref(img, resize, crop, mean, std):
+def _pil_ref(img, resize, crop, mean, std, kind="bilinear"):
     from PIL import Image
 
     H, W, _ = img.shape
     nh, nw = T.resize_size(H, W, resize)
-    r = np.asarray(Image.fromarray(img, "RGB").resize((nw, nh), Image.BILINEAR))
+    f = Image.BICUBIC if kind == "bicubic" else Image.BILINEAR
+    r = np.asarray(Image.fromarray(img, "RGB").resize((nw, nh), f))
     top, left = int(round((nh - crop) / 2.0)), int(round((nw - crop) / 2.0))
     c = r[top:top + crop, left:left + crop]
     x = np.transpose(c, (2, 0, 1)).astype(np.float32) / np.float32(255)
@@ -41,6 +42,16 @@ def test_oracle_resample_matches_pillow(h, w):
     for nw, nh in [T.resize_size(h, w, 256)[::-1], (w // 3 + 1, h // 2 + 5), (w + 37, h + 11)]:
         ref = np.asarray(Image.fromarray(img, "RGB").resize((nw, nh), Image.BILINEAR))
         assert np.array_equal(T.resample(img, nw, nh), ref)
+
+
+@pytest.mark.parametrize("h,w", [(425, 425), (300, 500), (240, 320), (64, 90)])
+def test_oracle_bicubic_resample_matches_pillow(h, w):
+    from PIL import Image
+
+    img = _img(h, w, h + 3 * w)
+    for nw, nh in [T.resize_size(h, w, 224)[::-1], (w + 19, h + 7)]:
+        ref = np.asarray(Image.fromarray(img, "RGB").resize((nw, nh), Image.BICUBIC))
+        assert np.array_equal(T.resample(img, nw, nh, "bicubic"), ref)
 
 
 def test_oracle_transform_matches_pil_pipeline():
@@ -107,3 +118,18 @@ def test_image_loader_order_and_paths(dev, tmp_path):
     first = batches[0][0].cpu().numpy()
     ref = _pil_ref(np.asarray(Image.open(stim["10"]).convert("RGB")), 256, 224, DS_MEAN["imgnet"], DS_STD["imgnet"])
     assert np.array_equal(first[0], ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h,w", [(425, 425), (300, 500), (512, 256), (1000, 700), (64, 90)])
+def test_clip_and_dino_transforms_bit_exact_vs_pillow_bicubic(dev, h, w):
+    from visreps_amd.dataloaders.obj_cls import DS_MEAN, DS_STD, clip_transform, dino_transform
+    from visreps_amd.models.foundation import CLIP_MEAN, CLIP_STD
+
+    imgs = [_img(h, w, 40 + s) for s in range(2)]
+    got = clip_transform().batch(imgs).cpu().numpy()
+    for i, im in enumerate(imgs):
+        assert np.array_equal(got[i], _pil_ref(im, 224, 224, CLIP_MEAN, CLIP_STD, "bicubic"))
+    got = dino_transform().batch(imgs).cpu().numpy()
+    for i, im in enumerate(imgs):
+        assert np.array_equal(got[i], _pil_ref(im, 224, 224, DS_MEAN["imgnet"], DS_STD["imgnet"], "bicubic"))

@@ -122,10 +122,10 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _c_sz, _vp],
     ),
-    "vr_transform_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64, _c_i64]),
+    "vr_transform_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_int]),
     "vr_transform_u8": (
         ctypes.c_int,
-        [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_sz, _vp],
+        [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_int, _vp, _vp, _vp, _vp, _c_sz, _vp],
     ),
     "vr_rng_state_bytes": (_c_sz, []),
     "vr_rng_seed": (ctypes.c_int, [_vp, ctypes.c_uint32]),

@@ -3,8 +3,9 @@
 //   Resize(resize, BILINEAR) -> CenterCrop(crop) -> ToTensor -> Normalize(mean, std)
 // on PIL images. torchvision hands a PIL image to Pillow's Image.resize, so the arithmetic
 // to match is Pillow's ImagingResample (libImaging/Resample.c, Pillow 12):
-//   * per output index a window [xmin, xmin + xmax) of input pixels with bilinear weights
-//     tent((x + xmin - center + 0.5) / filterscale), center = (xx + 0.5) * scale,
+//   * per output index a window [xmin, xmin + xmax) of input pixels with filter weights
+//     f((x + xmin - center + 0.5) / filterscale) (f: Pillow's bilinear tent, or its bicubic
+//     kernel with a = -0.5 for the CLIP / timm loaders), center = (xx + 0.5) * scale,
 //     filterscale = max(scale, 1) (the support widens when downscaling: antialiasing),
 //     normalised to sum 1 in double, then rounded to 22-bit fixed point;
 //   * a horizontal pass into a uint8 intermediate, then a vertical pass, each output
@@ -31,6 +32,7 @@ namespace vr {
 constexpr int TF_PREC = 22;  // Pillow PRECISION_BITS = 32 - 8 - 2
 
 struct TfGeom {
+  int filter;          // 0 bilinear (support 1), 1 bicubic (support 2, a = -0.5)
   int64_t H, W;        // input
   int64_t nh, nw;      // resized
   int64_t crop, top, left;
@@ -40,15 +42,18 @@ struct TfGeom {
 
 static int64_t round_half_even(double v) { return (int64_t)std::nearbyint(v); }
 
-static int ksize_of(int64_t in, int64_t out) {
+static double filter_support(int filter) { return filter == 1 ? 2.0 : 1.0; }
+
+static int ksize_of(int64_t in, int64_t out, int filter) {
   double fs = (double)in / (double)out;
   if (fs < 1.0) fs = 1.0;
-  return (int)std::ceil(1.0 * fs) * 2 + 1;
+  return (int)std::ceil(filter_support(filter) * fs) * 2 + 1;
 }
 
 // torchvision _compute_resized_output_size (size = [resize], no max_size)
-static TfGeom tf_geom(int64_t H, int64_t W, int64_t resize, int64_t crop) {
+static TfGeom tf_geom(int64_t H, int64_t W, int64_t resize, int64_t crop, int filter) {
   TfGeom g;
+  g.filter = filter;
   g.H = H;
   g.W = W;
   const int64_t s = W <= H ? W : H, l = W <= H ? H : W;
@@ -58,8 +63,8 @@ static TfGeom tf_geom(int64_t H, int64_t W, int64_t resize, int64_t crop) {
   g.crop = crop;
   g.top = round_half_even((double)(g.nh - crop) / 2.0);
   g.left = round_half_even((double)(g.nw - crop) / 2.0);
-  g.kh = ksize_of(W, g.nw);
-  g.kv = ksize_of(H, g.nh);
+  g.kh = ksize_of(W, g.nw, filter);
+  g.kv = ksize_of(H, g.nh, filter);
   g.r0 = 0;
   g.nrows = 0;
   return g;
@@ -85,15 +90,28 @@ static TfWs tf_layout(void* base, int64_t B, const TfGeom& g, int64_t max_rows, 
   return w;
 }
 
-// Pillow precompute_coeffs + normalize_coeffs_8bpc for output indices [o0, o0 + n) of an
-// in -> out resize (box [0, in)). One thread per output index.
-__device__ void tf_coeff_one(int64_t in, int64_t out, int64_t xx, int ksize, int32_t* k,
+// Pillow's filters (Resample.c bilinear_filter, bicubic_filter with a = -0.5)
+__device__ inline double tf_filter(int filter, double x) {
+#pragma clang fp contract(off)
+  if (x < 0.0) x = -x;
+  if (filter == 1) {
+    const double a = -0.5;
+    if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+    if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+    return 0.0;
+  }
+  return x < 1.0 ? 1.0 - x : 0.0;
+}
+
+// Pillow precompute_coeffs + normalize_coeffs_8bpc for output index xx of an in -> out
+// resize (box [0, in)). One thread per output index.
+__device__ void tf_coeff_one(int filter, int64_t in, int64_t out, int64_t xx, int ksize, int32_t* k,
                              int32_t* bounds) {
 #pragma clang fp contract(off)
   const double scale = (double)(float)((float)in - 0.0f) / (double)out;
   double filterscale = scale;
   if (filterscale < 1.0) filterscale = 1.0;
-  const double support = 1.0 * filterscale;
+  const double support = (filter == 1 ? 2.0 : 1.0) * filterscale;
   const double center = 0.0 + ((double)xx + 0.5) * scale;
   const double ss = 1.0 / filterscale;
   int xmin = (int)(center - support + 0.5);
@@ -104,9 +122,7 @@ __device__ void tf_coeff_one(int64_t in, int64_t out, int64_t xx, int ksize, int
   double w[64];
   double ww = 0.0;
   for (int x = 0; x < xmax; ++x) {
-    double t = ((double)(x + xmin) - center + 0.5) * ss;
-    if (t < 0.0) t = -t;
-    const double v = t < 1.0 ? 1.0 - t : 0.0;
+    const double v = tf_filter(filter, ((double)(x + xmin) - center + 0.5) * ss);
     w[x] = v;
     ww += v;
   }
@@ -122,10 +138,10 @@ __device__ void tf_coeff_one(int64_t in, int64_t out, int64_t xx, int ksize, int
 
 __global__ void k_tf_coeffs(TfGeom g, TfWs w) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < g.crop) tf_coeff_one(g.W, g.nw, g.left + i, g.kh, w.kh + i * g.kh, w.bh + 2 * i);
+  if (i < g.crop) tf_coeff_one(g.filter, g.W, g.nw, g.left + i, g.kh, w.kh + i * g.kh, w.bh + 2 * i);
   else if (i < 2 * g.crop) {
     const int64_t j = i - g.crop;
-    tf_coeff_one(g.H, g.nh, g.top + j, g.kv, w.kv + j * g.kv, w.bv + 2 * j);
+    tf_coeff_one(g.filter, g.H, g.nh, g.top + j, g.kv, w.kv + j * g.kv, w.bv + 2 * j);
   }
 }
 
@@ -188,7 +204,7 @@ __global__ __launch_bounds__(256) void k_tf_vert(int64_t B, TfGeom g, TfWs w, Tf
 // the ones used)
 static void tf_rows(TfGeom& g) {
   const double scale = (double)g.H / (double)g.nh;
-  const double fs = scale < 1.0 ? 1.0 : scale;
+  const double fs = (scale < 1.0 ? 1.0 : scale) * filter_support(g.filter);
   auto lo = [&](int64_t yy) {
     const double c = ((double)yy + 0.5) * scale;
     int64_t m = (int64_t)(c - fs + 0.5);
@@ -211,9 +227,10 @@ using namespace vr;
 
 extern "C" {
 
-size_t vr_transform_workspace(int64_t B, int64_t H, int64_t W, int64_t resize, int64_t crop) {
-  if (B <= 0 || H <= 0 || W <= 0 || resize <= 0 || crop <= 0) return 0;
-  TfGeom g = tf_geom(H, W, resize, crop);
+size_t vr_transform_workspace(int64_t B, int64_t H, int64_t W, int64_t resize, int64_t crop,
+                              int filter) {
+  if (B <= 0 || H <= 0 || W <= 0 || resize <= 0 || crop <= 0 || filter < 0 || filter > 1) return 0;
+  TfGeom g = tf_geom(H, W, resize, crop, filter);
   tf_rows(g);
   size_t bytes = 0;
   tf_layout(nullptr, B, g, g.nrows, &bytes);
@@ -221,18 +238,19 @@ size_t vr_transform_workspace(int64_t B, int64_t H, int64_t W, int64_t resize, i
 }
 
 int vr_transform_u8(const uint8_t* src, int64_t B, int64_t H, int64_t W, int64_t resize,
-                    int64_t crop, const float* mean, const float* std, float* out, void* ws,
-                    size_t ws_bytes, void* stream) {
+                    int64_t crop, int filter, const float* mean, const float* std, float* out,
+                    void* ws, size_t ws_bytes, void* stream) {
+  VR_REQUIRE(filter == 0 || filter == 1, "vr_transform_u8: filter %d (0 bilinear, 1 bicubic)", filter);
   VR_REQUIRE(B >= 0 && H > 0 && W > 0 && resize > 0 && crop > 0,
              "vr_transform_u8: bad shape B=%lld H=%lld W=%lld resize=%lld crop=%lld", (long long)B,
              (long long)H, (long long)W, (long long)resize, (long long)crop);
   if (B == 0) return VR_OK;
   VR_REQUIRE(src && out && mean && std && ws, "vr_transform_u8: null pointer");
-  TfGeom g = tf_geom(H, W, resize, crop);
+  TfGeom g = tf_geom(H, W, resize, crop, filter);
   VR_REQUIRE(crop <= g.nh && crop <= g.nw,
              "vr_transform_u8: crop %lld larger than the resized image %lldx%lld (torchvision pads)",
              (long long)crop, (long long)g.nh, (long long)g.nw);
-  VR_REQUIRE(g.kh <= 64 && g.kv <= 64, "vr_transform_u8: downscale factor above 31 (W=%lld H=%lld)",
+  VR_REQUIRE(g.kh <= 64 && g.kv <= 64, "vr_transform_u8: downscale factor too large (W=%lld H=%lld)",
              (long long)W, (long long)H);
   tf_rows(g);
   size_t need = 0;

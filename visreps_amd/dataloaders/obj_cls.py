@@ -21,7 +21,8 @@ import torch
 
 from .._lib import check, lib, stream_of, workspace
 
-__all__ = ["DS_MEAN", "DS_STD", "get_transform", "DeviceTransform", "ImageLoader"]
+__all__ = ["DS_MEAN", "DS_STD", "get_transform", "clip_transform", "dino_transform",
+           "DeviceTransform", "ImageLoader"]
 
 DS_MEAN = {"tiny-imagenet": [0.480, 0.448, 0.398], "imgnet": [0.485, 0.456, 0.406]}
 DS_STD = {"tiny-imagenet": [0.272, 0.265, 0.274], "imgnet": [0.229, 0.224, 0.225]}
@@ -51,14 +52,19 @@ class DeviceTransform:
     """Resize(resize) -> CenterCrop(crop) -> ToTensor -> Normalize(mean, std) on the device;
     with preprocess=False only ToTensor (transforms.ToTensor(): HWC uint8 -> CHW / 255)."""
 
+    FILTERS = {"bilinear": 0, "bicubic": 1}
+
     def __init__(self, resize: int, crop: int, mean: Sequence[float], std: Sequence[float],
-                 preprocess: bool = True):
+                 preprocess: bool = True, interpolation: str = "bilinear"):
         self.resize, self.crop, self.preprocess = int(resize), int(crop), bool(preprocess)
+        if interpolation not in self.FILTERS:
+            raise ValueError(f"interpolation {interpolation!r}: bilinear or bicubic")
+        self.interpolation = interpolation
         self.mean = np.asarray(mean, dtype=np.float32)
         self.std = np.asarray(std, dtype=np.float32)
 
     def __repr__(self):
-        return (f"DeviceTransform(Resize({self.resize}, bilinear), CenterCrop({self.crop}), "
+        return (f"DeviceTransform(Resize({self.resize}, {self.interpolation}), CenterCrop({self.crop}), "
                 f"ToTensor, Normalize({self.mean.tolist()}, {self.std.tolist()}))")
 
     def __call__(self, img) -> torch.Tensor:
@@ -72,9 +78,10 @@ class DeviceTransform:
             return src.permute(0, 3, 1, 2).float().div(255)
         out = torch.empty((B, 3, self.crop, self.crop), dtype=torch.float32, device=dev)
         L = lib()
-        ws = workspace.get(dev, L.vr_transform_workspace(B, H, W, self.resize, self.crop), "transform")
+        f = self.FILTERS[self.interpolation]
+        ws = workspace.get(dev, L.vr_transform_workspace(B, H, W, self.resize, self.crop, f), "transform")
         with torch.cuda.device(dev):
-            check(L.vr_transform_u8(src.data_ptr(), B, H, W, self.resize, self.crop,
+            check(L.vr_transform_u8(src.data_ptr(), B, H, W, self.resize, self.crop, f,
                                     self.mean.ctypes.data, self.std.ctypes.data, out.data_ptr(),
                                     ws.data_ptr(), ws.numel(), stream_of(dev)), "vr_transform_u8")
         return out
@@ -108,6 +115,22 @@ def get_transform(ds_stats: str = "imgnet", data_augment: bool = False, image_si
         raise KeyError(ds_stats)
     resize, crop = (64, 64) if ds_stats == "tiny-imagenet" else (256, image_size)
     return DeviceTransform(resize, crop, DS_MEAN[ds_stats], DS_STD[ds_stats], preprocess)
+
+
+def clip_transform(n_px: int = 224) -> DeviceTransform:
+    """clip._transform(n_px) (clip.load's preprocess, clip_representations.py:27):
+    Resize(n_px, BICUBIC), CenterCrop(n_px), RGB, ToTensor, Normalize(CLIP stats)."""
+    from ..models.foundation import CLIP_MEAN, CLIP_STD
+
+    return DeviceTransform(n_px, n_px, CLIP_MEAN, CLIP_STD, interpolation="bicubic")
+
+
+def dino_transform(img_size: int = 224, crop_pct: float = 1.0) -> DeviceTransform:
+    """timm create_transform(**resolve_model_data_config(dinov3), is_training=False)
+    (dino_representations.py:31-32): Resize(int(img_size / crop_pct), BICUBIC),
+    CenterCrop(img_size), ImageNet stats. The data config is assumed (timm is absent)."""
+    return DeviceTransform(int(img_size / crop_pct), img_size, DS_MEAN["imgnet"], DS_STD["imgnet"],
+                           interpolation="bicubic")
 
 
 class ImageLoader:

@@ -8,6 +8,10 @@ ViT CLS token) -> row L2 normalisation -> concatenation in loader order -> one
   save_features      utils.py:72-78 (datasets/obj_cls/{dataset}/features_{model}.npz)
   alexnet_fc2        alexnet_representations.py:25-27,43-45 (classifier[:6], F.normalize)
   vit_cls            vit_representations.py:25,33-35 (forward_features(x)[:, 0], F.normalize)
+  clip_image         clip_representations.py:26-38 (encode_image / its norm; CLIP ViT-L/14)
+  dino_cls           dino_representations.py:24-38 (forward_features(x)[:, 0], F.normalize)
+                     (models/foundation.py; loaders' bicubic preprocessing:
+                     dataloaders/obj_cls.clip_transform / dino_transform)
 
 Pretrained weights need a download the reference makes (torchvision / timm / clip); here
 the models are the repo's own random-initialised AlexNet / ViT-B/16 unless a local
@@ -25,7 +29,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-__all__ = ["extract_features", "save_features", "load_features", "alexnet_fc2", "vit_cls"]
+__all__ = ["extract_features", "save_features", "load_features", "alexnet_fc2", "vit_cls",
+           "clip_image", "dino_cls"]
 
 
 def alexnet_fc2(model: nn.Module) -> Tuple[nn.Module, Callable]:
@@ -41,6 +46,27 @@ def alexnet_fc2(model: nn.Module) -> Tuple[nn.Module, Callable]:
 
 def vit_cls(model: nn.Module) -> Tuple[nn.Module, Callable]:
     """(model, extract_fn) with extract_fn = L2-normalised CLS token of forward_features."""
+
+    def extract_fn(m, x):
+        return F.normalize(m.forward_features(x)[:, 0, :], p=2, dim=-1)
+
+    return model, extract_fn
+
+
+def clip_image(model: nn.Module) -> Tuple[nn.Module, Callable]:
+    """(model, extract_fn) with extract_fn = encode_image(x) / ||encode_image(x)||
+    (clip_representations.py:37-39: features / features.norm(dim=-1, keepdim=True))."""
+
+    def extract_fn(m, x):
+        f = m.encode_image(x)
+        return f / f.norm(dim=-1, keepdim=True)
+
+    return model, extract_fn
+
+
+def dino_cls(model: nn.Module) -> Tuple[nn.Module, Callable]:
+    """(model, extract_fn) with extract_fn = L2-normalised CLS of forward_features
+    (dino_representations.py:35-37)."""
 
     def extract_fn(m, x):
         return F.normalize(m.forward_features(x)[:, 0, :], p=2, dim=-1)
