@@ -224,6 +224,31 @@ int vr_srp_csr_f32(const int32_t* indptr, const int32_t* indices, const float* v
                    int64_t ldo, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------
+ * Multi-GPU RDM pieces (stimulus-sharded rows); replace the
+ * block-distributed use of vr_rdm_pearson_tiles_f32 + a sum all-reduce:
+ *  - each rank splits its own rows (row stats + centred bf16 hi/lo plane records);
+ *  - the planes and stats are all-gathered (the only feature exchange);
+ *  - each rank computes its tile range from the gathered planes;
+ *  - the ranges are exchanged packed (vr_rdm_tiles_pack -> all-gather -> unpack, which
+ *    also writes the mirror), instead of a zero-filled n x n sum all-reduce.
+ * Plane buffers hold vr_rdm_plane_rows(n) rows of vr_rdm_plane_row_bytes(d) bytes, rows
+ * >= n zero. A packed tile range holds 128 x 128 floats per tile, in tile order.
+ * -------------------------------------------------------------------------- */
+int64_t vr_rdm_plane_rows(int64_t n);
+size_t vr_rdm_plane_row_bytes(int64_t d);
+int vr_rdm_split_rows_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, float correction,
+                          float* mean, float* stdv, uint16_t* planes, void* stream);
+size_t vr_rdm_planes_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end);
+int vr_rdm_pearson_tiles_planes(const uint16_t* planes, const float* mean, const float* stdv,
+                                int64_t n, int64_t d, float* rdm, int64_t ldr, float correction,
+                                int64_t tile_begin, int64_t tile_end, void* ws, size_t ws_bytes,
+                                void* stream);
+int vr_rdm_tiles_pack(const float* rdm, int64_t ldr, int64_t n, int64_t tile_begin,
+                      int64_t tile_end, float* packed, void* stream);
+int vr_rdm_tiles_unpack(const float* packed, int64_t n, int64_t tile_begin, int64_t tile_end,
+                        float* rdm, int64_t ldr, void* stream);
+
+/* ------------------------------------------------------------------------------
  * Image preprocessing: the eval loaders' get_transform (visreps/dataloaders/obj_cls.py:
  * 27-45) = torchvision Resize(resize, BILINEAR) on a PIL image (Pillow's ImagingResample:
  * antialiased separable bilinear, 22-bit fixed point, uint8 intermediate) ->

@@ -122,6 +122,17 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _c_sz, _vp],
     ),
+    "vr_rdm_plane_rows": (_c_i64, [_c_i64]),
+    "vr_rdm_plane_row_bytes": (_c_sz, [_c_i64]),
+    "vr_rdm_split_rows_f32": (
+        ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, ctypes.c_float, _vp, _vp, _vp, _vp]),
+    "vr_rdm_planes_tiles_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64]),
+    "vr_rdm_pearson_tiles_planes": (
+        ctypes.c_int,
+        [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _c_i64, _c_i64, _vp, _c_sz, _vp],
+    ),
+    "vr_rdm_tiles_pack": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _vp]),
+    "vr_rdm_tiles_unpack": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp]),
     "vr_transform_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_int]),
     "vr_transform_u8": (
         ctypes.c_int,

@@ -944,7 +944,8 @@ static size_t gram_fbuf_floats() {
 }
 
 static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* base, float** mean,
-                      float** stdv, float** partial, uint16_t** planes, float** fbuf = nullptr) {
+                      float** stdv, float** partial, uint16_t** planes, float** fbuf = nullptr,
+                      bool own_planes = true) {
   const int64_t T = (n + GT - 1) / GT;
   const int R = gram_wide_rows(n, d, count, split3);
   const int64_t rest = R > 0 ? count - tri_start(2 * (int64_t)R, T) : count;
@@ -954,7 +955,8 @@ static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* ba
   float* s = c.take<float>((size_t)n);
   float* p = part ? c.take<float>(part) : nullptr;
   const int64_t prow = (n + WT - 1) / WT * WT;
-  uint16_t* pl = split3 ? c.take<uint16_t>((size_t)prow * (size_t)((d + GK - 1) / GK) * 64) : nullptr;
+  uint16_t* pl = split3 && own_planes ? c.take<uint16_t>((size_t)prow * (size_t)((d + GK - 1) / GK) * 64)
+                                      : nullptr;
   const bool flush = gram_flush_stages() > 0 && (d + GK - 1) / GK > gram_flush_stages();
   float* fb = flush ? c.take<float>(gram_fbuf_floats()) : nullptr;
   if (fbuf) *fbuf = fb;
@@ -1036,9 +1038,18 @@ static int row_stats_bf16(const uint16_t* X, int64_t n, int64_t d, int64_t ldx, 
 
 // bf16 input always takes the split kernel: only the row statistics and the split prepass
 // read X, so no fp32 copy of the features is ever made (the exact-fp32 kernel stages X).
+// Precomputed split rows (the multi-GPU path: each rank splits its own stimulus rows and
+// the planes + row statistics are all-gathered): the launch skips its prepass.
+struct PreSplit {
+  const uint16_t* planes = nullptr;  // [vr_rdm_plane_rows(n)][nstage][64], rows >= n zero
+  const float* mean = nullptr;       // [n]
+  const float* stdv = nullptr;       // [n]
+};
+
 static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* rdm, int64_t ldr,
                       float correction, int64_t tile_begin, int64_t tile_end, void* ws,
-                      size_t ws_bytes, void* stream, size_t need, bool raw = false, bool bf16 = false) {
+                      size_t ws_bytes, void* stream, size_t need, bool raw = false, bool bf16 = false,
+                      const PreSplit& pre = PreSplit{}) {
   const float* X = static_cast<const float*>(Xv);
   if (ws_bytes < need || ws == nullptr) {
     set_error("vr_rdm_pearson: workspace %zu < %zu", ws_bytes, need);
@@ -1047,13 +1058,19 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   hipStream_t st = as_stream(stream);
   GramParams P{};
   gram_geometry(n, d, tile_end - tile_begin, P.T, P.ntiles, P.splits, P.kslice);
-  const bool split3 = bf16 || gram_split(n, d);
+  const bool split3 = bf16 || pre.planes || gram_split(n, d);
   float *mean, *stdv;
   uint16_t* planes;
-  gram_ws(n, d, tile_end - tile_begin, split3, ws, &mean, &stdv, &P.partial, &planes, &P.fbuf);
+  gram_ws(n, d, tile_end - tile_begin, split3, ws, &mean, &stdv, &P.partial, &planes, &P.fbuf,
+          pre.planes == nullptr);
   const int flush_stages = P.fbuf ? gram_flush_stages() : 0;
   P.raw = raw ? 1 : 0;
-  if (raw) {  // zero means: the panels stage X itself
+  if (pre.planes) {
+    mean = const_cast<float*>(pre.mean);
+    stdv = const_cast<float*>(pre.stdv);
+    P.planes = pre.planes;
+    P.nstage = (d + GK - 1) / GK;
+  } else if (raw) {  // zero means: the panels stage X itself
     VR_CHECK_HIP(hipMemsetAsync(mean, 0, (size_t)n * sizeof(float), st));
     VR_CHECK_HIP(hipMemsetAsync(stdv, 0, (size_t)n * sizeof(float), st));
   } else if (bf16) {
@@ -1061,7 +1078,7 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   } else {
     VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
   }
-  if (split3) {
+  if (split3 && !pre.planes) {
     const int64_t rows = (n + WT - 1) / WT * WT, nstage = (d + GK - 1) / GK;
     const int64_t threads = rows * nstage * 8;
     if (bf16)
@@ -1083,7 +1100,7 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   P.ldx = ldx;
   P.ldr = ldr;
   P.correction = correction;
-  P.vec = ((reinterpret_cast<uintptr_t>(Xv) & 15) == 0) && ((ldx & 3) == 0) &&
+  P.vec = (pre.planes || (((reinterpret_cast<uintptr_t>(Xv) & 15) == 0) && ((ldx & 3) == 0))) &&
           ((reinterpret_cast<uintptr_t>(rdm) & 15) == 0);
   // tile range [t0, t0 + count): its own split-K geometry, generations, reduction
   auto run_range = [&](int64_t t0, int64_t count, bool fit) -> int {
@@ -1202,6 +1219,123 @@ int vr_gram_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* G, int
   VR_REQUIRE(n <= (1 << 20), "vr_gram_f32: n=%lld too large", (long long)n);
   return rdm_launch(X, n, d, ldx, G, ldg, 0.f, 0, gram_tiles(n), ws, ws_bytes, stream,
                     vr_rdm_pearson_workspace(n, d), true);
+}
+
+
+// ---------------------------------------------------------------------------------
+// Multi-GPU pieces: split rows locally, Gram tiles from gathered planes, tile exchange
+// ---------------------------------------------------------------------------------
+int64_t vr_rdm_plane_rows(int64_t n) { return n > 0 ? (n + WT - 1) / WT * WT : 0; }
+
+size_t vr_rdm_plane_row_bytes(int64_t d) {
+  return d > 0 ? (size_t)((d + GK - 1) / GK) * 64 * sizeof(uint16_t) : 0;
+}
+
+int vr_rdm_split_rows_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, float correction,
+                          float* mean, float* stdv, uint16_t* planes, void* stream) {
+  VR_REQUIRE(rows >= 0 && d > 0 && ldx >= d, "vr_rdm_split_rows_f32: bad shape rows=%lld d=%lld",
+             (long long)rows, (long long)d);
+  if (rows == 0) return VR_OK;
+  VR_REQUIRE(X && mean && stdv && planes, "vr_rdm_split_rows_f32: null pointer");
+  VR_TRY(vr_row_stats_f32(X, rows, d, ldx, mean, stdv, correction, stream));
+  const int64_t nstage = (d + GK - 1) / GK, threads = rows * nstage * 8;
+  k_split3<float><<<(unsigned)((threads + 255) / 256), 256, 0, as_stream(stream)>>>(
+      X, rows, d, ldx, mean, rows, nstage, planes);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+size_t vr_rdm_planes_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
+  if (n <= 0 || d <= 0 || tile_end <= tile_begin) return 256;
+  return gram_ws(n, d, tile_end - tile_begin, true, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                 false);
+}
+
+int vr_rdm_pearson_tiles_planes(const uint16_t* planes, const float* mean, const float* stdv,
+                                int64_t n, int64_t d, float* rdm, int64_t ldr, float correction,
+                                int64_t tile_begin, int64_t tile_end, void* ws, size_t ws_bytes,
+                                void* stream) {
+  VR_REQUIRE(n >= 0 && d > 0 && ldr >= n, "vr_rdm_pearson_tiles_planes: bad shape n=%lld d=%lld",
+             (long long)n, (long long)d);
+  VR_REQUIRE(n <= (1 << 20), "vr_rdm_pearson_tiles_planes: n too large");
+  if (n == 0 || tile_end <= tile_begin) return VR_OK;
+  VR_REQUIRE(tile_begin >= 0 && tile_end <= gram_tiles(n), "vr_rdm_pearson_tiles_planes: tiles [%lld, %lld)",
+             (long long)tile_begin, (long long)tile_end);
+  VR_REQUIRE(planes && mean && stdv && rdm, "vr_rdm_pearson_tiles_planes: null pointer");
+  PreSplit pre;
+  pre.planes = planes;
+  pre.mean = mean;
+  pre.stdv = stdv;
+  return rdm_launch(planes, n, d, (d + 3) / 4 * 4, rdm, ldr, correction, tile_begin, tile_end, ws,
+                    ws_bytes, stream, vr_rdm_planes_tiles_workspace(n, d, tile_begin, tile_end),
+                    false, false, pre);
+}
+
+}  // extern "C"
+
+namespace vr {
+// tile index -> (block row, block col) of the upper-triangle tile list (GT tiles)
+__device__ inline void tile_rc(int64_t T, int64_t p, int64_t& bi, int64_t& bj) {
+  // r = largest row with tri_start(r, T) <= p
+  double disc = (2.0 * T + 1) * (2.0 * T + 1) - 8.0 * (double)p;
+  int64_t r = (int64_t)(((2.0 * T + 1) - sqrt(disc)) / 2.0);
+  if (r < 0) r = 0;
+  while (r > 0 && r * T - r * (r - 1) / 2 > p) --r;
+  while ((r + 1) * T - (r + 1) * r / 2 <= p) ++r;
+  bi = r;
+  bj = r + (p - (r * T - r * (r - 1) / 2));
+}
+
+// packed[(t - t0) * GT * GT + i * GT + j] <-> rdm[(row0 + i) * ldr + col0 + j]
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_tiles_move(float* __restrict__ rdm, int64_t ldr, int64_t n,
+                                                    int64_t t0, float* __restrict__ packed) {
+  const int64_t T = (n + GT - 1) / GT;
+  int64_t bi, bj;
+  tile_rc(T, t0 + blockIdx.x, bi, bj);
+  const int64_t r0 = bi * GT, c0 = bj * GT;
+  const int64_t h = n - r0 < GT ? n - r0 : GT, w = n - c0 < GT ? n - c0 : GT;
+  float* pk = packed + (size_t)blockIdx.x * GT * GT;
+  for (int e = threadIdx.x; e < GT * GT; e += blockDim.x) {
+    const int i = e / GT, j = e % GT;
+    if (i >= h || j >= w) continue;
+    float* dst = rdm + (size_t)(r0 + i) * ldr + c0 + j;
+    if (PACK) {
+      pk[e] = *dst;
+    } else {
+      *dst = pk[e];
+      rdm[(size_t)(c0 + j) * ldr + r0 + i] = pk[e];  // mirror (diagonal tiles: itself)
+    }
+  }
+}
+}  // namespace vr
+
+extern "C" {
+
+int vr_rdm_tiles_pack(const float* rdm, int64_t ldr, int64_t n, int64_t tile_begin, int64_t tile_end,
+                      float* packed, void* stream) {
+  VR_REQUIRE(n > 0 && ldr >= n && tile_begin >= 0 && tile_end <= gram_tiles(n),
+             "vr_rdm_tiles_pack: bad range n=%lld [%lld, %lld)", (long long)n, (long long)tile_begin,
+             (long long)tile_end);
+  if (tile_end <= tile_begin) return VR_OK;
+  VR_REQUIRE(rdm && packed, "vr_rdm_tiles_pack: null pointer");
+  k_tiles_move<true><<<(unsigned)(tile_end - tile_begin), 256, 0, as_stream(stream)>>>(
+      const_cast<float*>(rdm), ldr, n, tile_begin, packed);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+int vr_rdm_tiles_unpack(const float* packed, int64_t n, int64_t tile_begin, int64_t tile_end, float* rdm,
+                        int64_t ldr, void* stream) {
+  VR_REQUIRE(n > 0 && ldr >= n && tile_begin >= 0 && tile_end <= gram_tiles(n),
+             "vr_rdm_tiles_unpack: bad range n=%lld [%lld, %lld)", (long long)n, (long long)tile_begin,
+             (long long)tile_end);
+  if (tile_end <= tile_begin) return VR_OK;
+  VR_REQUIRE(rdm && packed, "vr_rdm_tiles_unpack: null pointer");
+  k_tiles_move<false><<<(unsigned)(tile_end - tile_begin), 256, 0, as_stream(stream)>>>(
+      rdm, ldr, n, tile_begin, const_cast<float*>(packed));
+  VR_CHECK_LAUNCH();
+  return VR_OK;
 }
 
 }  // extern "C"

@@ -4,10 +4,11 @@ multi-GPU path of the eval driver).
 Per step (BASELINE.json configs[1]: CustomCNN points x NSD ROIs, N stimuli, 1000 boots):
   1. extraction   each rank forwards its stimulus shard; the 14 hooked points are
                   flattened into per-point (n_local, D) HBM buffers;
-  2. RDMs         per point / ROI: RCCL all-gather of the feature rows (the one
-                  data-path exchange), each rank computes a cost-balanced range of the
-                  128x128 upper-triangle Gram tiles into a zeroed RDM, and a sum
-                  all-reduce assembles the RDM on every rank;
+  2. RDMs         per point / ROI: each rank splits its own rows (row statistics +
+                  centred bf16 hi/lo planes), RCCL all-gathers the planes (the one
+                  feature exchange), computes a cost-balanced range of the 128x128
+                  upper-triangle Gram tiles, and the packed tile ranges are all-gathered
+                  and unpacked (with their mirrors) into every rank's RDM;
   3. rank plans   each rank sorts the triangles of the RDMs its units use;
   4. units        (point, ROI) units listed ROI-major, one contiguous range per rank; a
                   rank's units sharing a ROI are one engine call (vr_bootstrap_spearman_multi:
@@ -135,101 +136,230 @@ def _gram_flops(n: int, d: int) -> float:
     return float(n) * (n + 1) * d
 
 
+def _gram_exact_fp32() -> bool:
+    import os
+
+    return os.environ.get("VISREPS_GRAM") == "fp32"
+
+
+class RdmKernels:
+    """The HIP entry points of the distributed RDM (csrc/rdm.hip). The orchestration below
+    calls nothing else on the device, so the gloo tests substitute a CPU emulation of
+    exactly these five calls and run the orchestration itself unchanged."""
+
+    @staticmethod
+    def plane_rows(n: int) -> int:
+        return int(lib().vr_rdm_plane_rows(n))
+
+    @staticmethod
+    def plane_elems(d: int) -> int:  # uint16 elements per row of plane records
+        return int(lib().vr_rdm_plane_row_bytes(d)) // 2
+
+    @staticmethod
+    def split_rows(x: torch.Tensor, correction: float):
+        """(planes (rows, plane_elems) int16, mean (rows,), std (rows,)) of local rows."""
+        rows, d = x.shape
+        planes = torch.empty((rows, RdmKernels.plane_elems(d)), dtype=torch.int16, device=x.device)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        std = torch.empty(rows, dtype=torch.float32, device=x.device)
+        if rows:
+            check(lib().vr_rdm_split_rows_f32(x.data_ptr(), rows, d, x.stride(0), float(correction),
+                                              mean.data_ptr(), std.data_ptr(), planes.data_ptr(),
+                                              stream_of(x.device)), "vr_rdm_split_rows_f32")
+        return planes, mean, std
+
+    @staticmethod
+    def tiles_from_planes(planes, mean, std, n: int, d: int, out: torch.Tensor, t0: int, t1: int,
+                          correction: float, times: Optional[StepTimes] = None) -> None:
+        if t1 <= t0:
+            return
+        L = lib()
+        ws = workspace.get(out.device, L.vr_rdm_planes_tiles_workspace(n, d, t0, t1), "rdm")
+        ev = None
+        if times is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        check(L.vr_rdm_pearson_tiles_planes(planes.data_ptr(), mean.data_ptr(), std.data_ptr(), n, d,
+                                            out.data_ptr(), n, float(correction), t0, t1, ws.data_ptr(),
+                                            ws.numel(), stream_of(out.device)), "vr_rdm_pearson_tiles_planes")
+        if times is not None:
+            ev[1].record()
+            times.record("gram", ev[0], ev[1], _gram_flops(n, d) * _tile_fraction(n, t0, t1))
+
+    @staticmethod
+    def pack(out: torch.Tensor, n: int, t0: int, t1: int, packed: torch.Tensor) -> None:
+        check(lib().vr_rdm_tiles_pack(out.data_ptr(), n, n, t0, t1, packed.data_ptr(),
+                                      stream_of(out.device)), "vr_rdm_tiles_pack")
+
+    @staticmethod
+    def unpack(packed: torch.Tensor, n: int, t0: int, t1: int, out: torch.Tensor) -> None:
+        check(lib().vr_rdm_tiles_unpack(packed.data_ptr(), n, t0, t1, out.data_ptr(), n,
+                                        stream_of(out.device)), "vr_rdm_tiles_unpack")
+
+    @staticmethod
+    def tiles_from_rows(x, out, t0, t1, correction, times=None) -> None:
+        rdm_tiles_into(x, out, t0, t1, correction, times)
+
+
+KERNELS = RdmKernels()
+TILE = 128  # floats per packed tile edge (csrc/rdm.hip GT)
+
+
+def _all_gather_padded(t: torch.Tensor, sizes: Sequence[int], pg, async_op: bool = False):
+    """All-gather of a rank-local (sizes[rank], ...) tensor, padded to max(sizes) rows;
+    returns (work, buffer (world * per, ...), send buffer)."""
+    world = len(sizes)
+    per = max(sizes)
+    send = torch.zeros((per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    send[: t.size(0)] = t
+    full = torch.empty((world * per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    if dist.get_backend(pg) == "nccl":
+        work = dist.all_gather_into_tensor(full, send, group=pg, async_op=async_op)
+    else:  # gloo: the CPU tests of the orchestration
+        work = dist.all_gather(list(full.chunk(world)), send, group=pg, async_op=async_op)
+    return work, full, send
+
+
+def _compact(full: torch.Tensor, sizes: Sequence[int], rows_out: int) -> torch.Tensor:
+    """Rows of every rank's slot of a padded gather, in rank order, into (rows_out, ...)
+    with zero rows after the last real one."""
+    per = max(sizes)
+    out = torch.zeros((rows_out,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
+    at = 0
+    for r, sz in enumerate(sizes):
+        out[at:at + sz] = full[r * per: r * per + sz]
+        at += sz
+    return out
+
+
+class _Gathered:
+    """The exchanged rows of one point, ready for the rank's tile range."""
+
+    def __init__(self, kind: str, n: int, d: int, **parts):
+        self.kind, self.n, self.d, self.parts = kind, n, d, parts
+
+
+def gather_point_async(x_local: torch.Tensor, n: int, pg, correction: float = 1e-12,
+                       kernels: RdmKernels = None):
+    """Start one point's feature exchange; returns finish() -> _Gathered.
+
+    Split path (default): the rank splits its OWN rows (row statistics + centred bf16
+    hi/lo plane records, vr_rdm_split_rows_f32) and the planes and statistics are
+    all-gathered, so no rank recomputes another rank's prepass. Exact-fp32 Gram
+    (VISREPS_GRAM=fp32): the fp32 rows themselves. The collective runs on the
+    communicator's stream, so work already queued on the compute stream overlaps it."""
+    K = kernels or KERNELS
+    rank, world = _world(pg)
+    x_local = x_local.float().contiguous()
+    d = x_local.size(1)
+    sizes = [len(shard_rows(n, r, world)) for r in range(world)]
+    if _gram_exact_fp32():
+        work, full, send = _all_gather_padded(x_local, sizes, pg, async_op=True)
+
+        def finish_rows(_keep=send) -> _Gathered:
+            work.wait()
+            return _Gathered("rows", n, d, x=_compact(full, sizes, n))
+
+        return finish_rows
+    planes, mean, std = K.split_rows(x_local, correction)
+    stats = torch.stack([mean, std], dim=1)
+    # plane records travel as bytes (RCCL and gloo have no 16-bit integer type)
+    w1, pfull, s1 = _all_gather_padded(planes.view(torch.uint8), sizes, pg, async_op=True)
+    w2, sfull, s2 = _all_gather_padded(stats, sizes, pg, async_op=True)
+
+    def finish_planes(_keep=(s1, s2)) -> _Gathered:
+        w1.wait()
+        w2.wait()
+        st = _compact(sfull, sizes, n)
+        return _Gathered("planes", n, d, planes=_compact(pfull, sizes, K.plane_rows(n)).view(torch.int16),
+                         mean=st[:, 0].contiguous(), std=st[:, 1].contiguous())
+
+    return finish_planes
+
+
+def rdm_from_gathered(g: _Gathered, pg, times: Optional[StepTimes] = None, correction: float = 1e-12,
+                      kernels: RdmKernels = None) -> torch.Tensor:
+    """Every rank computes its balanced tile range (tile_ranges) into the (n, n) RDM, packs
+    it (128 x 128 floats per tile), and the packed ranges are all-gathered and unpacked
+    (tile + mirror) into every rank's RDM. Every entry is written by exactly one rank's
+    tile, so there is no zero fill and no sum: each rank receives about n^2/2 floats
+    instead of the 2 n^2 a ring sum all-reduce of the full matrix moves."""
+    K = kernels or KERNELS
+    rank, world = _world(pg)
+    n = g.n
+    dev = g.parts["planes"].device if g.kind == "planes" else g.parts["x"].device
+    out = torch.empty((n, n), dtype=torch.float32, device=dev)
+    ranges = tile_ranges(n, world) if world > 1 else [(0, int(lib().vr_rdm_tile_count(n)))]
+    t0, t1 = ranges[rank]
+    if g.kind == "planes":
+        K.tiles_from_planes(g.parts["planes"], g.parts["mean"], g.parts["std"], n, g.d, out, t0, t1,
+                            correction, times)
+    else:
+        K.tiles_from_rows(g.parts["x"], out, t0, t1, correction, times)
+    if world == 1:
+        return out
+    counts = [b - a for a, b in ranges]
+    packed = torch.empty((t1 - t0, TILE * TILE), dtype=torch.float32, device=dev)
+    if t1 > t0:
+        K.pack(out, n, t0, t1, packed)
+    _, allp, _keep = _all_gather_padded(packed, counts, pg)
+    per = max(counts)
+    for r, (a, b) in enumerate(ranges):
+        if r != rank and b > a:
+            K.unpack(allp[r * per: r * per + (b - a)], n, a, b, out)
+    return out
+
+
 def gather_rows(x_local: torch.Tensor, n: int, pg) -> torch.Tensor:
     """RCCL all-gather of every rank's stimulus rows into the full (n, d) matrix."""
     rank, world = _world(pg)
     if world == 1:
         return x_local
     sizes = [len(shard_rows(n, r, world)) for r in range(world)]
-    per = max(sizes)
-    d = x_local.size(1)
-    buf = torch.zeros((per, d), dtype=x_local.dtype, device=x_local.device)
-    buf[: x_local.size(0)] = x_local
-    full = torch.empty((world * per, d), dtype=x_local.dtype, device=x_local.device)
-    if dist.get_backend(pg) == "nccl":
-        dist.all_gather_into_tensor(full, buf, group=pg)
-    else:  # gloo (CPU tests of the orchestration)
-        dist.all_gather(list(full.chunk(world)), buf, group=pg)
-    if all(s == per for s in sizes):
-        return full
-    return torch.cat([full[r * per: r * per + sizes[r]] for r in range(world)], 0)
-
-
-def gather_rows_async(x_local: torch.Tensor, n: int, pg):
-    """Start the all-gather of gather_rows; returns a finish() -> (n, d) callable. The
-    collective runs on the communicator's stream, so work queued meanwhile on the
-    compute stream (the previous point's Gram) overlaps it."""
-    rank, world = _world(pg)
-    x_local = x_local.float().contiguous()
-    if world == 1:
-        return lambda: x_local
-    sizes = [len(shard_rows(n, r, world)) for r in range(world)]
-    per = max(sizes)
-    d = x_local.size(1)
-    buf = torch.zeros((per, d), dtype=x_local.dtype, device=x_local.device)
-    buf[: x_local.size(0)] = x_local
-    full = torch.empty((world * per, d), dtype=x_local.dtype, device=x_local.device)
-    if dist.get_backend(pg) == "nccl":
-        work = dist.all_gather_into_tensor(full, buf, group=pg, async_op=True)
-    else:  # gloo (CPU tests of the orchestration)
-        work = dist.all_gather(list(full.chunk(world)), buf, group=pg, async_op=True)
-
-    def finish(_send=buf) -> torch.Tensor:  # _send keeps the source buffer alive until here
-        work.wait()  # the compute stream waits for the gather
-        if all(sz == per for sz in sizes):
-            return full
-        return torch.cat([full[r * per: r * per + sizes[r]] for r in range(world)], 0)
-
-    return finish
-
-
-def _rdm_from_rows(x: torch.Tensor, n: int, pg, times, tiles_into) -> torch.Tensor:
-    rank, world = _world(pg)
-    if world == 1:
-        out = torch.empty((n, n), dtype=torch.float32, device=x.device)
-        tiles_into(x, out, 0, int(lib().vr_rdm_tile_count(n)), times=times)
-        return out
-    out = torch.zeros((n, n), dtype=torch.float32, device=x.device)
-    t0, t1 = tile_ranges(n, world)[rank]
-    tiles_into(x, out, t0, t1, times=times)
-    dist.all_reduce(out, op=dist.ReduceOp.SUM, group=pg)
-    return out
+    work, full, _keep = _all_gather_padded(x_local, sizes, pg)
+    return _compact(full, sizes, n)
 
 
 class PrefetchedRDMs:
     """RDM source for all_units_rsa over stimulus-sharded features: asking for point
-    points[i] first starts the all-gather of points[i + 1], so the exchange of the next
-    point's rows overlaps this point's Gram. Every rank asks for the points in the same
-    order (all_units_rsa walks `points`), so the collectives are issued in one order."""
+    points[i] first starts the exchange of points[i + 1] (gather_point_async), so the next
+    point's plane all-gather overlaps this point's Gram. Every rank asks for the points in
+    the same order (all_units_rsa walks `points`), so the collectives are issued in one
+    order."""
 
     def __init__(self, feats: Dict[str, torch.Tensor], points: Sequence[str], n: int, pg=None,
-                 times: Optional[StepTimes] = None, tiles_into=None):
+                 times: Optional[StepTimes] = None, kernels: RdmKernels = None):
         self.feats, self.points, self.n, self.pg, self.times = feats, list(points), n, pg, times
-        self.tiles_into = tiles_into or rdm_tiles_into
-        self.pending: Dict[str, Callable[[], torch.Tensor]] = {}
+        self.kernels = kernels or KERNELS
+        self.pending: Dict[str, Callable[[], _Gathered]] = {}
 
     def _start(self, p: str) -> None:
         if p not in self.pending:
-            self.pending[p] = gather_rows_async(self.feats[p], self.n, self.pg)
+            self.pending[p] = gather_point_async(self.feats[p], self.n, self.pg, kernels=self.kernels)
 
     def __call__(self, p: str) -> torch.Tensor:
+        if _world(self.pg)[1] == 1:  # one GPU: the single-launch RDM (no exchange, no prepass split)
+            return distributed_rdm(self.feats[p], self.n, None, self.times)
         self._start(p)
         i = self.points.index(p)
         if i + 1 < len(self.points):
             self._start(self.points[i + 1])
-        x = self.pending.pop(p)()
-        return _rdm_from_rows(x, self.n, self.pg, self.times, self.tiles_into)
+        g = self.pending.pop(p)()
+        return rdm_from_gathered(g, self.pg, self.times, kernels=self.kernels)
 
 
-def distributed_rdm(x_local: torch.Tensor, n: int, pg=None,
-                    times: Optional[StepTimes] = None, tiles_into=None) -> torch.Tensor:
-    """Full (n, n) RDM on every rank from each rank's stimulus rows: all-gather the rows,
-    each rank writes its balanced tile range (and mirrors) into a zeroed matrix, and a
-    sum all-reduce assembles it (every entry has exactly one writer, so the sum is exact).
-    tiles_into(x, out, t0, t1, times=...) defaults to the HIP Gram kernel."""
-    tiles_into = tiles_into or rdm_tiles_into
-    x = gather_rows(x_local.float().contiguous(), n, pg)
-    return _rdm_from_rows(x, n, pg, times, tiles_into)
+def distributed_rdm(x_local: torch.Tensor, n: int, pg=None, times: Optional[StepTimes] = None,
+                    kernels: RdmKernels = None) -> torch.Tensor:
+    """Full (n, n) RDM on every rank from each rank's stimulus rows (gather_point_async +
+    rdm_from_gathered). One GPU: the single-launch RDM of the local rows."""
+    rank, world = _world(pg)
+    if world == 1:
+        x = x_local.float().contiguous()
+        out = torch.empty((n, n), dtype=torch.float32, device=x.device)
+        rdm_tiles_into(x, out, 0, int(lib().vr_rdm_tile_count(n)), times=times)
+        return out
+    g = gather_point_async(x_local, n, pg, kernels=kernels)()
+    return rdm_from_gathered(g, pg, times, kernels=kernels)
 
 
 # ---------------------------------------------------------------------------------------
