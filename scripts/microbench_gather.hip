@@ -23,6 +23,34 @@
     }                                                                  \
   } while (0)
 
+// 128 subsets per pass: one u32 (two u16 subsets) per lane of a 256-B TB row and one u64
+// (two u32 subsets) per lane of a 512-B chunk-base row
+template <int NB>
+__global__ __launch_bounds__(1024) void gather2(const uint32_t* __restrict__ tb, const uint32_t* __restrict__ perm,
+                                                const uint2* __restrict__ base, uint32_t nbase,
+                                                uint32_t rows, uint32_t per_wave, uint32_t* out) {
+  const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t r0 = wave * per_wave;
+  uint32_t acc = 0;
+  for (uint32_t r = r0; r < r0 + per_wave; r += 64) {
+    const uint32_t pr = (r + lane < rows) ? perm[r + lane] : 0u;
+#pragma unroll
+    for (int h = 0; h < 64; h += NB) {
+      uint32_t v[NB];
+      uint2 b[NB];
+#pragma unroll
+      for (int t = 0; t < NB; ++t) {
+        const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)pr, h + t);
+        v[t] = tb[(size_t)row * 64 + lane];
+        b[t] = base[(size_t)(row % nbase) * 64 + lane];
+      }
+#pragma unroll
+      for (int t = 0; t < NB; ++t) acc += (v[t] & 0xffff) + (v[t] >> 16) + b[t].x + b[t].y;
+    }
+  }
+  out[wave * 64 + lane] = acc;
+}
+
 template <typename T, int NB, bool BASE>
 __global__ __launch_bounds__(1024) void gather(const T* __restrict__ tb, const uint32_t* __restrict__ perm,
                                                const uint32_t* __restrict__ base, uint32_t nbase,
@@ -67,7 +95,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&perm, (size_t)pairs * 4));
   CK(hipMalloc(&out, (size_t)waves * 64 * 4));
   const uint32_t nbase = 8138;  // 2 MB of 256-B base rows (round-1 chunk table at N=10k)
-  CK(hipMalloc(&base, (size_t)nbase * 256));
+  CK(hipMalloc(&base, (size_t)nbase * 512));
   fill<uint32_t><<<4096, 256>>>((uint32_t*)tb, max_bytes / 4);
   fill<uint32_t><<<64, 256>>>(base, (size_t)nbase * 64);
   hipEvent_t a, b;
@@ -113,6 +141,9 @@ int main(int argc, char** argv) {
   run("g32 NB8", 256, [&] { gather<uint32_t, 8, false><<<grid, 1024>>>((uint32_t*)tb, perm, base, nbase, pairs, per, out); });
   run("g32 NB16", 256, [&] { gather<uint32_t, 16, false><<<grid, 1024>>>((uint32_t*)tb, perm, base, nbase, pairs, per, out); });
   run("g32+base NB8", 256, [&] { gather<uint32_t, 8, true><<<grid, 1024>>>((uint32_t*)tb, perm, base, nbase, pairs, per, out); });
+  run("g32x2+base64 NB8 (4 MB base)", 256, [&] { gather2<8><<<grid, 1024>>>((uint32_t*)tb, perm, (uint2*)base, nbase, pairs, per, out); });
+  run("g32x2+base64 NB4 (4 MB base)", 256, [&] { gather2<4><<<grid, 1024>>>((uint32_t*)tb, perm, (uint2*)base, nbase, pairs, per, out); });
+  run("g32x2+base64 NB8 (2 MB base)", 256, [&] { gather2<8><<<grid, 1024>>>((uint32_t*)tb, perm, (uint2*)base, nbase / 2, pairs, per, out); });
   // u64 rows (512 B) over the same 12.8 GB: 25M rows
   if (make_perm(pairs / 2)) return 1;
   run("g64 NB8 (25M rows)", 512, [&] { gather<uint64_t, 8, false><<<grid, 1024>>>((uint64_t*)tb, perm, base, nbase, pairs, per, out); });

@@ -935,7 +935,7 @@ static int gram_wide_rows(int64_t n, int64_t d, int64_t count, bool split3) {
 // 4096 k) and the flush buffer: one fp32 tile per block of the largest launch (a generation:
 // 2 x CUs 128-tiles or 1 x CUs 256-super-tiles).
 static int gram_flush_stages() {
-  int f = 128;
+  int f = 256;  // k = 8192 per flush: profiles/r2_gram_flush.log (128: -7 % TF/s, errors within 2x)
   if (const char* e = getenv("VISREPS_GRAM_FLUSH")) f = atoi(e);
   return f > 0 ? f : 0;
 }

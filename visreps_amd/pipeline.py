@@ -50,13 +50,22 @@ class StepTimes:
     engine_bytes: float = 0.0      # the engine's own algorithmic bytes (engine_call_bytes)
     engine_ref_bytes: float = 0.0  # reference-equivalent bytes (engine_bytes(), §8(d))
     engine_calls: int = 0          # units
+    phase_ms: Dict[str, float] = field(default_factory=dict)  # step phases (bench breakdown)
     _pending: list = field(default_factory=list)
+
+    def phases(self, names: Sequence[str], events: Sequence) -> None:
+        """Phase i spans events[i] .. events[i + 1] (HIP events on the compute stream)."""
+        self._pending.append(("phases", list(names), list(events), 0.0, 0, 0.0))
 
     def record(self, kind: str, start, end, work: float, calls: int = 1, ref: float = 0.0):
         self._pending.append((kind, start, end, work, calls, ref))
 
     def resolve(self):
         for kind, s, e, w, c, ref in self._pending:
+            if kind == "phases":
+                for i, name in enumerate(s):
+                    self.phase_ms[name] = self.phase_ms.get(name, 0.0) + e[i].elapsed_time(e[i + 1])
+                continue
             ms = s.elapsed_time(e)
             if kind == "gram":
                 self.gram_ms += ms
