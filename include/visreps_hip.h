@@ -224,6 +224,16 @@ int vr_srp_csr_f32(const int32_t* indptr, const int32_t* indices, const float* v
                    int64_t ldo, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------
+ * Full-triangle Spearman of two RDMs with up to 2^32 - 1 pairs (n <= 92681), no rank plan:
+ * the compute_rdm_correlation(.., "Spearman") path above the engine's 16-bit stimulus
+ * indices (rsa.py:96-129 at configs[2]'s 73k stimuli). Radix sort of (key, triangle
+ * index), average ranks, exact u128 sums; out [device] one double.
+ * -------------------------------------------------------------------------- */
+size_t vr_spearman_full_workspace(int64_t n);
+int vr_spearman_full_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out,
+                         void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------
  * Multi-GPU RDM pieces (stimulus-sharded rows); replace the
  * block-distributed use of vr_rdm_pearson_tiles_f32 + a sum all-reduce:
  *  - each rank splits its own rows (row stats + centred bf16 hi/lo plane records);

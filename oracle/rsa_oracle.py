@@ -113,9 +113,12 @@ def midrank_spearman(v1: np.ndarray, v2: np.ndarray) -> float:
     a = r1.astype(np.int64)
     b = r2.astype(np.int64)
     mu = m * (m + 1) ** 2
-    sab = int(np.dot(a.astype(object), b.astype(object))) if m < 2**20 else int((a * b).sum())
-    saa = int(np.dot(a.astype(object), a.astype(object))) if m < 2**20 else int((a * a).sum())
-    sbb = int(np.dot(b.astype(object), b.astype(object))) if m < 2**20 else int((b * b).sum())
+
+    def exact_dot(x, y):  # each product < (2m)^2 fits int64; chunk sums summed as Python ints
+        p = x * y
+        return sum(int(c) for c in np.add.reduceat(p, np.arange(0, m, 4096)))
+
+    sab, saa, sbb = exact_dot(a, b), exact_dot(a, a), exact_dot(b, b)
     num, va, vb = sab - mu, saa - mu, sbb - mu
     if va <= 0 or vb <= 0:
         return float("nan")

@@ -211,6 +211,35 @@ def test_cfg3_73k_rdm(dev):
     cols = _rows(dev, n, 6)
     assert torch.equal(rdm[rows][:, cols], rdm[cols][:, rows].T)  # exact symmetry, sampled
     assert torch.all(rdm[rows] >= 0) and torch.all(rdm[rows] <= 2)
+    # configs[2]'s full-triangle Spearman (2.66e9 pairs) on the plan-free path: exact
+    # properties of the rank statistic at full size (the arithmetic itself is pinned to the
+    # rank-plan engine and scipy at small n, tests/test_gpu_parity.py, and at n = 65535 below)
+    del x
+    torch.cuda.empty_cache()
+    r_aa = R.compute_rdm_correlation(rdm, rdm, correlation="Spearman")
+    assert abs(r_aa - 1.0) <= 1e-12
+    neg = -rdm  # the reversed order, same ties
+    assert abs(R.spearman_full(rdm, neg) + 1.0) <= 1e-12
+    del neg
+    other = rdm.clone()
+    other[:, : n // 2] = other[:, : n // 2].sqrt()  # monotone on half the columns only
+    other = torch.minimum(other, other.T)  # symmetric again
+    r_ab = R.spearman_full(rdm, other)
+    assert R.spearman_full(other, rdm) == r_ab and 0.5 < r_ab < 1.0
+
+
+def test_spearman_full_equals_engine_at_plan_limit(dev):
+    # n = 65535 (2.15e9 pairs), the largest rank plan: the plan-free full Spearman and the
+    # rank-plan engine are both exact integer statistics and must agree bit for bit
+    n = 65535
+    g = torch.Generator(device=dev).manual_seed(11)
+    z = torch.randn(n, 32, device=dev, generator=g)
+    a = R.compute_rdm(z + 0.5 * torch.randn(n, 32, device=dev, generator=g))
+    b = R.compute_rdm(z + 0.5 * torch.randn(n, 32, device=dev, generator=g))
+    del z
+    full = R.spearman_full(a, b)
+    eng = R.compute_rdm_correlation(a, b, correlation="Spearman")
+    assert full == eng and 0.0 < full < 1.0
 
 
 # ----------------------------------------------------------------------------- configs[4]

@@ -429,3 +429,35 @@ def test_rdm_wide_supertiles(dev, wide, monkeypatch):
     ref.fill_diagonal_(0.0)
     assert float((got - ref).abs().max()) <= 5e-6
     assert torch.equal(got, got.T) and torch.all(torch.diagonal(got) == 0)
+
+
+# --------------------------------------------------------------------------- large n
+@pytest.mark.parametrize("n,levels", [(2, None), (3, None), (700, None), (1500, 5), (3000, 40)])
+def test_spearman_full_equals_plan_path_and_oracle(dev, n, levels):
+    # the plan-free full-triangle Spearman (used above n = 65535) against the rank-plan
+    # engine (bit for bit: both exact integer sums) and scipy (tie-heavy RDMs included)
+    a = O.synthetic_features(n, [40], seed=n)[0]
+    b = O.synthetic_features(n, [60], seed=n + 1)[0]
+    ra, rb = O.compute_rdm(a), O.compute_rdm(b)
+    if levels:
+        ra = (np.floor(ra * levels) / levels).astype(np.float32)
+    ta, tb = torch.from_numpy(ra).to(dev), torch.from_numpy(rb).to(dev)
+    got = R.spearman_full(ta, tb)
+    ref = R.compute_rdm_correlation(ta, tb, correlation="Spearman")
+    if n < 3:
+        assert np.isnan(got) and np.isnan(ref)
+        return
+    assert got == ref
+    iu = np.triu_indices(n, 1)
+    assert abs(got - O.midrank_spearman(ra[iu], rb[iu])) <= 1e-12
+    assert R.spearman_full(tb, ta) == got
+
+
+def test_spearman_full_nan_and_constant(dev):
+    a = torch.rand(50, 50, device=dev)
+    a = (a + a.T) / 2
+    c = torch.ones(50, 50, device=dev)
+    assert np.isnan(R.spearman_full(a, c))
+    b = a.clone()
+    b[3, 7] = float("nan")
+    assert np.isnan(R.spearman_full(a, b))

@@ -122,6 +122,8 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _c_sz, _vp],
     ),
+    "vr_spearman_full_workspace": (_c_sz, [_c_i64]),
+    "vr_spearman_full_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
     "vr_rdm_plane_rows": (_c_i64, [_c_i64]),
     "vr_rdm_plane_row_bytes": (_c_sz, [_c_i64]),
     "vr_rdm_split_rows_f32": (

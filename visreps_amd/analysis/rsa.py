@@ -42,6 +42,7 @@ __all__ = [
     "bootstrap_spearman",
     "bootstrap_spearman_multi",
     "bootstrap_kendall",
+    "spearman_full",
     "percentile",
     "_rank",
     "_concept_average_exact",
@@ -160,7 +161,9 @@ class RankPlan:
         r = _as_device_f32(rdm, self.device)
         self.n = int(r.size(0))
         if self.n > 65535:
-            raise ValueError("rank plans support n <= 65535 stimuli")
+            raise ValueError("rank plans (the bootstrap engine's 16-bit pair codes) support n <= "
+                             "65535 stimuli; the full-triangle Spearman of a larger RDM is "
+                             "compute_rdm_correlation / spearman_full")
         L = lib()
         self.buf = torch.empty(L.vr_rank_plan_bytes(self.n), dtype=torch.uint8, device=self.device)
         ws = workspace.get(self.device, L.vr_rank_plan_workspace(self.n), "plan_build")
@@ -329,6 +332,8 @@ def compute_rdm_correlation(
     out = torch.empty(1, dtype=torch.float64, device=dev)
     L = lib()
     with torch.cuda.device(dev):
+        if corr == "spearman" and n > 65535:
+            return spearman_full(a, b)
         if corr == "spearman":
             ws = workspace.get(dev, L.vr_spearman_triu_workspace(n), "triu")
             check(
@@ -354,6 +359,31 @@ def compute_rdm_correlation(
     if math.isnan(val):
         logger.warning("NaN returned for %s correlation", correlation)
         return float("nan")
+    return val
+
+
+def spearman_full(rdm1: torch.Tensor, rdm2: torch.Tensor) -> float:
+    """Spearman of the strict upper triangles without a rank plan (vr_spearman_full_f32):
+    radix sort of (value, triangle index) per RDM, average ranks, exact integer sums; any
+    n with n(n-1)/2 < 2^32 (n <= 92681). compute_rdm_correlation uses it above the rank
+    plan's n <= 65535 (configs[2]'s 73k-stimulus RDM)."""
+    dev = _device_for(rdm1, rdm2)
+    a = _as_device_f32(rdm1, dev)
+    b = _as_device_f32(rdm2, dev)
+    if a.shape != b.shape or a.ndim != 2 or a.size(0) != a.size(1):
+        raise ValueError("RDMs must share the same square 2-D shape")
+    if a.stride(0) != b.stride(0):
+        a, b = a.contiguous(), b.contiguous()
+    n = a.size(0)
+    out = torch.empty(1, dtype=torch.float64, device=dev)
+    L = lib()
+    ws = workspace.get(dev, L.vr_spearman_full_workspace(n), "spearman_full")
+    with torch.cuda.device(dev):
+        check(L.vr_spearman_full_f32(_ptr(a), _ptr(b), n, a.stride(0), _ptr(out), _ptr(ws), ws.numel(),
+                                     stream_of(dev)), "vr_spearman_full_f32")
+    val = float(out.item())
+    if math.isnan(val):
+        logger.warning("NaN returned for Spearman correlation")
     return val
 
 

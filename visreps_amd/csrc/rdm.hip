@@ -931,8 +931,8 @@ static int gram_wide_rows(int64_t n, int64_t d, int64_t count, bool split3) {
 
 // Scratch of one RDM launch over `count` tiles: row stats, split-K partial tiles, and the
 // bf16 plane records of the split kernel (rows padded to the 256-row super-tile edge).
-// Accumulator flush interval in k stages (VISREPS_GRAM_FLUSH, 0 = off; default 128 stages =
-// 4096 k) and the flush buffer: one fp32 tile per block of the largest launch (a generation:
+// Accumulator flush interval in k stages (VISREPS_GRAM_FLUSH, 0 = off; default 256 stages =
+// 8192 k) and the flush buffer: one fp32 tile per block of the largest launch (a generation:
 // 2 x CUs 128-tiles or 1 x CUs 256-super-tiles).
 static int gram_flush_stages() {
   int f = 256;  // k = 8192 per flush: profiles/r2_gram_flush.log (128: -7 % TF/s, errors within 2x)
