@@ -232,6 +232,20 @@ int vr_srp_csr_f32(const int32_t* indptr, const int32_t* indices, const float* v
 size_t vr_spearman_full_workspace(int64_t n);
 int vr_spearman_full_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out,
                          void* ws, size_t ws_bytes, void* stream);
+/* Local pieces of the distributed global rank (sample sort over ranks,
+ * visreps_amd/analysis/distributed_spearman.py): sortable keys of fp32 values, an in-place
+ * (key, value) radix sort, doubled midranks (+ 2 base) of a sorted key run with its tie
+ * term sum (k^3 - k) as a u128 {lo, hi}, and an exact u64 dot product (u128 {lo, hi}). */
+int vr_f32_sort_keys(const float* v, int64_t m, uint32_t* keys, void* stream);
+size_t vr_sort_pairs_workspace(int64_t m);
+int vr_sort_pairs_u32(uint32_t* keys, uint32_t* vals, int64_t m, void* ws, size_t ws_bytes,
+                      void* stream);
+size_t vr_midranks_workspace(int64_t m);
+int vr_midranks_sorted(const uint32_t* keys, int64_t m, uint64_t base, uint64_t* y, uint64_t* tie,
+                       void* ws, size_t ws_bytes, void* stream);
+size_t vr_dot_u64_workspace(void);
+int vr_dot_u64(const uint64_t* a, const uint64_t* b, int64_t m, uint64_t* out, void* ws,
+               size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------
  * Multi-GPU RDM pieces (stimulus-sharded rows); replace the

@@ -124,6 +124,13 @@ _PROTOTYPES = {
     ),
     "vr_spearman_full_workspace": (_c_sz, [_c_i64]),
     "vr_spearman_full_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "vr_f32_sort_keys": (ctypes.c_int, [_vp, _c_i64, _vp, _vp]),
+    "vr_sort_pairs_workspace": (_c_sz, [_c_i64]),
+    "vr_sort_pairs_u32": (ctypes.c_int, [_vp, _vp, _c_i64, _vp, _c_sz, _vp]),
+    "vr_midranks_workspace": (_c_sz, [_c_i64]),
+    "vr_midranks_sorted": (ctypes.c_int, [_vp, _c_i64, ctypes.c_uint64, _vp, _vp, _vp, _c_sz, _vp]),
+    "vr_dot_u64_workspace": (_c_sz, []),
+    "vr_dot_u64": (ctypes.c_int, [_vp, _vp, _c_i64, _vp, _vp, _c_sz, _vp]),
     "vr_rdm_plane_rows": (_c_i64, [_c_i64]),
     "vr_rdm_plane_row_bytes": (_c_sz, [_c_i64]),
     "vr_rdm_split_rows_f32": (

@@ -229,4 +229,126 @@ int vr_spearman_full_f32(const float* A, const float* B, int64_t n, int64_t ld, 
   return VR_OK;
 }
 
+
+// ---------------------------------------------------------------------------------
+// Local pieces of the distributed global rank (analysis/distributed_spearman.py)
+// ---------------------------------------------------------------------------------
+size_t vr_sort_pairs_workspace(int64_t m) {
+  if (m <= 1) return 256;
+  Carver c(nullptr);
+  c.take<uint32_t>((size_t)m);
+  c.take<uint32_t>((size_t)m);
+  c.take<uint32_t>(radix_ws_elems(m));
+  return c.bytes();
+}
+
+int vr_sort_pairs_u32(uint32_t* keys, uint32_t* vals, int64_t m, void* ws, size_t ws_bytes, void* stream) {
+  VR_REQUIRE(m >= 0 && m < ((int64_t)1 << 32), "vr_sort_pairs_u32: m=%lld", (long long)m);
+  if (m <= 1) return VR_OK;
+  VR_REQUIRE(keys && vals && ws && ws_bytes >= vr_sort_pairs_workspace(m), "vr_sort_pairs_u32: workspace");
+  Carver c(ws);
+  uint32_t* ka = c.take<uint32_t>((size_t)m);
+  uint32_t* va = c.take<uint32_t>((size_t)m);
+  uint32_t* rw = c.take<uint32_t>(radix_ws_elems(m));
+  return radix_sort_kv(keys, vals, ka, va, m, rw, as_stream(stream));
+}
+
+__global__ void k_sort_keys(const float* __restrict__ v, int64_t m, uint32_t* __restrict__ keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) keys[i] = f32_sort_key(v[i]);
+}
+
+int vr_f32_sort_keys(const float* v, int64_t m, uint32_t* keys, void* stream) {
+  VR_REQUIRE(m >= 0 && m < ((int64_t)1 << 32), "vr_f32_sort_keys: m=%lld", (long long)m);
+  if (m == 0) return VR_OK;
+  VR_REQUIRE(v && keys, "vr_f32_sort_keys: null pointer");
+  k_sort_keys<<<(unsigned)((m + 255) / 256), 256, 0, as_stream(stream)>>>(v, m, keys);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+__global__ __launch_bounds__(FULL_BS) void k_midranks_run(const uint32_t* __restrict__ flags,
+                                                           const uint32_t* __restrict__ gidx,
+                                                           const uint32_t* __restrict__ gstart, int64_t m,
+                                                           uint64_t base2, uint64_t* __restrict__ y,
+                                                           uint64_t* __restrict__ part) {
+  u128 tie = 0;
+  for (int64_t i = (int64_t)blockIdx.x * FULL_BS + threadIdx.x; i < m; i += (int64_t)gridDim.x * FULL_BS) {
+    uint64_t k;
+    y[i] = base2 + midrank2(flags, gidx, gstart, i, k);
+    if (flags[i]) tie += (u128)(k * k) * k - k;
+  }
+  block_sum_u128(tie, part, 0, 1);
+}
+
+__global__ __launch_bounds__(FULL_BS) void k_dot_u64(const uint64_t* __restrict__ a,
+                                                      const uint64_t* __restrict__ b, int64_t m,
+                                                      uint64_t* __restrict__ part) {
+  u128 s = 0;
+  for (int64_t i = (int64_t)blockIdx.x * FULL_BS + threadIdx.x; i < m; i += (int64_t)gridDim.x * FULL_BS)
+    s += (u128)a[i] * b[i];
+  block_sum_u128(s, part, 0, 1);
+}
+
+__global__ void k_sum_parts(const uint64_t* __restrict__ part, int nblk, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  u128 s = 0;
+  for (int b = 0; b < nblk; ++b) s += ((u128)part[2 * b + 1] << 64) | part[2 * b];
+  out[0] = (uint64_t)s;
+  out[1] = (uint64_t)(s >> 64);
+}
+
+size_t vr_midranks_workspace(int64_t m) {
+  Carver c(nullptr);
+  c.take<uint32_t>((size_t)std::max<int64_t>(m, 1));
+  c.take<uint32_t>((size_t)std::max<int64_t>(m, 1));
+  c.take<uint32_t>((size_t)m + 1);
+  c.take<uint32_t>(scan_ws_elems(m));
+  c.take<uint64_t>((size_t)full_grid() * 2);
+  return c.bytes();
+}
+
+int vr_midranks_sorted(const uint32_t* keys, int64_t m, uint64_t base, uint64_t* y, uint64_t* tie,
+                       void* ws, size_t ws_bytes, void* stream) {
+  VR_REQUIRE(m >= 0 && m < ((int64_t)1 << 32), "vr_midranks_sorted: m=%lld", (long long)m);
+  VR_REQUIRE(tie && ws && ws_bytes >= vr_midranks_workspace(m), "vr_midranks_sorted: workspace");
+  hipStream_t st = as_stream(stream);
+  if (m == 0) {
+    VR_CHECK_HIP(hipMemsetAsync(tie, 0, 2 * sizeof(uint64_t), st));
+    return VR_OK;
+  }
+  VR_REQUIRE(keys && y, "vr_midranks_sorted: null pointer");
+  Carver c(ws);
+  uint32_t* flags = c.take<uint32_t>((size_t)m);
+  uint32_t* gidx = c.take<uint32_t>((size_t)m);
+  uint32_t* gstart = c.take<uint32_t>((size_t)m + 1);
+  uint32_t* sw = c.take<uint32_t>(scan_ws_elems(m));
+  uint64_t* part = c.take<uint64_t>((size_t)full_grid() * 2);
+  const unsigned gb = (unsigned)((m + 255) / 256);
+  k_group_flags_full<<<gb, 256, 0, st>>>(keys, m, flags);
+  VR_CHECK_LAUNCH();
+  VR_TRY(scan_exclusive_u32(flags, gidx, m, nullptr, sw, st));
+  k_group_starts_full<<<gb, 256, 0, st>>>(flags, gidx, m, gstart);
+  VR_CHECK_LAUNCH();
+  k_midranks_run<<<full_grid(), FULL_BS, 0, st>>>(flags, gidx, gstart, m, 2 * base, y, part);
+  VR_CHECK_LAUNCH();
+  k_sum_parts<<<1, 64, 0, st>>>(part, full_grid(), tie);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+size_t vr_dot_u64_workspace(void) { return (size_t)full_grid() * 2 * sizeof(uint64_t) + 256; }
+
+int vr_dot_u64(const uint64_t* a, const uint64_t* b, int64_t m, uint64_t* out, void* ws, size_t ws_bytes,
+               void* stream) {
+  VR_REQUIRE(m >= 0 && out && ws && ws_bytes >= vr_dot_u64_workspace(), "vr_dot_u64: bad arguments");
+  hipStream_t st = as_stream(stream);
+  uint64_t* part = static_cast<uint64_t*>(ws);
+  k_dot_u64<<<full_grid(), FULL_BS, 0, st>>>(a, b, m, part);
+  VR_CHECK_LAUNCH();
+  k_sum_parts<<<1, 64, 0, st>>>(part, full_grid(), out);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
 }  // extern "C"
