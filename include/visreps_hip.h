@@ -289,6 +289,31 @@ int vr_transform_u8(const uint8_t* src, int64_t B, int64_t H, int64_t W, int64_t
                     void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------
+ * PCA covariance for the coarse-grained PCA labels: replaces
+ * batched_pca's mean and covariance, scripts/coarsegrain/compute_eigenvectors.py:23-36
+ *   mean = X.mean(axis=0);  cov = sum_b (X[b].astype(f64) - mean)^T (..) / (n - 1).
+ * X [dev] fp32 row-major (n, p), leading dimension ldx >= p.
+ * -------------------------------------------------------------------------- */
+/* Column sums in numpy's float32 order (rows added in row order, one float32 running sum
+ * per column), continued from init [dev] p (nullable: 0). sum [dev] p. Bit-identical to
+ * numpy's X.sum(axis=0) on a C-order float32 array; chained over row shards it is the
+ * same sum (the multi-GPU form passes the previous shard's sum as init). */
+int vr_col_sum_f32(const float* X, int64_t n, int64_t p, int64_t ldx, const float* init,
+                   float* sum, void* stream);
+/* X.mean(axis=0) as numpy: the column sums / float32(n). mean [dev] p. */
+int vr_col_mean_f32(const float* X, int64_t n, int64_t p, int64_t ldx, float* mean, void* stream);
+/* mean [dev] p = sum [dev] p / float32(n) (may alias). */
+int vr_mean_from_sum_f32(const float* sum, int64_t p, int64_t n, float* mean, void* stream);
+/* cov [dev] fp64 (p, p), leading dimension ldc: sum over rows of
+ * ((double)x - (double)mean)^T ((double)x - (double)mean) / denom, exactly symmetric, on
+ * the fp64 MFMA. mean [dev] fp32 p. denom = n - 1 for the reference's covariance, 1 for a
+ * rank's partial sum (multi-GPU: all-reduce, then divide). */
+size_t vr_pca_cov_workspace(int64_t n, int64_t p);
+int vr_pca_cov_f64(const float* X, int64_t n, int64_t p, int64_t ldx, const float* mean,
+                   double denom, double* cov, int64_t ldc, void* ws, size_t ws_bytes,
+                   void* stream);
+
+/* ------------------------------------------------------------------------------
  * Host: legacy numpy RandomState (MT19937) index streams, bit-exact.
  * Replaces np.random.RandomState(seed) + .choice(n, k, replace=False) / .permutation(n)
  * (evals.py:260-261,356,362-364; rsa.py:169,176,248-250; evals.py:111-113).

@@ -24,3 +24,24 @@ def dev():
 
     assert torch.cuda.is_available(), "gpu tests need a HIP device"
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def _release_device_memory(request):
+    """GPU tests at bench and cfg3 sizes hold tens of GB each (workspaces, plans, RDMs):
+    after every GPU test drop the library's scratch pool and torch's cached blocks, so
+    the next test starts from an empty device (the suite runs in one process)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+
+    import torch
+
+    if not torch.cuda.is_available():
+        return
+    from visreps_amd._lib import workspace
+
+    workspace.release()
+    gc.collect()
+    torch.cuda.empty_cache()

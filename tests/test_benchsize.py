@@ -125,12 +125,73 @@ def idx():
     return bootstrap_indices(42, N, int(0.9 * N), NB)
 
 
+# ----------------------------------------------------------------------------- configs[2]
+# (first in the module: they need ~130 GB of device memory before the module-scoped bench
+# features are created)
+def test_cfg3_73k_rdm(dev):
+    n, d = 73000, 43264
+    g = torch.Generator(device=dev).manual_seed(7)
+    z = torch.randn(n, 64, device=dev, generator=g)
+    x = z @ (torch.randn(64, d, device=dev, generator=g) / 8)
+    x += 2 * torch.randn(n, d, device=dev, generator=g)
+    x.relu_()
+    del z
+    rdm = R.compute_rdm(x)
+    rows = _rows(dev, n, 5)
+    err = _row_err(rdm, x, rows)
+    err32 = _row_err(_fp32_rdm(x), x, rows)
+    assert err <= max(ROW_TOL, err32), (err, err32)
+    assert torch.all(torch.diagonal(rdm) == 0)
+    cols = _rows(dev, n, 6)
+    assert torch.equal(rdm[rows][:, cols], rdm[cols][:, rows].T)  # exact symmetry, sampled
+    assert torch.all(rdm[rows] >= 0) and torch.all(rdm[rows] <= 2)
+    # configs[2]'s full-triangle Spearman (2.66e9 pairs) on the plan-free path: exact
+    # properties of the rank statistic at full size (the arithmetic itself is pinned to the
+    # rank-plan engine and scipy at small n, tests/test_gpu_parity.py, and at n = 65535 below)
+    del x
+    torch.cuda.empty_cache()
+    r_aa = R.compute_rdm_correlation(rdm, rdm, correlation="Spearman")
+    assert abs(r_aa - 1.0) <= 1e-12
+    neg = -rdm  # the reversed order, same ties
+    assert abs(R.spearman_full(rdm, neg) + 1.0) <= 1e-12
+    del neg
+    other = rdm.clone()
+    other[:, : n // 2] = other[:, : n // 2].sqrt()  # monotone on half the columns only
+    other = torch.minimum(other, other.T)  # symmetric again
+    r_ab = R.spearman_full(rdm, other)
+    assert R.spearman_full(other, rdm) == r_ab and 0.5 < r_ab < 1.0
+
+
+def test_spearman_full_equals_engine_at_plan_limit(dev):
+    # n = 65535 (2.15e9 pairs), the largest rank plan: the plan-free full Spearman and the
+    # rank-plan engine are both exact integer statistics and must agree bit for bit
+    n = 65535
+    g = torch.Generator(device=dev).manual_seed(11)
+    z = torch.randn(n, 32, device=dev, generator=g)
+    a = R.compute_rdm(z + 0.5 * torch.randn(n, 32, device=dev, generator=g))
+    b = R.compute_rdm(z + 0.5 * torch.randn(n, 32, device=dev, generator=g))
+    del z
+    full = R.spearman_full(a, b)
+    eng = R.compute_rdm_correlation(a, b, correlation="Spearman")
+    assert full == eng and 0.0 < full < 1.0
+
+
 # ------------------------------------------------------------------------ bench features
 @pytest.fixture(scope="module")
 def bench(dev):
     """bench.py's inputs: random-init CustomCNN (seed 0), 10k synthetic images, the 14
     flattened points, and the V1 responses."""
+    import os
+
+    # bench.py switches on cudnn.benchmark and MIOpen's find mode at import; the later
+    # modules' exact-equality tests extract twice and need one fixed algorithm per shape
+    prev = torch.backends.cudnn.benchmark, os.environ.get("MIOPEN_FIND_MODE")
     from bench import LAYERS, extract
+    torch.backends.cudnn.benchmark = prev[0]
+    if prev[1] is None:
+        os.environ.pop("MIOPEN_FIND_MODE", None)
+    else:
+        os.environ["MIOPEN_FIND_MODE"] = prev[1]
     from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_responses
     from visreps_amd.models.custom_model import CustomCNN
     from visreps_amd.models.utils import FeatureExtractor
@@ -191,55 +252,6 @@ def test_synthetic_width_split_gram_parity(dev, idx, d):
     s_split = _scores(rdm, R.compute_rdm(y), idx)
     s_64 = _scores(rdm_f64(x), rdm_f64(y), idx)
     assert float(np.max(np.abs(s_split - s_64))) < SPEARMAN_TOL
-
-
-# ----------------------------------------------------------------------------- configs[2]
-def test_cfg3_73k_rdm(dev):
-    n, d = 73000, 43264
-    g = torch.Generator(device=dev).manual_seed(7)
-    z = torch.randn(n, 64, device=dev, generator=g)
-    x = z @ (torch.randn(64, d, device=dev, generator=g) / 8)
-    x += 2 * torch.randn(n, d, device=dev, generator=g)
-    x.relu_()
-    del z
-    rdm = R.compute_rdm(x)
-    rows = _rows(dev, n, 5)
-    err = _row_err(rdm, x, rows)
-    err32 = _row_err(_fp32_rdm(x), x, rows)
-    assert err <= max(ROW_TOL, err32), (err, err32)
-    assert torch.all(torch.diagonal(rdm) == 0)
-    cols = _rows(dev, n, 6)
-    assert torch.equal(rdm[rows][:, cols], rdm[cols][:, rows].T)  # exact symmetry, sampled
-    assert torch.all(rdm[rows] >= 0) and torch.all(rdm[rows] <= 2)
-    # configs[2]'s full-triangle Spearman (2.66e9 pairs) on the plan-free path: exact
-    # properties of the rank statistic at full size (the arithmetic itself is pinned to the
-    # rank-plan engine and scipy at small n, tests/test_gpu_parity.py, and at n = 65535 below)
-    del x
-    torch.cuda.empty_cache()
-    r_aa = R.compute_rdm_correlation(rdm, rdm, correlation="Spearman")
-    assert abs(r_aa - 1.0) <= 1e-12
-    neg = -rdm  # the reversed order, same ties
-    assert abs(R.spearman_full(rdm, neg) + 1.0) <= 1e-12
-    del neg
-    other = rdm.clone()
-    other[:, : n // 2] = other[:, : n // 2].sqrt()  # monotone on half the columns only
-    other = torch.minimum(other, other.T)  # symmetric again
-    r_ab = R.spearman_full(rdm, other)
-    assert R.spearman_full(other, rdm) == r_ab and 0.5 < r_ab < 1.0
-
-
-def test_spearman_full_equals_engine_at_plan_limit(dev):
-    # n = 65535 (2.15e9 pairs), the largest rank plan: the plan-free full Spearman and the
-    # rank-plan engine are both exact integer statistics and must agree bit for bit
-    n = 65535
-    g = torch.Generator(device=dev).manual_seed(11)
-    z = torch.randn(n, 32, device=dev, generator=g)
-    a = R.compute_rdm(z + 0.5 * torch.randn(n, 32, device=dev, generator=g))
-    b = R.compute_rdm(z + 0.5 * torch.randn(n, 32, device=dev, generator=g))
-    del z
-    full = R.spearman_full(a, b)
-    eng = R.compute_rdm_correlation(a, b, correlation="Spearman")
-    assert full == eng and 0.0 < full < 1.0
 
 
 # ----------------------------------------------------------------------------- configs[4]

@@ -122,6 +122,14 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _c_sz, _vp],
     ),
+    "vr_col_sum_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "vr_col_mean_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp]),
+    "vr_mean_from_sum_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _vp, _vp]),
+    "vr_pca_cov_workspace": (_c_sz, [_c_i64, _c_i64]),
+    "vr_pca_cov_f64": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _c_i64, _vp, ctypes.c_double, _vp, _c_i64, _vp, _c_sz, _vp],
+    ),
     "vr_spearman_full_workspace": (_c_sz, [_c_i64]),
     "vr_spearman_full_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
     "vr_f32_sort_keys": (ctypes.c_int, [_vp, _c_i64, _vp, _vp]),

@@ -21,14 +21,14 @@ negative summed squared error (``l2_neg_loss``), averaged over folds; per-target
 alpha = first argmax over alphas (``local_alpha=True``); refit on all fit rows with each
 target's alpha. Wide layers (p >= n) run in kernel (dual) form: with K = X X^T = Q diag(lam) Q^T the fit
 on rows T predicts rows V as K[V, T] Q diag(1 / (lam + alpha)) Q^T Y[T], which equals the
-primal SVD solution X_V V diag(s / (s^2 + alpha)) U^T Y with lam = s^2. Eigenvalues below
-n * eps_fp32 * lam_max are treated as the exact zeros of a rank-deficient X (the primal
-SVD has no such components). Narrow layers (p < n) run the primal form on the p x p
-Grams X_T^T X_T of each fold (``ridge_cv_predict_primal``). K comes from the MI355X Gram kernel (``vr_gram_f32``: the
-RDM's MFMA kernel without centring or epilogue; one Gram of the stacked fit + val rows
-holds both blocks); the eigendecomposition and the small dense products run in fp64
-through torch (rocSOLVER / rocBLAS); the statistic and its bootstrap run in
-``vr_corr_score_f32``.
+primal SVD solution X_V V diag(s / (s^2 + alpha)) U^T Y with lam = s^2. Every component
+with lam above the fp64 rounding floor of the decomposition (n * eps_64 * lam_max) is kept,
+as himalaya's SVD solver keeps every singular value. Narrow layers (p < n) run the primal
+form on the p x p Grams X_T^T X_T of each fold (``ridge_cv_predict_primal``). The ridge
+Grams are fp64 (``gram64``, rocBLAS DGEMM: the solves are conditioning-sensitive, ADVICE
+r1); the eigendecompositions and the small dense products run in fp64 through torch
+(rocSOLVER / rocBLAS); the statistic and its bootstrap run in ``vr_corr_score_f32``. The
+MFMA Gram kernel (``vr_gram_f32``, ``gram``) stays available for fp32 callers.
 
 Parity: the correlation statistic follows himalaya's ``correlation_score`` (checked
 against scipy.stats.pearsonr, as the reference's tests/test_encoding_score.py:1251-1376)
