@@ -178,11 +178,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; more ranks than GPUs (the gloo rehearsal of the multi-rank path
+    # on a one-GPU box) share devices round-robin
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL (backend "nccl") over xGMI; VISREPS_DIST_BACKEND=gloo only rehearses the
+        # orchestration when ranks share a GPU (RCCL refuses two ranks on one device)
+        backend = os.environ.get("VISREPS_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         pg = dist.group.WORLD
     N = args.n
     rows = shard_rows(N, rank, world)

@@ -97,7 +97,9 @@ def test_eval_end_to_end_matches_oracle(dev):
         point, scores, lo, hi = O.bootstrap_rsa(g_m, g_n, n_bootstrap=20, seed=42)
         assert abs(df.iloc[i]["score"] - point) <= 1e-12
         assert np.max(np.abs(np.asarray(df.iloc[i]["bootstrap_scores"]) - scores)) <= 1e-12
-        assert df.iloc[i]["ci_low"] == lo and df.iloc[i]["ci_high"] == hi
+        # percentiles of score vectors equal to 1e-12 (the engine's exact-integer statistic vs
+        # scipy's float ranks differ in the last bits)
+        assert abs(df.iloc[i]["ci_low"] - lo) <= 1e-12 and abs(df.iloc[i]["ci_high"] - hi) <= 1e-12
         # (b) fully oracle RDMs: entries within 1e-5; at n = 96 (4,560 pairs) the last-bit
         #     differences of near-tied entries move ranks, a few 1e-5 of rho (the 1e-5
         #     bound at the bench's own N = 10k is tests/test_benchsize.py)

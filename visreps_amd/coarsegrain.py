@@ -150,7 +150,8 @@ def batched_pca_sharded(x_local: torch.Tensor, n_components: int, pg=None):
     mean = mean_from_sum(s, n)
     part = cov_sum(x, mean, 1.0)
     dist.all_reduce(part, group=pg)
-    cov = part / (n - 1)
+    # true division (torch divides by a Python scalar as a multiply by its reciprocal)
+    cov = part / torch.full_like(part, float(n - 1))
     comps, vals, total = eig_top(cov, n_components)
     return comps, vals, mean.cpu().numpy(), np.float64(total)
 
