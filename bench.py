@@ -169,7 +169,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=10000)
+    ap.add_argument("--n", "--stimuli", dest="n", type=int, default=10000)
     ap.add_argument("--boot", type=int, default=1000)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -9,13 +9,15 @@ out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp MIOPEN_FIND_MODE=FAST
 VISREPS_DIST_BACKEND=gloo timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-    --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 1 --warmup 1 --n $n \
+    --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 1 --warmup 1 --stimuli $n \
     --no-cpu-baseline > $out/w2.json 2> $out/w2.err || { echo "world-2 failed"; tail -30 $out/w2.err; exit 1; }
-timeout -k 10 300 python bench.py --steps 1 --warmup 1 --n $n --no-cpu-baseline > $out/w1.json 2> $out/w1.err \
+timeout -k 10 300 python bench.py --steps 1 --warmup 1 --stimuli $n --no-cpu-baseline > $out/w1.json 2> $out/w1.err \
     || { echo "world-1 failed"; tail -30 $out/w1.err; exit 1; }
 python3 - $out <<'PY'
 import json, sys
-a = json.load(open(sys.argv[1] + "/w2.json")); b = json.load(open(sys.argv[1] + "/w1.json"))
+def line(f):  # gloo prints its connection lines to stdout too
+    return json.loads([l for l in open(f) if l.startswith('{"metric"')][-1])
+a = line(sys.argv[1] + "/w2.json"); b = line(sys.argv[1] + "/w1.json")
 print("world2", a["value"], a["check"]); print("world1", b["value"], b["check"])
 print("check equal:", a["check"] == b["check"])
 PY
