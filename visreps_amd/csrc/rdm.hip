@@ -487,36 +487,101 @@ constexpr int S_STAGE = GT * SROW;    // bf16 per panel per stage
 
 // Planes: per row and 32-k stage one 128-byte record [hi k0..31 | lo k0..31]; rows padded
 // to the tile edge and k to the stage with exact zeros (so the Gram kernel has no edges).
+// Fused prepass of the split kernel: the row statistics of k_row_stats (same per-thread
+// fp64 sums in the same order, so mean and std are bit-identical to it) and, in the
+// centred second pass, the bf16 hi/lo stage records (x - mean = hi + lo, hi = bf16(v), lo = bf16(v - hi)). One
+// read of X fewer than separate statistics and split passes (12 instead of 16 B per element). Rows in
+// [n, gridDim.x) and k in [d, 32 nstage) get exact-zero records.
+__device__ inline void split_pair(float v, uint16_t& h, uint16_t& l) {
+  const __bf16 hb = (__bf16)v;
+  h = __builtin_bit_cast(uint16_t, hb);
+  l = __builtin_bit_cast(uint16_t, (__bf16)(v - (float)hb));
+}
+
+__device__ inline void split_store4(uint16_t* prow, int64_t i, f32x4 v) {
+  uint16_t h[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) split_pair(v[e], h[e], l[e]);
+  uint16_t* dst = prow + (i >> 3) * 64 + (i & 7) * 4;  // stage i / 8, 4-k group i % 8
+  *reinterpret_cast<uint2*>(dst) = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+  *reinterpret_cast<uint2*>(dst + 32) = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+}
+
+__device__ inline void split_store1(uint16_t* prow, int64_t k, float v) {
+  uint16_t h, l;
+  split_pair(v, h, l);
+  prow[(k >> 5) * 64 + (k & 31)] = h;
+  prow[(k >> 5) * 64 + 32 + (k & 31)] = l;
+}
+
 template <typename T>
-__global__ void k_split3(const T* __restrict__ X, int64_t n, int64_t d, int64_t ldx,
-                         const float* __restrict__ mean, int64_t rows, int64_t nstage,
-                         uint16_t* __restrict__ planes) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (row, stage, 4-k group)
-  const int64_t per_row = nstage * 8;
-  if (t >= rows * per_row) return;
-  const int64_t r = t / per_row, q = t - r * per_row;
-  const int64_t s = q >> 3;
-  const int g = (int)(q & 7);
-  const int64_t k = s * GK + g * 4;
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-  if (r < n) {
-    const float m = mean[r];
-    const T* src = X + r * ldx + k;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (k + e < d) v[e] = in_f32(src[e]) - m;
+__global__ __launch_bounds__(RSTAT_BS) void k_stats_split(const T* __restrict__ X, int64_t n, int64_t d,
+                                                          int64_t ldx, int64_t nstage, float correction, int vec,
+                                                          float* __restrict__ mean, float* __restrict__ stdv,
+                                                          uint16_t* __restrict__ planes) {
+  __shared__ double lds[RSTAT_BS / 64 + 1];
+  const int64_t r = blockIdx.x, kp = nstage * GK;
+  uint16_t* prow = planes + r * nstage * 64;
+  if (r >= n) {  // padding row
+    for (int64_t i = threadIdx.x; i < kp / 4; i += RSTAT_BS) split_store4(prow, i, f32x4{0.f, 0.f, 0.f, 0.f});
+    return;
   }
-  uint32_t hw[2], lw[2];
-#pragma unroll
-  for (int e = 0; e < 4; e += 2) {
-    const __bf16 h0 = (__bf16)v[e], h1 = (__bf16)v[e + 1];
-    const __bf16 l0 = (__bf16)(v[e] - (float)h0), l1 = (__bf16)(v[e + 1] - (float)h1);
-    hw[e / 2] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-    lw[e / 2] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+  const T* row = X + r * ldx;
+  double s = 0;
+  const int64_t d4 = vec ? d / 4 : 0;
+  if (vec) {
+    for (int64_t i = threadIdx.x; i < d4; i += RSTAT_BS) {
+      f32x4 v = in_f32x4(row + 4 * i);
+      s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+    }
+    for (int64_t i = d4 * 4 + threadIdx.x; i < d; i += RSTAT_BS) s += (double)in_f32(row[i]);
+  } else {
+    for (int64_t i = threadIdx.x; i < d; i += RSTAT_BS) s += (double)in_f32(row[i]);
   }
-  uint16_t* dst = planes + (r * nstage + s) * 64 + g * 4;
-  *reinterpret_cast<uint2*>(dst) = make_uint2(hw[0], hw[1]);
-  *reinterpret_cast<uint2*>(dst + 32) = make_uint2(lw[0], lw[1]);
+  s = block_sum_f64(s, lds);
+  const float m = (float)(s / (double)d);
+  double q = 0;
+  if (vec) {
+    for (int64_t i = threadIdx.x; i < d4; i += RSTAT_BS) {
+      f32x4 v = in_f32x4(row + 4 * i);
+      f32x4 c = {v.x - m, v.y - m, v.z - m, v.w - m};
+      q += (double)(c.x * c.x) + (double)(c.y * c.y) + (double)(c.z * c.z) + (double)(c.w * c.w);
+      split_store4(prow, i, c);
+    }
+    for (int64_t i = d4 * 4 + threadIdx.x; i < d; i += RSTAT_BS) {
+      float a = in_f32(row[i]) - m;
+      q += (double)(a * a);
+    }
+    for (int64_t k = d4 * 4 + threadIdx.x; k < kp; k += RSTAT_BS)  // tail and k padding
+      split_store1(prow, k, k < d ? in_f32(row[k]) - m : 0.f);
+  } else {
+    for (int64_t k = threadIdx.x; k < kp; k += RSTAT_BS) {
+      float a = 0.f;
+      if (k < d) {
+        a = in_f32(row[k]) - m;
+        q += (double)(a * a);
+      }
+      split_store1(prow, k, a);
+    }
+  }
+  q = block_sum_f64(q, lds);
+  if (threadIdx.x == 0) {
+    float var = (float)(q / (double)d);
+    float sd = sqrtf(var + correction);
+    if (sd < correction * 10.0f) sd = 1.0f;  // rsa.py:84-87 zero-variance guard
+    mean[r] = m;
+    stdv[r] = sd;
+  }
+}
+
+template <typename T>
+static int stats_split(const T* X, int64_t n, int64_t rows, int64_t d, int64_t ldx, float correction,
+                       float* mean, float* stdv, uint16_t* planes, hipStream_t st) {
+  const int vec = ((reinterpret_cast<uintptr_t>(X) & (sizeof(T) == 4 ? 15 : 7)) == 0) && ((ldx & 3) == 0);
+  k_stats_split<T><<<(unsigned)rows, RSTAT_BS, 0, st>>>(X, n, d, ldx, (d + GK - 1) / GK, correction, vec, mean,
+                                                          stdv, planes);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
 }
 
 // this thread's 4 x 16 B of a panel's stage record block (128 rows x 128 B)
@@ -1073,23 +1138,18 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   } else if (raw) {  // zero means: the panels stage X itself
     VR_CHECK_HIP(hipMemsetAsync(mean, 0, (size_t)n * sizeof(float), st));
     VR_CHECK_HIP(hipMemsetAsync(stdv, 0, (size_t)n * sizeof(float), st));
+  } else if (split3) {  // row statistics + hi/lo records in one pass over X
+    const int64_t rows = (n + WT - 1) / WT * WT;
+    if (bf16)
+      VR_TRY(stats_split(static_cast<const uint16_t*>(Xv), n, rows, d, ldx, correction, mean, stdv, planes, st));
+    else
+      VR_TRY(stats_split(X, n, rows, d, ldx, correction, mean, stdv, planes, st));
+    P.planes = planes;
+    P.nstage = (d + GK - 1) / GK;
   } else if (bf16) {
     VR_TRY(row_stats_bf16(static_cast<const uint16_t*>(Xv), n, d, ldx, mean, stdv, correction, st));
   } else {
     VR_TRY(vr_row_stats_f32(X, n, d, ldx, mean, stdv, correction, stream));
-  }
-  if (split3 && !pre.planes) {
-    const int64_t rows = (n + WT - 1) / WT * WT, nstage = (d + GK - 1) / GK;
-    const int64_t threads = rows * nstage * 8;
-    if (bf16)
-      k_split3<uint16_t><<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(
-          static_cast<const uint16_t*>(Xv), n, d, ldx, mean, rows, nstage, planes);
-    else
-      k_split3<float><<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(X, n, d, ldx, mean, rows, nstage,
-                                                                         planes);
-    VR_CHECK_LAUNCH();
-    P.planes = planes;
-    P.nstage = nstage;
   }
   P.X = X;
   P.mean = mean;
@@ -1237,12 +1297,7 @@ int vr_rdm_split_rows_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, 
              (long long)rows, (long long)d);
   if (rows == 0) return VR_OK;
   VR_REQUIRE(X && mean && stdv && planes, "vr_rdm_split_rows_f32: null pointer");
-  VR_TRY(vr_row_stats_f32(X, rows, d, ldx, mean, stdv, correction, stream));
-  const int64_t nstage = (d + GK - 1) / GK, threads = rows * nstage * 8;
-  k_split3<float><<<(unsigned)((threads + 255) / 256), 256, 0, as_stream(stream)>>>(
-      X, rows, d, ldx, mean, rows, nstage, planes);
-  VR_CHECK_LAUNCH();
-  return VR_OK;
+  return stats_split(X, rows, rows, d, ldx, correction, mean, stdv, planes, as_stream(stream));
 }
 
 size_t vr_rdm_planes_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
