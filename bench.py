@@ -293,8 +293,8 @@ def main():
             gpeak, gkern = FP32_MFMA_PEAK_TF, "k_gram (exact fp32, v_mfma_f32_32x32x2_f32)"
         else:  # 3 bf16 MFMA products per algorithmic FLOP: ceiling = bf16 dense peak / 3
             gpeak = round(BF16_MFMA_PEAK_TF / 3, 1)
-            gkern = ("k_gram3w / k_gram3 (centred rows split hi+lo bf16, 3 x v_mfma_f32_32x32x16_bf16 "
-                     "per k-step, fp32 accumulate; peak = bf16 dense peak / 3)")
+            gkern = ("k_gram3p / k_gram3 (centred rows split hi+lo bf16 by k_stats_split, 3 x "
+                     "v_mfma_f32_32x32x16_bf16 per k-step, fp32 accumulate; peak = bf16 dense peak / 3)")
         roof_gram = {"bound": "mfma", "achieved": round(gram_tf, 2), "peak": gpeak,
                      "unit": "TFLOP/s", "frac": round(gram_tf / gpeak, 4), "kernel": gkern,
                      "algorithmic_flops": "N(N+1)D per RDM (phase-1 selection RDMs included)",

@@ -853,6 +853,185 @@ __global__ __launch_bounds__(W_THREADS, 1) void k_gram3w(GramParams P) {
   gram_store_w(P, acc, row0, col0, diag);
 }
 
+// ------------------------------------------------------------------------------------
+// Pipelined wide split Gram (default for full RDMs): k_gram3w's 256 x 256 super-tiles and
+// 8-wave 2 x 4 decomposition, with the panels moved global -> LDS by global_load_lds
+// (16 B per lane, no register staging) in 16-k sub-stages: a sub-stage is, per row, the
+// 64 bytes [hi k0..15 | lo k0..15] of a 32-k record (two 32-B pieces), 16 KB per panel.
+// Four sub-stage slots (A + B = 32 KB each, 128 KB of LDS): while sub-stage q is consumed
+// (24 MFMAs per wave), q+1 and q+2 are in flight and q+3 is issued into the slot q-1 used.
+// Each wave waits only for its own loads of q (counted vmcnt: the loads of q+1 and q+2
+// stay in flight) and then a raw s_barrier, after which every wave's part of q has landed;
+// the slot rewritten by q+3 was last read in iteration q-1, before that barrier. The LDS
+// image is lane-linear per wave-instruction (16 rows x 64 B); 16-B chunk j of row r sits
+// at chunk j ^ ((r >> 2) & 3), applied on the global source address, so a fragment read
+// (32 rows, one chunk) touches 16 distinct 16-B bank slots per 16 lanes.
+// ------------------------------------------------------------------------------------
+#ifndef VR_GRAM_PRIO
+#define VR_GRAM_PRIO 0  // 1: raise the wave priority over its MFMA block (A/B)
+#endif
+constexpr int P_PANEL = WT * 64;       // bytes of one panel sub-stage
+constexpr int P_SLOT = 2 * P_PANEL;    // A + B
+constexpr int P_SLOTS = 4;
+
+// this wave's two 1-KB pieces (16 rows each) of a panel sub-stage: rows [16 (2 w + i), +16)
+__device__ inline void p_issue(const GramParams& P, char* panel, int64_t row0, int q) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t st = q >> 1;
+  const int t = q & 1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rbase = (wid * 2 + i) * 16;
+    const int r = rbase + (lane >> 2);
+    const int j = (lane & 3) ^ ((r >> 2) & 3);  // the logical chunk this lane's slot holds
+    const int off = ((j & 2) << 5) + 32 * t + ((j & 1) << 4);
+    const char* src = reinterpret_cast<const char*>(P.planes) + ((row0 + r) * P.nstage + st) * 128 + off;
+    __builtin_amdgcn_global_load_lds(src, panel + rbase * 64, 16, 0, 0);
+  }
+}
+
+__device__ inline bf16x8 p_frag(const char* panel, int row, int j) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(panel + row * 64 + ((j ^ ((row >> 2) & 3)) << 4)));
+}
+
+template <int N>
+__device__ inline void p_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+struct PFrag {
+  bf16x8 aH[4], aL[4], bH[2], bL[2];
+};
+
+__device__ inline void p_read(const char* As, const char* Bs, PFrag& f) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3, h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int r = wr * 128 + m * 32 + l32;
+    f.aH[m] = p_frag(As, r, h);
+    f.aL[m] = p_frag(As, r, 2 + h);
+  }
+#pragma unroll
+  for (int nn = 0; nn < 2; ++nn) {
+    const int r = wc * 64 + nn * 32 + l32;
+    f.bH[nn] = p_frag(Bs, r, h);
+    f.bL[nn] = p_frag(Bs, r, 2 + h);
+  }
+}
+
+__device__ inline void p_mfma(const PFrag& f, f32x16 (&acc)[4][2]) {
+#if VR_GRAM_PRIO
+  __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn)
+      acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.aH[m], f.bH[nn], acc[m][nn], 0, 0, 0);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn)
+      acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.aH[m], f.bL[nn], acc[m][nn], 0, 0, 0);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn)
+      acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.aL[m], f.bH[nn], acc[m][nn], 0, 0, 0);
+#if VR_GRAM_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
+// Iteration q: sub-stage q's fragments are already in registers (cur); wait for this wave's
+// loads of q+1 (q+2 stays in flight), barrier, issue q+3 into the slot sub-stage q-1 used,
+// start the LDS reads of q+1 into nxt, then the 24 MFMAs of q, which do not wait for them.
+template <bool DIAG>
+__device__ inline void gram3p_step(const GramParams& P, char* lds, int64_t row0, int64_t col0, int q, int Q,
+                                   const PFrag& cur, PFrag& nxt, f32x16 (&acc)[4][2]) {
+  constexpr int PER = DIAG ? 2 : 4;  // glds per wave per sub-stage
+  if (q + 1 < Q) {
+    if (q + 2 < Q)
+      p_wait<PER>();
+    else
+      p_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (q + 3 < Q) {
+      char* slot = lds + ((q + 3) & (P_SLOTS - 1)) * P_SLOT;
+      p_issue(P, slot, row0, q + 3);
+      if (!DIAG) p_issue(P, slot + P_PANEL, col0, q + 3);
+    }
+    const char* As = lds + ((q + 1) & (P_SLOTS - 1)) * P_SLOT;
+    p_read(As, DIAG ? As : As + P_PANEL, nxt);
+  }
+  p_mfma(cur, acc);
+  // every P.flush stages (the same two-level sum as k_gram3w); its global loads and stores
+  // drain this wave's loads in flight (the compiler waits vmcnt(0)): correct, and rare
+  if (P.flush && (q & 1) && q + 1 < Q && ((q >> 1) + 1) % P.flush == 0) {
+    const int wid = threadIdx.x >> 6;
+    gram_flush<WT>(acc, P.fbuf + (size_t)blockIdx.x * WT * WT, (wid >> 2) * 128, (wid & 3) * 64,
+                   (q >> 1) + 1 == P.flush);
+  }
+}
+
+template <bool DIAG>
+__device__ inline void gram3p_loop(const GramParams& P, char* lds, int64_t row0, int64_t col0,
+                                   f32x16 (&acc)[4][2]) {
+  const int Q = 2 * (int)P.nstage;  // even
+  for (int q = 0; q < 3 && q < Q; ++q) {
+    char* slot = lds + q * P_SLOT;
+    p_issue(P, slot, row0, q);
+    if (!DIAG) p_issue(P, slot + P_PANEL, col0, q);
+  }
+  // sub-stage 0 landed: loads of 1 and 2 may stay in flight
+  if (Q > 2)
+    p_wait<DIAG ? 4 : 8>();
+  else if (Q > 1)
+    p_wait<DIAG ? 2 : 4>();
+  else
+    p_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  PFrag f0, f1;
+  p_read(lds, DIAG ? lds : lds + P_PANEL, f0);
+  for (int q = 0; q < Q; q += 2) {  // two sub-stages per trip: the fragment sets swap roles
+    gram3p_step<DIAG>(P, lds, row0, col0, q, Q, f0, f1, acc);
+    gram3p_step<DIAG>(P, lds, row0, col0, q + 1, Q, f1, f0, acc);
+  }
+}
+
+__global__ __launch_bounds__(W_THREADS, 1) void k_gram3p(GramParams P) {
+  __shared__ __attribute__((aligned(16))) char lds[P_SLOTS * P_SLOT];
+  const int id = P.blk0 + (int)xcd_remap(blockIdx.x, (uint32_t)gridDim.x);
+  int bi, bj;
+  band_tile(id, 0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension here
+  const bool diag = (bi == bj);
+  const int64_t row0 = (int64_t)bi * WT, col0 = (int64_t)bj * WT;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  (void)lane;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+  if (diag)
+    gram3p_loop<true>(P, lds, row0, col0, acc);
+  else
+    gram3p_loop<false>(P, lds, row0, col0, acc);
+  if (P.flush && (int)P.nstage > P.flush)
+    gram_unflush<WT>(acc, P.fbuf + (size_t)blockIdx.x * WT * WT, wr * 128, wc * 64);
+  gram_store_w(P, acc, row0, col0, diag);
+}
+
+// VISREPS_GRAM_PIPE=0: the register-staged k_gram3w (A/B timing)
+static bool gram_pipe() {
+  const char* e = getenv("VISREPS_GRAM_PIPE");
+  return !(e && strcmp(e, "0") == 0);
+}
+
 // Sums the split partials of one tile in split order and applies the epilogue; the
 // mirror half goes through an LDS transpose so both writes are row-coalesced.
 __global__ __launch_bounds__(256) void k_gram_reduce(GramParams P) {
@@ -1205,10 +1384,14 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   W.tile_count = (int)tri_start(R, W.T);
   W.splits = 1;
   const int gen = num_cus();
+  const bool pipe = gram_pipe();
   W.flush = (size_t)gen * WT * WT <= gram_fbuf_floats() ? flush_stages : 0;
   for (int b0 = 0; b0 < W.tile_count; b0 += gen) {
     W.blk0 = b0;
-    k_gram3w<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
+    if (pipe)
+      k_gram3p<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
+    else
+      k_gram3w<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
     VR_CHECK_LAUNCH();
   }
   const int64_t t0 = tri_start(2 * (int64_t)R, P.T);
