@@ -11,13 +11,17 @@
 //                   per input feature, so a nonzero's batch column is one coalesced row
 //  k_srp_spmm       a workgroup owns 64 output features x 64 batch rows; each wave walks
 //                   16 CSR rows (index/value loads are wave-uniform s_loads), lane = batch
-//                   row, fp32 fma in CSR order; the tile is transposed through LDS so the
+//                   row, SRP_U row loads in flight, fp32 fma in CSR order; the tile is transposed through LDS so the
 //                   (B x k) output is written in 256-byte rows.
 #include "internal.h"
 
 namespace vr {
 
 constexpr int SRP_T = 64;
+#ifndef VR_SRP_U
+#define VR_SRP_U 16
+#endif
+constexpr int SRP_U = VR_SRP_U;  // nonzeros per batch of row loads
 
 __global__ __launch_bounds__(256) void k_srp_transpose(const float* __restrict__ X, int64_t B,
                                                        int64_t D, int64_t ldx, int64_t Bp,
@@ -58,15 +62,12 @@ __global__ __launch_bounds__(256) void k_srp_spmm(const int32_t* __restrict__ in
     if (r < k) {
       const int32_t j0 = srp_sload(indptr + r), j1 = srp_sload(indptr + r + 1);
       int32_t j = j0;
-      for (; j + 4 <= j1; j += 4) {  // four independent row loads in flight
-        const float x0 = xt[(int64_t)srp_sload(indices + j) * Bp];
-        const float x1 = xt[(int64_t)srp_sload(indices + j + 1) * Bp];
-        const float x2 = xt[(int64_t)srp_sload(indices + j + 2) * Bp];
-        const float x3 = xt[(int64_t)srp_sload(indices + j + 3) * Bp];
-        acc = __builtin_fmaf(srp_sload(vals + j), x0, acc);
-        acc = __builtin_fmaf(srp_sload(vals + j + 1), x1, acc);
-        acc = __builtin_fmaf(srp_sload(vals + j + 2), x2, acc);
-        acc = __builtin_fmaf(srp_sload(vals + j + 3), x3, acc);
+      for (; j + SRP_U <= j1; j += SRP_U) {  // SRP_U independent row loads in flight, then the
+        float x[SRP_U];                      // fmas in CSR order
+#pragma unroll
+        for (int u = 0; u < SRP_U; ++u) x[u] = xt[(int64_t)srp_sload(indices + j + u) * Bp];
+#pragma unroll
+        for (int u = 0; u < SRP_U; ++u) acc = __builtin_fmaf(srp_sload(vals + j + u), x[u], acc);
       }
       for (; j < j1; ++j) acc = __builtin_fmaf(srp_sload(vals + j), xt[(int64_t)srp_sload(indices + j) * Bp], acc);
     }

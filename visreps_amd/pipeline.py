@@ -272,8 +272,10 @@ def gather_point_async(x_local: torch.Tensor, n: int, pg, correction: float = 1e
         return finish_rows
     planes, mean, std = K.split_rows(x_local, correction)
     stats = torch.stack([mean, std], dim=1)
-    # plane records travel as bytes (RCCL and gloo have no 16-bit integer type)
-    w1, pfull, s1 = _all_gather_padded(planes.view(torch.uint8), sizes, pg, async_op=True)
+    # plane records travel as 8-byte words (RCCL and gloo have no 16-bit integer type; a
+    # row is nstage x 128 B, and 8-B elements keep the element count of a 10k x 290,400
+    # point (11.6 GB) below 2^31)
+    w1, pfull, s1 = _all_gather_padded(planes.view(torch.int64), sizes, pg, async_op=True)
     w2, sfull, s2 = _all_gather_padded(stats, sizes, pg, async_op=True)
 
     def finish_planes(_keep=(s1, s2)) -> _Gathered:
