@@ -183,7 +183,7 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    pg = None
+    pg = feat_pg = None
     if world > 1:
         # RCCL (backend "nccl") over xGMI; VISREPS_DIST_BACKEND=gloo only rehearses the
         # orchestration when ranks share a GPU (RCCL refuses two ranks on one device)
@@ -193,6 +193,8 @@ def main():
         else:
             dist.init_process_group(backend)
         pg = dist.group.WORLD
+        # the feature-plane exchange gets its own communicator (PrefetchedRDMs.start_all)
+        feat_pg = dist.new_group(list(range(world)))
     N = args.n
     rows = shard_rows(N, rank, world)
 
@@ -224,16 +226,19 @@ def main():
         ev[0].record()
         feats = extract(extractor, images, args.batch)
         ev[1].record()
+        # N > 1: every point's plane all-gather starts now, on its own communicator, and
+        # streams under phase 1, the neural RDMs and the model Grams
+        rdms = PrefetchedRDMs(feats, points, N, pg, times, exchange_pg=feat_pg)
+        rdms.start_all()
         sel = phase1_select(feats, projectors, responses, points, N, n_select=1000, seed=42,
                             pg=pg, times=times)
         ev[2].record()
         neural = {r: distributed_rdm(y, N, pg, times) for r, y in responses.items()}
         ev[3].record()
-        res = all_units_rsa(PrefetchedRDMs(feats, points, N, pg, times), points, neural,
-                            N, n_boot=args.boot, seed=42, pg=pg, times=times)
+        res = all_units_rsa(rdms, points, neural, N, n_boot=args.boot, seed=42, pg=pg, times=times)
         ev[4].record()
         times.phases(["extract", "phase1", "neural_rdms", "units"], ev)
-        del feats
+        del feats, rdms
         return res, neural, sel
 
     for w in range(args.warmup):

@@ -164,8 +164,12 @@ def _worker(rank, world, port, n, d, n_boot, out_dir):
     X, Y, Z = _data(n, d)
     rows = shard_rows(n, rank, world)
     loc = {k: torch.from_numpy(v[rows.start:rows.stop]) for k, v in {"x": X, "y": Y, "z": Z}.items()}
+    # as bench.py: every point's plane exchange in flight on its own group while the other
+    # collectives (neural RDMs, tile ranges, scores) run on pg
+    feat_pg = dist.new_group(list(range(world)))
+    src = P.PrefetchedRDMs({"x": loc["x"], "z": loc["z"]}, ["x", "z"], n, pg, kernels=K, exchange_pg=feat_pg)
+    src.start_all()
     rdm_y = P.distributed_rdm(loc["y"], n, pg, kernels=K)
-    src = P.PrefetchedRDMs({"x": loc["x"], "z": loc["z"]}, ["x", "z"], n, pg, kernels=K)
     res = P.all_units_rsa(src, ["x", "z"], {"r0": rdm_y, "r1": P.distributed_rdm(loc["x"], n, pg, kernels=K)},
                           n, n_boot=n_boot, seed=42, pg=pg)
     assert not src.pending

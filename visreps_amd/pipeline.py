@@ -336,17 +336,29 @@ class PrefetchedRDMs:
     points[i] first starts the exchange of points[i + 1] (gather_point_async), so the next
     point's plane all-gather overlaps this point's Gram. Every rank asks for the points in
     the same order (all_units_rsa walks `points`), so the collectives are issued in one
-    order."""
+    order.
+
+    exchange_pg: a second process group (its own RCCL communicator and stream) for the
+    plane all-gathers. With it, start_all() issues every point's exchange at once: they
+    stream over xGMI while phase 1, the neural RDMs and the first points' Grams run, and
+    the collectives on `pg` (phase-1 rows, packed tile ranges, scores) do not queue
+    behind them. All ranks call start_all() at the same point of the step."""
 
     def __init__(self, feats: Dict[str, torch.Tensor], points: Sequence[str], n: int, pg=None,
-                 times: Optional[StepTimes] = None, kernels: RdmKernels = None):
+                 times: Optional[StepTimes] = None, kernels: RdmKernels = None, exchange_pg=None):
         self.feats, self.points, self.n, self.pg, self.times = feats, list(points), n, pg, times
         self.kernels = kernels or KERNELS
+        self.exchange_pg = exchange_pg if exchange_pg is not None else pg
         self.pending: Dict[str, Callable[[], _Gathered]] = {}
 
     def _start(self, p: str) -> None:
         if p not in self.pending:
-            self.pending[p] = gather_point_async(self.feats[p], self.n, self.pg, kernels=self.kernels)
+            self.pending[p] = gather_point_async(self.feats[p], self.n, self.exchange_pg, kernels=self.kernels)
+
+    def start_all(self) -> None:
+        if _world(self.pg)[1] > 1:
+            for p in self.points:
+                self._start(p)
 
     def __call__(self, p: str) -> torch.Tensor:
         if _world(self.pg)[1] == 1:  # one GPU: the single-launch RDM (no exchange, no prepass split)
