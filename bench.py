@@ -86,12 +86,12 @@ def pmc_traffic():
     gfx950 correction, calibrated for these 128-B row gathers in
     profiles/r2_fetch_calibration.json) + WRITE_SIZE, per unit. A PMC pass cannot share
     this timed run, so the figure comes from that separate profile."""
-    path = os.path.join(ROOT, "profiles", "r2_pmc_engine.json")
+    path = os.path.join(ROOT, "profiles", "r2_pmc_engine_est3.json")
     try:
         with open(path) as f:
             d = json.load(f)
         return round(float(d["bytes_per_unit"])), (
-            f"profiles/r2_pmc_engine.json: {d['source']}")
+            f"profiles/r2_pmc_engine_est3.json: {d['source']}")
     except (OSError, KeyError, ValueError):
         return None, None
 
@@ -274,17 +274,25 @@ def main():
         ref_gbs = times.engine_ref_bytes / (times.engine_ms / 1e3) / 1e9 if times.engine_ms else 0.0
         gram_tf = times.gram_flops / (times.gram_ms / 1e3) / 1e12 if times.gram_ms else 0.0
         traffic, tsrc = pmc_traffic()
-        form = "EST" if os.environ.get("VISREPS_ENGINE_EST") == "1" else "exact chunk-base"
+        est = os.environ.get("VISREPS_ENGINE_EST") != "0"
+        form = ("EST (pass 0, holding the full set, in the exact chunk-base form)" if est
+                else "exact chunk-base")
         roof = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(eng_gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
                 "kernel": (f"bootstrap engine call ({form} form; vr_bootstrap_spearman_multi: per pass of "
                            "64 subsets one A-side rank walk of the neural plan + one B-side walk per "
                            "model plan; k_rankB dominates)"),
                 "algorithmic_bytes_per_unit": round(times.engine_bytes / calls),
-                "algorithmic_bytes_model": ("per pair: A walk 4 B codes + 128 B TB row write per pass "
-                                            "(shared by the call's units), B walk 4+4+4 B streams + 128 B "
-                                            "TB row gather per pass and unit (the 256-B chunk-base rows "
-                                            "are L2-resident), join 20 B per unit"),
+                "algorithmic_bytes_model": (("per pair: EST passes: A side 4+4 B codes (count pre-pass "
+                                             "+ rank walk) + 128 B TB row write per pass (shared by the "
+                                             "call's units), B walk 4+4 B streams + 128 B TB row gather "
+                                             "per pass and unit; pass 0 exact: A 4 + 128 B, B 4+4+4 + "
+                                             "128 B (chunk-base rows L2-resident); join 20 B per unit")
+                                            if est else
+                                            ("per pair: A walk 4 B codes + 128 B TB row write per pass "
+                                             "(shared by the call's units), B walk 4+4+4 B streams + 128 B "
+                                             "TB row gather per pass and unit (the 256-B chunk-base rows "
+                                             "are L2-resident), join 20 B per unit")),
                 "avg_unit_ms": round(unit_ms, 3),
                 "reference_equivalent_gbs": round(ref_gbs, 1),
                 "reference_equivalent_note": ("SURVEY §8(d) bytes (both fp32 triangles read once per "

@@ -10,6 +10,7 @@ if os.environ.get("ALT_LIB"):
     _L.LIB_PATH = os.environ["ALT_LIB"]
 from bench import LAYERS, extract
 from visreps_amd.analysis import rsa as R
+from visreps_amd import _lib
 from visreps_amd.analysis._random import bootstrap_indices
 from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_responses
 from visreps_amd.models.custom_model import CustomCNN
@@ -35,5 +36,12 @@ for _ in range(int(os.environ.get("REPS", 2))):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(); s = R.bootstrap_spearman_multi(neural, models, idx); b.record(); torch.cuda.synchronize()
     ts.append(a.elapsed_time(b))
+ref_note = ""
+if os.environ.get("CHECK_EXACT", "1") == "1" and os.environ.get("VISREPS_ENGINE_EST") == "1":
+    os.environ["VISREPS_ENGINE_EST"] = "0"  # the same RDMs in the exact form, same process
+    ref = R.bootstrap_spearman_multi(neural, models, idx)
+    os.environ["VISREPS_ENGINE_EST"] = "1"
+    ref_note = f" exact_equal={bool(torch.equal(ref, s))} max_diff={float((ref - s).abs().max()):.3g}"
 print(f"engine bench-RDMs NB={len(models)}: {min(ts) / len(models):.2f} ms/unit  "
-      f"checksum={float(s.double().sum()):.15g}", flush=True)
+      f"checksum={float(s.double().sum()):.15g} est_reruns={int(_lib.lib().vr_engine_est_reruns())}{ref_note}",
+      flush=True)

@@ -2,9 +2,12 @@
 form and the CPU oracle.
 
 EST keeps each pair's absolute doubled A rank modulo 2^16 and recovers it on the B side
-from an interpolated count table; a pass whose ranks cannot be recovered is re-run in the
-exact form. Both forms are exact integer arithmetic, so scores must agree bit for bit
-(VISREPS_ENGINE_EST=1 selects the EST form, =0 the exact form, for every pass).
+from an estimate of the included-pair count (EST 3, the default: one wave-uniform linear
+estimate, the pass holding the full set run exact; EST 1: an interpolated per-lane table in
+LDS; EST 2: a per-lane linear estimate); a pass whose ranks cannot be recovered is re-run
+in the exact form. Both forms are exact integer arithmetic, so scores must agree bit for bit
+(VISREPS_ENGINE_EST=1 selects the EST form, =0 the exact form, for every pass;
+VISREPS_ENGINE_EST_MODE the estimate).
 """
 import os
 
@@ -116,3 +119,19 @@ def test_est_giant_tie_groups_fall_back_to_exact(dev):
         i = np.asarray(idx[s])
         ref_s = O.compute_rdm_correlation(a[np.ix_(i, i)], b[np.ix_(i, i)], "Spearman")
         assert abs(est[1 + s] - ref_s) <= 1e-12
+
+
+@pytest.mark.parametrize("mode", ["1", "2", "3"])
+def test_est_modes_equal_exact_form(dev, mode, monkeypatch):
+    # every estimate form, a partial last pass (201 subsets: lanes 9..63 hold no subset)
+    monkeypatch.setenv("VISREPS_ENGINE_EST_MODE", mode)
+    n = 2500
+    neural = R.RankPlan(_rdm(dev, n, 120, 21))
+    models = [R.RankPlan(_rdm(dev, n, 90, 22, relu=True)), R.RankPlan(_rdm(dev, n, 300, 23))]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 200)
+    r0 = int(lib().vr_engine_est_reruns())
+    est = R.bootstrap_spearman_multi(neural, models, idx, full_first=True).cpu().numpy()
+    assert int(lib().vr_engine_est_reruns()) == r0, "continuous RDMs must not need the exact re-run"
+    with exact_engine():
+        ref = R.bootstrap_spearman_multi(neural, models, idx, full_first=True).cpu().numpy()
+    assert np.array_equal(est, ref)

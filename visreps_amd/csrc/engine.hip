@@ -68,24 +68,22 @@ static std::atomic<int64_t> g_est_reruns{0};  // passes re-run in the exact form
 // boundary; the 4096 steps are whole positions) with ceil(M / 2^b) <= 96, or, for larger
 // triangles, <= EST_NC (a step of 2^(b-12) positions moves lo by <= 2^(b-11): b <= 23
 // keeps that at a few thousand of the 2^15 of slack).
-static int est_bits(int64_t M) {
+// maxrows < EST_NC: the table must fit beside the masks in LDS (fewer, longer intervals).
+static int est_bits(int64_t M, uint32_t maxrows = EST_NC) {
   int b = 12;
   while (((M + ((int64_t)1 << b) - 1) >> b) > 96 && b < 23) ++b;
-  while (((M + ((int64_t)1 << b) - 1) >> b) > EST_NC) ++b;
+  while (((M + ((int64_t)1 << b) - 1) >> b) > (int64_t)maxrows && b < 31) ++b;
   return b;
 }
 static uint32_t est_intervals(int64_t M, int b) { return (uint32_t)((M + ((int64_t)1 << b) - 1) >> b); }
-static size_t est_table_bytes(int64_t M) {
-  return M > 0 ? (size_t)est_intervals(M, est_bits(M)) * LANES * sizeof(uint2) : 0;
-}
 
-// EST form only with VISREPS_ENGINE_EST=1. Measured in the bench (profiles/r2_engine_ab.log):
-// the exact form's k_rankB runs 1.90 ms per pass at two workgroups per CU; the EST form's
-// 1.94-2.04 ms (its saved chunk-base gather is paid back in per-pair VALU/SALU work and in
-// the L2 mask reads it needs for the same occupancy), so the exact form is the default.
+// EST form by default (VISREPS_ENGINE_EST=0: every pass exact). Measured on the bench RDMs
+// (profiles/r2_engine_est3.log): k_rankB 1.56 ms per pass in EST 3 against 1.96 ms in the
+// exact form. The table form (EST 1) and the masks-from-L2 variants measured 1.86-2.04 ms
+// (profiles/r2_engine_ab.log): their per-pair table reads cost what the base gather saved.
 static bool engine_est() {
   const char* e = getenv("VISREPS_ENGINE_EST");
-  return e && strcmp(e, "1") == 0;
+  return !(e && strcmp(e, "0") == 0);
 }
 
 // Launch shape. The walks are bound by the latency of their random TB gathers, so they run
@@ -97,13 +95,24 @@ struct EngineCfg {
   int nwaves;    // grid * WAVES_PER_WG = number of chunk segments (A and B each)
   bool use_lds;  // exact kernels, k_countA: masks in LDS
   size_t lds;    // their dynamic LDS (the masks, or 0)
-  size_t tab;    // EST rank walks: dynamic LDS = the interval table
+  // EST passes (every kernel of one EST pass uses these; est_nwaves <= nwaves)
+  bool est_lds;   // EST rank walks: masks in LDS beside the table (else masks from L2)
+  int est_grid, est_nwaves;
+  int est_mode;       // 1: interval table in LDS, 2: one linear interval in registers
+  int est_b;          // log2 of the table interval
+  uint32_t est_rows;  // table rows (intervals)
+  size_t tab;         // EST rank walks' dynamic LDS: [masks] + table
 };
+
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
 
 static EngineCfg engine_cfg(int64_t n) {
   EngineCfg c;
+  const int64_t M = pairs_of(n);
   const size_t need = (size_t)n * sizeof(uint64_t);
-  c.tab = est_table_bytes(pairs_of(n));
   const size_t cap = 160 * 1024 - 1024;
   const char* e = getenv("VISREPS_ENGINE_MASKS");  // "global": masks from L2 (A/B timing)
   c.use_lds = need <= cap && !(e && strcmp(e, "global") == 0);
@@ -111,6 +120,24 @@ static EngineCfg engine_cfg(int64_t n) {
   const int per_cu = std::max<int>(1, std::min<int>(2048 / ENG_THREADS, (int)(cap / std::max<size_t>(c.lds, 1))));
   c.grid = num_cus() * per_cu;
   c.nwaves = c.grid * WAVES_PER_WG;
+  // EST: masks and table both in LDS when the table gets >= 1 row beside the masks at
+  // VISREPS_ENGINE_EST_WG workgroups per CU (default 2, the exact form's occupancy);
+  // otherwise masks from L2 and the table alone in LDS.
+  const size_t row = (size_t)LANES * sizeof(uint2);
+  const int est_wg = std::max(1, std::min(per_cu, env_int("VISREPS_ENGINE_EST_WG", per_cu)));
+  const size_t per_wg = cap / est_wg;
+  c.est_lds = c.use_lds && env_int("VISREPS_ENGINE_EST_LDS", 1) != 0 && per_wg >= need + row;
+  // VISREPS_ENGINE_EST_LIN=1: one linear interval (EST 2), no table in LDS
+  c.est_mode = std::max(1, std::min(3, env_int("VISREPS_ENGINE_EST_MODE", 3)));
+  if (c.est_mode >= 2) c.est_lds = c.use_lds && env_int("VISREPS_ENGINE_EST_LDS", 1) != 0 && per_wg >= need;
+  uint32_t rows_fit =
+      c.est_lds ? (uint32_t)std::min<size_t>(EST_NC, (per_wg - need) / row) : (uint32_t)EST_NC;
+  if (c.est_mode >= 2) rows_fit = 1;
+  c.est_b = est_bits(M, rows_fit);
+  c.est_rows = M > 0 ? est_intervals(M, c.est_b) : 0;
+  c.est_grid = c.est_lds ? num_cus() * est_wg : c.grid;
+  c.est_nwaves = c.est_grid * WAVES_PER_WG;
+  c.tab = (c.est_lds ? need : 0) + (c.est_mode == 1 ? (size_t)c.est_rows * row : 0);
   return c;
 }
 
@@ -298,6 +325,45 @@ __device__ inline uint32_t est_recover(uint32_t v, uint32_t lo) { return lo + (u
 // EST: true if y is outside the window [lo, lo + 2^16)
 __device__ inline bool est_bad(uint32_t y, uint32_t lo) { return y - lo > 65535u; }
 
+// The window low end of either EST form. EST 1: the interpolated interval table (LDS).
+// EST 2 (one interval over the whole triangle): lo = trunc(fma(R, pos, L)) in f32 from two
+// per-lane registers, R = 2 M'/M and L = 1 - 2^15 (k_c0_lin): no table read per pair.
+// Both are deterministic and monotone non-decreasing in pos (the A side checks only the
+// ends of a group), and the A and B walks evaluate the same function.
+// EST 3 (every active lane a subset of the same size, so one included-pair total M' for
+// the wave): lo = L + (2 pos R >> 32), R = floor(2^32 M'/M), L = 1 - 2^15: wave-uniform,
+// scalar arithmetic (s_mul_hi_u32), no per-lane work besides the 16-bit recovery.
+struct EstLo {
+  const uint2* tab;
+  int bits;
+  float L, R;
+  uint32_t Lu, Ru;
+};
+template <int EST>
+__device__ inline uint32_t est_lo_t(const EstLo& e, uint32_t pos, int lane) {
+  if constexpr (EST == 3)
+    return e.Lu + __umulhi(pos << 1, e.Ru);
+  else if constexpr (EST == 2)
+    return (uint32_t)(int32_t)__builtin_fmaf(e.R, (float)pos, e.L);
+  else
+    return est_lo(e.tab, pos, lane, e.bits);
+}
+template <int EST>
+__device__ inline EstLo est_setup(const uint2* __restrict__ gtab, uint32_t rows, int bits, uint2* smem) {
+  EstLo e{nullptr, bits, 0.f, 0.f, 0u, 0u};
+  if constexpr (EST == 3) {
+    e.Lu = wave_uniform(sload(&gtab->x));
+    e.Ru = wave_uniform(sload(&gtab->y));
+  } else if constexpr (EST == 2) {
+    const uint2 v = gtab[threadIdx.x & 63];
+    e.L = __uint_as_float(v.x);
+    e.R = __uint_as_float(v.y);
+  } else if constexpr (EST == 1) {
+    e.tab = stage_table(gtab, rows, smem);
+  }
+  return e;
+}
+
 // ---------------------------------------------------------------------------------
 // EST pre-pass: included pairs per A segment (for the absolute ranks of k_rankA<EST>)
 // and the segment-relative count at every coarse boundary inside the segment
@@ -362,6 +428,20 @@ __global__ void k_c0(const uint32_t* __restrict__ c0rel, const uint32_t* __restr
   ftab[(size_t)c * LANES + lane] = make_uint2(2u * a + 1u - 32768u, (uint32_t)((2 * d) >> EST_STEP_BITS));
 }
 
+// EST 3: the wave-uniform estimate {L, R} from lane 0's included-pair total (every active
+// lane of the pass has the same); R = floor(2^32 M'/M) < 2^32 as M' < M
+__global__ void k_c0_u(const uint32_t* __restrict__ total, int64_t M, uint2* __restrict__ ftab) {
+  const uint64_t r = ((uint64_t)total[0] << 32) / (uint64_t)M;
+  ftab[0] = make_uint2(1u - 32768u, (uint32_t)(r > 0xffffffffull ? 0xffffffffull : r));
+}
+
+// EST 2: the one-interval estimate {L, R} per lane (f32 bit patterns in ftab row 0)
+__global__ void k_c0_lin(const uint32_t* __restrict__ total, int64_t M, uint2* __restrict__ ftab) {
+  const int lane = threadIdx.x;
+  const float R = (float)(2.0 * (double)total[lane] / (double)M);
+  ftab[lane] = make_uint2(__float_as_uint(1.0f - 32768.0f), __float_as_uint(R));
+}
+
 // ---------------------------------------------------------------------------------
 // A pass
 // ---------------------------------------------------------------------------------
@@ -372,17 +452,18 @@ struct EstA {
   uint32_t tabrows;
   int bits;
   uint32_t* viol;          // this pass's flag: some stored rank is not recoverable
+  int nl;                  // lanes holding a subset (the others have no included pair)
 };
 
 // rows [r0, r0 + cnt) of TB get y mod 2^16 (EST); bad |= some row's y is not recoverable.
 // lo is monotone in the position, so the group's two end rows bound the rest.
+template <int EST>
 __device__ inline void store_rows_est(uint16_t* __restrict__ TB, uint32_t stride, uint32_t r0,
-                                      uint32_t cnt, int lane, uint32_t y, const uint2* tab,
-                                      int bits, bool& bad) {
+                                      uint32_t cnt, int lane, uint32_t y, const EstLo& el, bool& bad) {
   if (cnt == 0) return;
   // a group inside one 64-position window is covered by that window's check (k_rankA)
   if (VR_EST_CHECK && (r0 >> 6) != ((r0 + cnt - 1u) >> 6))
-    bad |= est_bad(y, est_lo(tab, r0, lane, bits)) || est_bad(y, est_lo(tab, r0 + cnt - 1u, lane, bits));
+    bad |= est_bad(y, est_lo_t<EST>(el, r0, lane)) || est_bad(y, est_lo_t<EST>(el, r0 + cnt - 1u, lane));
   uint16_t* row = TB + (size_t)r0 * stride + lane;
   uint32_t i = 0;
   for (; i + 4 <= cnt; i += 4, row += 4 * (size_t)stride) {
@@ -397,7 +478,7 @@ __device__ inline void store_rows_est(uint16_t* __restrict__ TB, uint32_t stride
 // A side. Exact form (EST false): chunk-relative doubled ranks y - 2 lp (u16 or u32) and
 // the chunk-start counts lpA for baseA. EST form: absolute doubled ranks modulo 2^16,
 // each checked against the count estimate the B side will use.
-template <bool LDS, bool FULL, typename TBT, bool BIGT, bool EST>
+template <bool LDS, bool FULL, typename TBT, bool BIGT, int EST>
 __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
@@ -407,14 +488,14 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
   static_assert(!EST || sizeof(TBT) == 2, "EST ranks are u16");
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
-  const uint2* tab = nullptr;
-  if constexpr (EST) tab = stage_table(est.ftab, est.tabrows, reinterpret_cast<uint2*>(smask + (LDS ? n : 0)));
+  EstLo el{nullptr, 0, 0.f, 0.f, 0u, 0u};
+  if constexpr (EST != 0)
+    el = est_setup<EST>(est.ftab, est.tabrows, est.bits, reinterpret_cast<uint2*>(smask + (LDS ? n : 0)));
   const int lane = threadIdx.x & 63;
   const bool active = FULL || lane < lw;
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
   const uint32_t wave = wave_uniform(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
   const Segment sg = my_segment(nchunks, nseg, wave);
-  const int bits = EST ? est.bits : 0;
 
   uint64_t tie = 0;  // sum over groups of k^3 - k (k < 2^16)
   u128 tie_big = 0;  //   (k >= 2^16)
@@ -439,8 +520,8 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
       tie_add<BIGT>(tie, tie_big, ce - cgs);
       if (active) {
         if constexpr (EST)
-          store_rows_est(reinterpret_cast<uint16_t*>(TB), stride, gs, xe - gs, lane, y0 + cgs + ce + 1u,
-                         tab, bits, bad);
+          store_rows_est<EST>(reinterpret_cast<uint16_t*>(TB), stride, gs, xe - gs, lane, y0 + cgs + ce + 1u,
+                              el, bad);
         else
           store_rows<FULL, TBT>(TB, stride, gs, xe - gs, lane, (TBT)(cgs + ce + 1u - 2u * lp));
       }
@@ -468,7 +549,7 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
         // groups are checked where they close.
         if (VR_EST_CHECK) {
           const uint32_t Y0 = y0 + 2u * cw + 1u;
-          bad |= est_bad(Y0, est_lo(tab, w0 + 63u, lane, bits)) || est_bad(Y0 + 128u, est_lo(tab, w0, lane, bits));
+          bad |= est_bad(Y0, est_lo_t<EST>(el, w0 + 63u, lane)) || est_bad(Y0 + 128u, est_lo_t<EST>(el, w0, lane));
         }
       }
       if (w0 + 64 < P1) {
@@ -511,7 +592,7 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
   seg_part[PA_TIEL * fs + o] = (uint64_t)t;
   seg_part[PA_TIEH * fs + o] = (uint64_t)(t >> 64);
   if constexpr (EST) {
-    if (__ballot(bad) != 0 && lane == 0) *est.viol = 1u;  // benign race: every writer stores 1
+    if (__ballot(bad && lane < est.nl) != 0 && lane == 0) *est.viol = 1u;  // benign race: every writer stores 1
   }
 }
 
@@ -718,19 +799,59 @@ __device__ inline void gather_wait_t(uint32_t t[EBB]) {
 #ifndef VR_EST_ASM
 #define VR_EST_ASM 1  // 0: plain loads (the compiler places the waits)
 #endif
+#ifndef VR_EST_D16
+#define VR_EST_D16 0  // 1: two pairs' u16 entries per VGPR (short_d16 / short_d16_hi loads)
+#endif
+
+// EST, d16: wait for all of this wave's loads; ties the EBB / 2 packed registers
+__device__ inline void gather_wait_t16(uint32_t p[EBB / 2]) {
+  if constexpr (EBB == 8) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3]) : : "memory");
+  } else if constexpr (EBB == 16) {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3]), "+v"(p[4]), "+v"(p[5]), "+v"(p[6]),
+                   "+v"(p[7])
+                 :
+                 : "memory");
+  } else {
+    wait_tie16(p, true);
+  }
+}
+
+// EST, d16: pairs j0 + 2i and j0 + 2i + 1 land in the low / high half of t[i], so a batch
+// of EBB pairs in flight holds EBB / 2 VGPRs
+__device__ inline void gather_issue_t16(const uint16_t* __restrict__ TB, uint32_t stride, uint32_t pa,
+                                        uint32_t j0, uint32_t lane_bt, uint32_t t[EBB / 2]) {
+#pragma unroll
+  for (int q = 0; q < EBB / 2; ++q) {
+    const char* r0 = reinterpret_cast<const char*>(TB) + (size_t)readlane_u32(pa, j0 + 2 * q) * (stride * 2);
+    const char* r1 = reinterpret_cast<const char*>(TB) + (size_t)readlane_u32(pa, j0 + 2 * q + 1) * (stride * 2);
+    asm volatile("global_load_short_d16 %0, %1, %2" VR_TB_CACHE : "=v"(t[q]) : "v"(lane_bt), "s"(r0) : "memory");
+    asm volatile("global_load_short_d16_hi %0, %1, %2" VR_TB_CACHE : "+v"(t[q]) : "v"(lane_bt), "s"(r1) : "memory");
+  }
+}
 
 // EST: yA of the window's 64 pairs (TB row entry + the window low end from the LDS table),
 // EBB pairs per batch, handed to fn(h, ya[EBB]). The batch's loads are waited for right
 // after they are issued (no compiler code between the asm issue and the asm wait, which
 // could otherwise read the destination registers before the data lands); the window
 // low ends are computed after the wait.
-template <typename Fn>
-__device__ inline void gather_window_est(const uint16_t* __restrict__ TB, uint32_t stride, const uint2* tab,
-                                         int bits, uint32_t pa, uint32_t lane_bt, int lane, Fn&& fn) {
+template <int EST, typename Fn>
+__device__ inline void gather_window_est(const uint16_t* __restrict__ TB, uint32_t stride, const EstLo& el,
+                                         uint32_t pa, uint32_t lane_bt, int lane, Fn&& fn) {
 #pragma unroll
   for (int h = 0; h < 64 / EBB; ++h) {
     uint32_t t[EBB];
-    if constexpr (VR_EST_ASM) {
+    if constexpr (VR_EST_D16 && EBB >= 8) {
+      uint32_t p[EBB / 2];
+      gather_issue_t16(TB, stride, pa, h * EBB, lane_bt, p);
+      gather_wait_t16(p);
+#pragma unroll
+      for (int q = 0; q < EBB / 2; ++q) {
+        t[2 * q] = p[q];  // est_recover uses only the low 16 bits
+        t[2 * q + 1] = p[q] >> 16;
+      }
+    } else if constexpr (VR_EST_ASM) {
       gather_issue_t(TB, stride, pa, h * EBB, lane_bt, t);
       gather_wait_t(t);
     } else {
@@ -741,7 +862,7 @@ __device__ inline void gather_window_est(const uint16_t* __restrict__ TB, uint32
       }
     }
 #pragma unroll
-    for (int q = 0; q < EBB; ++q) t[q] = est_recover(t[q], est_lo(tab, readlane_u32(pa, h * EBB + q), lane, bits));
+    for (int q = 0; q < EBB; ++q) t[q] = est_recover(t[q], est_lo_t<EST>(el, readlane_u32(pa, h * EBB + q), lane));
     fn(h, t);
   }
 }
@@ -783,7 +904,7 @@ __device__ inline void gather_window(const TBT* __restrict__ TB, const uint32_t*
 
 // B side. Exact form: yA = 2 baseA[chunkA] + TB[posA] (two gathers per pair). EST form:
 // yA recovered from TB[posA] (absolute, modulo 2^16) and the LDS count table (one gather).
-template <bool LDS, bool FULL, typename TBT, bool BIGT, bool EST>
+template <bool LDS, bool FULL, typename TBT, bool BIGT, int EST>
 __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MINW) void k_rankB(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
@@ -796,8 +917,8 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
   constexpr int NB = EST ? EBB : BB;  // pairs per gather batch
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
-  const uint2* tab = nullptr;
-  if constexpr (EST) tab = stage_table(ftab, tabrows, reinterpret_cast<uint2*>(smask + (LDS ? n : 0)));
+  EstLo el{nullptr, 0, 0.f, 0.f, 0u, 0u};
+  if constexpr (EST != 0) el = est_setup<EST>(ftab, tabrows, bits, reinterpret_cast<uint2*>(smask + (LDS ? n : 0)));
   const int lane = threadIdx.x & 63;
   const bool active = FULL || lane < lw;
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
@@ -844,7 +965,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
       auto gather = [&](auto&& fn) {
         if constexpr (EST)
-          gather_window_est(reinterpret_cast<const uint16_t*>(TB), stride, tab, bits, pa_c, lane_bt, lane, fn);
+          gather_window_est<EST>(reinterpret_cast<const uint16_t*>(TB), stride, el, pa_c, lane_bt, lane, fn);
         else
           gather_window<TBT>(TB, baseA, stride, pa_c, ca_c, lane_bt, lane_b4, fn);
       };
@@ -1027,28 +1148,33 @@ static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const
 // A side of a pass, EST form: count pre-pass -> segment bases and the interval table ->
 // absolute u16 ranks in A order (flagging *viol when one is not recoverable). The count
 // pre-pass reads the masks from LDS when they fit (CL), the rank walk from L2.
-template <bool CL, bool FULL, bool BTA>
-static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, const EngineCfg& cfg,
+template <int EM, bool CL, bool FULL, bool BTA>
+static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, int nl, const EngineCfg& cfg,
                       uint32_t* viol, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     VR_TRY(allow_big_lds(k_countA<CL, FULL>));
-    VR_TRY(allow_big_lds(k_rankA<false, FULL, uint16_t, BTA, true>));
+    VR_TRY(allow_big_lds(k_rankA<CL, FULL, uint16_t, BTA, EM>));
     attr = true;
   }
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
-  const uint32_t nseg = (uint32_t)cfg.nwaves;
-  const int bits = est_bits(M);
-  const uint32_t nc = est_intervals(M, bits);
-  k_countA<CL, FULL><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(A.codes, A.gstart, A.chunk_g, nch, E.masks,
-                                                              n, lw, bits, E.c0rel, E.c0seg, E.segA_tot, nseg);
+  const uint32_t nseg = (uint32_t)cfg.est_nwaves;
+  const int bits = cfg.est_b;
+  const uint32_t nc = cfg.est_rows;
+  k_countA<CL, FULL><<<cfg.est_grid, ENG_THREADS, CL ? (size_t)n * sizeof(uint64_t) : 0, st>>>(
+      A.codes, A.gstart, A.chunk_g, nch, E.masks, n, lw, bits, E.c0rel, E.c0seg, E.segA_tot, nseg);
   VR_CHECK_LAUNCH();
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
-  k_c0<<<nc, LANES, 0, st>>>(E.c0rel, E.c0seg, E.segA_pre, E.totA, nc, bits, M, E.ftab);
+  if constexpr (EM == 3)
+    k_c0_u<<<1, 1, 0, st>>>(E.totA, M, E.ftab);
+  else if constexpr (EM == 2)
+    k_c0_lin<<<1, LANES, 0, st>>>(E.totA, M, E.ftab);
+  else
+    k_c0<<<nc, LANES, 0, st>>>(E.c0rel, E.c0seg, E.segA_pre, E.totA, nc, bits, M, E.ftab);
   VR_CHECK_LAUNCH();
-  const EstA est{E.segA_pre, E.ftab, nc, bits, viol};
-  k_rankA<false, FULL, uint16_t, BTA, true><<<cfg.grid, ENG_THREADS, cfg.tab, st>>>(
+  const EstA est{E.segA_pre, E.ftab, nc, bits, viol, nl};
+  k_rankA<CL, FULL, uint16_t, BTA, EM><<<cfg.est_grid, ENG_THREADS, cfg.tab, st>>>(
       A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<uint16_t*>(E.TB), lw, E.lpA,
       E.segA_tot, E.segA_part, nseg, est);
   VR_CHECK_LAUNCH();
@@ -1057,7 +1183,7 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, c
 
 // B side of a pass for one B plan, joined to A by posA_byB (and chunkA_byB in the exact
 // form): the nl scores of the pass.
-template <bool LDS, bool FULL, typename TBT, bool BTB, bool EST>
+template <bool LDS, bool FULL, typename TBT, bool BTB, int EST>
 static int pass_b(const PlanView& A, const PlanView& B, const uint32_t* posA_byB,
                   const uint32_t* chunkA_byB, int64_t n, const EngineWs& E, int lw, int nl,
                   double* scores_out, const EngineCfg& cfg, hipStream_t st) {
@@ -1068,10 +1194,10 @@ static int pass_b(const PlanView& A, const PlanView& B, const uint32_t* posA_byB
   }
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
-  const uint32_t nseg = (uint32_t)cfg.nwaves;
-  const int bits = EST ? est_bits(M) : 0;
-  const uint32_t rows = EST ? est_intervals(M, bits) : 0;
-  k_rankB<LDS, FULL, TBT, BTB, EST><<<cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
+  const uint32_t nseg = (uint32_t)(EST ? cfg.est_nwaves : cfg.nwaves);
+  const int bits = EST ? cfg.est_b : 0;
+  const uint32_t rows = EST ? cfg.est_rows : 0;
+  k_rankB<LDS, FULL, TBT, BTB, EST><<<EST ? cfg.est_grid : cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
       B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
       posA_byB, chunkA_byB, E.baseA, E.segB_tot, E.segB_part, nseg, E.ftab, rows, bits);
   VR_CHECK_LAUNCH();
@@ -1142,7 +1268,9 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
     }
     return VR_OK;
   };
-  VR_TRY(join(!est));
+  // EST 3 runs the pass holding the full set (pass 0 with full_first) in the exact form
+  const bool exact0 = est && cfg.est_mode == 3 && full_first;
+  VR_TRY(join(!est || exact0));
   // the exact chunk-base form of the pass starting at subset set0
   auto exact_pass = [&](auto tag, int64_t set0) -> int {
     using Tg = decltype(tag);
@@ -1168,11 +1296,17 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
     });
   }
   const int64_t npass = (total + lw - 1) / lw;
-  bool chunk_joins = false;
-  for (int64_t p0 = 0; p0 < npass; p0 += EST_MAX_PASSES) {
-    const int64_t p1 = std::min<int64_t>(npass, p0 + EST_MAX_PASSES);
+  bool chunk_joins = exact0;
+  const int64_t pfirst = exact0 ? 1 : 0;
+  if (pfirst) {
+    VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) { return exact_pass(tag, 0); }));
+  }
+  // The first EST pass runs alone: when the estimate cannot hold these A ranks (strongly
+  // structured RDMs, giant tie groups) every pass is run in the exact form from there on.
+  for (int64_t p0 = pfirst, p1 = pfirst; p0 < npass; p0 = p1) {
+    p1 = std::min<int64_t>(npass, p0 == pfirst ? p0 + 1 : p0 + EST_MAX_PASSES);
     VR_CHECK_HIP(hipMemsetAsync(E.viol, 0, (size_t)(p1 - p0) * sizeof(uint32_t), st));
-    VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, true, [&](auto tag) -> int {
+    VR_TRY(with_pass_tag(cfg.est_lds, lw == LANES, true, [&](auto tag) -> int {
       using Tg = decltype(tag);
       if constexpr (sizeof(typename Tg::tbt) == 2) {
         for (int64_t p = p0; p < p1; ++p) {
@@ -1180,15 +1314,22 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
           const int nl = (int)std::min<int64_t>(lw, total - set0);
           VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
           uint32_t* viol = E.viol + (p - p0);
-          VR_TRY((bigA ? pass_a_est<Tg::lds, Tg::full, true>(A, n, E, lw, cfg, viol, st)
-                       : pass_a_est<Tg::lds, Tg::full, false>(A, n, E, lw, cfg, viol, st)));
-          for (int64_t j = 0; j < nb; ++j) {
-            double* out = scores + j * score_ld + set0;
-            const uint32_t* pj = joins[2 * j];
-            VR_TRY((h[(size_t)j + 1].max_group >= 65536u
-                        ? pass_b<false, Tg::full, uint16_t, true, true>(A, Bs[j], pj, nullptr, n, E, lw, nl, out, cfg, st)
-                        : pass_b<false, Tg::full, uint16_t, false, true>(A, Bs[j], pj, nullptr, n, E, lw, nl, out, cfg, st)));
-          }
+          auto run_pass = [&](auto em) -> int {
+            constexpr int EM = decltype(em)::value;
+            VR_TRY((bigA ? pass_a_est<EM, Tg::lds, Tg::full, true>(A, n, E, lw, nl, cfg, viol, st)
+                         : pass_a_est<EM, Tg::lds, Tg::full, false>(A, n, E, lw, nl, cfg, viol, st)));
+            for (int64_t j = 0; j < nb; ++j) {
+              double* out = scores + j * score_ld + set0;
+              const uint32_t* pj = joins[2 * j];
+              VR_TRY((h[(size_t)j + 1].max_group >= 65536u
+                          ? pass_b<Tg::lds, Tg::full, uint16_t, true, EM>(A, Bs[j], pj, nullptr, n, E, lw, nl, out, cfg, st)
+                          : pass_b<Tg::lds, Tg::full, uint16_t, false, EM>(A, Bs[j], pj, nullptr, n, E, lw, nl, out, cfg, st)));
+            }
+            return VR_OK;
+          };
+          VR_TRY(cfg.est_mode == 3   ? run_pass(std::integral_constant<int, 3>{})
+                 : cfg.est_mode == 2 ? run_pass(std::integral_constant<int, 2>{})
+                                     : run_pass(std::integral_constant<int, 1>{}));
         }
       }
       return VR_OK;
@@ -1204,6 +1345,12 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
       }
       g_est_reruns.fetch_add(1);
       VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) { return exact_pass(tag, p * lw); }));
+    }
+    if (p0 == pfirst && flags[0] && p1 < npass) {  // give up on the estimate for this call
+      return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
+        for (int64_t p = p1; p < npass; ++p) VR_TRY(exact_pass(tag, p * lw));
+        return VR_OK;
+      });
     }
   }
   return VR_OK;
