@@ -1,9 +1,9 @@
 #!/bin/bash
 # EST pass-form A/B on the bench RDMs (probe_engine_bench.py under rocprofv3 kernel stats,
 # each EST form checked bit for bit against the exact form in the same process), then the
-# EST parity tests in every form.
+# EST parity tests. Usage: bash scripts/gpu_est_ab.sh <tag> [name:lib.so ...]
 set -o pipefail
-tag=${1:-estab}
+tag=${1:-estab}; shift
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
@@ -21,9 +21,9 @@ for r in csv.DictReader(open(sys.argv[1])):
 PY
   rm -f $out/$name/p_kernel_trace.csv
 }
-run est3 VISREPS_ENGINE_EST=1 VISREPS_ENGINE_EST_MODE=3 || exit 1
-run est1_wg2 VISREPS_ENGINE_EST=1 VISREPS_ENGINE_EST_MODE=1 || exit 1
-for m in 3 1; do
-  VISREPS_ENGINE_EST_MODE=$m timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-      tests/test_engine_est.py > $out/pytest_est_mode$m.log 2>&1; echo "pytest mode $m rc=$?: $(tail -1 $out/pytest_est_mode$m.log)"
+run default VISREPS_ENGINE_EST=1 || exit 1
+for spec in "$@"; do
+  run ${spec%%:*} VISREPS_ENGINE_EST=1 ALT_LIB=$PWD/${spec#*:} || exit 1
 done
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_engine_est.py \
+    > $out/pytest_est.log 2>&1; echo "pytest rc=$?: $(tail -1 $out/pytest_est.log)"

@@ -203,16 +203,20 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
 // ---------------------------------------------------------------------------------
 // per-unit join and per-pass masks
 // ---------------------------------------------------------------------------------
+// The second array: the A chunk (exact form, JOIN_CHUNK) or the EST 3 window low end of the
+// A position, L + (2 posA R >> 32) (JOIN_LO): the B walk then reads it instead of computing it.
+enum { JOIN_NONE = 0, JOIN_CHUNK = 1, JOIN_LO = 2 };
 __global__ void k_join(const uint32_t* __restrict__ codesB, int64_t M, int64_t n,
-                       const uint2* __restrict__ pairMapA,
-                       uint32_t* __restrict__ posA_byB, uint32_t* __restrict__ chunkA_byB) {
+                       const uint2* __restrict__ pairMapA, uint32_t* __restrict__ posA_byB,
+                       uint32_t* __restrict__ second, int mode, uint32_t Lu, uint32_t Ru) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M) return;
   const uint32_t cb = codesB[i];
   const uint64_t t = tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n);
   const uint2 pc = pairMapA[t];
   posA_byB[i] = pc.x;
-  if (chunkA_byB) chunkA_byB[i] = pc.y;  // only the exact (chunk-base) form reads it
+  if (mode == JOIN_CHUNK) second[i] = pc.y;
+  if (mode == JOIN_LO) second[i] = Lu + __umulhi(pc.x << 1, Ru);
 }
 
 // bit w of masks[x] <- x in subset (set0 + w); subset 0 is "all stimuli" when full_first.
@@ -428,11 +432,17 @@ __global__ void k_c0(const uint32_t* __restrict__ c0rel, const uint32_t* __restr
   ftab[(size_t)c * LANES + lane] = make_uint2(2u * a + 1u - 32768u, (uint32_t)((2 * d) >> EST_STEP_BITS));
 }
 
-// EST 3: the wave-uniform estimate {L, R} from lane 0's included-pair total (every active
-// lane of the pass has the same); R = floor(2^32 M'/M) < 2^32 as M' < M
-__global__ void k_c0_u(const uint32_t* __restrict__ total, int64_t M, uint2* __restrict__ ftab) {
-  const uint64_t r = ((uint64_t)total[0] << 32) / (uint64_t)M;
-  ftab[0] = make_uint2(1u - 32768u, (uint32_t)(r > 0xffffffffull ? 0xffffffffull : r));
+// EST 3: the wave-uniform estimate {L, R} (est3_params) into ftab row 0 for the A side
+__global__ void k_c0_u(uint32_t Lu, uint32_t Ru, uint2* __restrict__ ftab) { ftab[0] = make_uint2(Lu, Ru); }
+
+// EST 3 estimate of a call whose subsets all hold k stimuli: M' = k (k - 1) / 2 included
+// pairs per lane, R = floor(2^32 M'/M) (host and device use these same two words; a lane
+// whose count differs, e.g. an index row with repeats, is caught by the A-side check).
+static inline uint2 est3_params(int64_t k, int64_t M) {
+  const unsigned __int128 mp = (unsigned __int128)(uint64_t)(k * (k - 1) / 2);
+  unsigned __int128 r = M > 0 ? (mp << 32) / (unsigned __int128)(uint64_t)M : 0;
+  if (r > 0xffffffffu) r = 0xffffffffu;
+  return make_uint2(1u - 32768u, (uint32_t)r);
 }
 
 // EST 2: the one-interval estimate {L, R} per lane (f32 bit patterns in ftab row 0)
@@ -838,7 +848,7 @@ __device__ inline void gather_issue_t16(const uint16_t* __restrict__ TB, uint32_
 // low ends are computed after the wait.
 template <int EST, typename Fn>
 __device__ inline void gather_window_est(const uint16_t* __restrict__ TB, uint32_t stride, const EstLo& el,
-                                         uint32_t pa, uint32_t lane_bt, int lane, Fn&& fn) {
+                                         uint32_t pa, uint32_t la, uint32_t lane_bt, int lane, Fn&& fn) {
 #pragma unroll
   for (int h = 0; h < 64 / EBB; ++h) {
     uint32_t t[EBB];
@@ -862,7 +872,9 @@ __device__ inline void gather_window_est(const uint16_t* __restrict__ TB, uint32
       }
     }
 #pragma unroll
-    for (int q = 0; q < EBB; ++q) t[q] = est_recover(t[q], est_lo_t<EST>(el, readlane_u32(pa, h * EBB + q), lane));
+    for (int q = 0; q < EBB; ++q)  // EST 3: the join's precomputed low end (lane j = pair j)
+      t[q] = est_recover(t[q], EST == 3 ? readlane_u32(la, h * EBB + q)
+                                        : est_lo_t<EST>(el, readlane_u32(pa, h * EBB + q), lane));
     fn(h, t);
   }
 }
@@ -948,7 +960,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       const uint32_t pos = w + (uint32_t)lane;
       const bool valid = pos >= P0 && pos < P1;
       pa = valid ? posA_byB[pos] : 0u;
-      ca = (!EST && valid) ? chunkA_byB[pos] : 0u;
+      ca = ((!EST || EST == 3) && valid) ? chunkA_byB[pos] : 0u;  // EST 3: window low end
       cd = valid ? codes[pos] : 0u;
       f0 = sload(gflag + (w >> 5));
       f1 = sload(gflag + (w >> 5) + 1);
@@ -965,7 +977,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
       auto gather = [&](auto&& fn) {
         if constexpr (EST)
-          gather_window_est<EST>(reinterpret_cast<const uint16_t*>(TB), stride, el, pa_c, lane_bt, lane, fn);
+          gather_window_est<EST>(reinterpret_cast<const uint16_t*>(TB), stride, el, pa_c, ca_c, lane_bt, lane, fn);
         else
           gather_window<TBT>(TB, baseA, stride, pa_c, ca_c, lane_bt, lane_b4, fn);
       };
@@ -977,7 +989,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
         // 2^50 (yA < 2^32, segment counts < 2^18), so a window sums them in 64 bits.
         close(cw);
         uint64_t a64 = 0;
-        uint32_t c = cw;
+        uint32_t c1 = cw + 1u;  // 1 + included count before position j
         gather([&](int h, uint32_t* ya) {
 #pragma unroll
           for (int q = 0; q < NB; ++q) {
@@ -985,12 +997,12 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
             const uint32_t b = (uint32_t)(x >> j) & 1u;
             const uint32_t yb = b ? ya[q] : 0u;  // x is 0 on inactive lanes
             if (j < 63) {
-              a64 += (uint64_t)yb * (c + 1u);
+              a64 += (uint64_t)yb * c1;
               St += yb;
-              c += b;
+              c1 += b;
             } else {
               S = yb;
-              cgs = c;
+              cgs = c1 - 1u;
             }
           }
         });
@@ -1150,7 +1162,7 @@ static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const
 // pre-pass reads the masks from LDS when they fit (CL), the rank walk from L2.
 template <int EM, bool CL, bool FULL, bool BTA>
 static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, int nl, const EngineCfg& cfg,
-                      uint32_t* viol, hipStream_t st) {
+                      uint2 e3, uint32_t* viol, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     VR_TRY(allow_big_lds(k_countA<CL, FULL>));
@@ -1167,7 +1179,7 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
   VR_CHECK_LAUNCH();
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
   if constexpr (EM == 3)
-    k_c0_u<<<1, 1, 0, st>>>(E.totA, M, E.ftab);
+    k_c0_u<<<1, 1, 0, st>>>(e3.x, e3.y, E.ftab);
   else if constexpr (EM == 2)
     k_c0_lin<<<1, LANES, 0, st>>>(E.totA, M, E.ftab);
   else
@@ -1260,17 +1272,20 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
   const bool narrow = (uint64_t)PLAN_L + h[0].max_group <= 32767u;
   const bool bigA = h[0].max_group >= 65536u;
   const bool est = engine_est();
-  auto join = [&](bool chunks) -> int {
+  const uint2 e3 = est3_params(k, M);
+  int second = JOIN_NONE;  // what the joins' second arrays hold
+  auto join = [&](int mode) -> int {
     for (int64_t j = 0; j < nb; ++j) {
       k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(Bs[j].codes, M, n, A.pair_map, joins[2 * j],
-                                                         chunks ? joins[2 * j + 1] : nullptr);
+                                                         joins[2 * j + 1], mode, e3.x, e3.y);
       VR_CHECK_LAUNCH();
     }
+    second = mode;
     return VR_OK;
   };
   // EST 3 runs the pass holding the full set (pass 0 with full_first) in the exact form
   const bool exact0 = est && cfg.est_mode == 3 && full_first;
-  VR_TRY(join(!est || exact0));
+  VR_TRY(join(!est || exact0 ? JOIN_CHUNK : (cfg.est_mode == 3 ? JOIN_LO : JOIN_NONE)));
   // the exact chunk-base form of the pass starting at subset set0
   auto exact_pass = [&](auto tag, int64_t set0) -> int {
     using Tg = decltype(tag);
@@ -1296,15 +1311,16 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
     });
   }
   const int64_t npass = (total + lw - 1) / lw;
-  bool chunk_joins = exact0;
   const int64_t pfirst = exact0 ? 1 : 0;
   if (pfirst) {
     VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) { return exact_pass(tag, 0); }));
   }
   // The first EST pass runs alone: when the estimate cannot hold these A ranks (strongly
   // structured RDMs, giant tie groups) every pass is run in the exact form from there on.
+  const int want = cfg.est_mode == 3 ? JOIN_LO : JOIN_NONE;  // what the EST passes read
   for (int64_t p0 = pfirst, p1 = pfirst; p0 < npass; p0 = p1) {
     p1 = std::min<int64_t>(npass, p0 == pfirst ? p0 + 1 : p0 + EST_MAX_PASSES);
+    if (want != JOIN_NONE && second != want) VR_TRY(join(want));
     VR_CHECK_HIP(hipMemsetAsync(E.viol, 0, (size_t)(p1 - p0) * sizeof(uint32_t), st));
     VR_TRY(with_pass_tag(cfg.est_lds, lw == LANES, true, [&](auto tag) -> int {
       using Tg = decltype(tag);
@@ -1316,14 +1332,15 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
           uint32_t* viol = E.viol + (p - p0);
           auto run_pass = [&](auto em) -> int {
             constexpr int EM = decltype(em)::value;
-            VR_TRY((bigA ? pass_a_est<EM, Tg::lds, Tg::full, true>(A, n, E, lw, nl, cfg, viol, st)
-                         : pass_a_est<EM, Tg::lds, Tg::full, false>(A, n, E, lw, nl, cfg, viol, st)));
+            VR_TRY((bigA ? pass_a_est<EM, Tg::lds, Tg::full, true>(A, n, E, lw, nl, cfg, e3, viol, st)
+                         : pass_a_est<EM, Tg::lds, Tg::full, false>(A, n, E, lw, nl, cfg, e3, viol, st)));
             for (int64_t j = 0; j < nb; ++j) {
               double* out = scores + j * score_ld + set0;
               const uint32_t* pj = joins[2 * j];
+              const uint32_t* lj = EM == 3 ? joins[2 * j + 1] : nullptr;  // EST 3: window low ends
               VR_TRY((h[(size_t)j + 1].max_group >= 65536u
-                          ? pass_b<Tg::lds, Tg::full, uint16_t, true, EM>(A, Bs[j], pj, nullptr, n, E, lw, nl, out, cfg, st)
-                          : pass_b<Tg::lds, Tg::full, uint16_t, false, EM>(A, Bs[j], pj, nullptr, n, E, lw, nl, out, cfg, st)));
+                          ? pass_b<Tg::lds, Tg::full, uint16_t, true, EM>(A, Bs[j], pj, lj, n, E, lw, nl, out, cfg, st)
+                          : pass_b<Tg::lds, Tg::full, uint16_t, false, EM>(A, Bs[j], pj, lj, n, E, lw, nl, out, cfg, st)));
             }
             return VR_OK;
           };
@@ -1339,14 +1356,12 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
     VR_CHECK_HIP(hipStreamSynchronize(st));
     for (int64_t p = p0; p < p1; ++p) {
       if (!flags[(size_t)(p - p0)]) continue;
-      if (!chunk_joins) {
-        VR_TRY(join(true));
-        chunk_joins = true;
-      }
+      if (second != JOIN_CHUNK) VR_TRY(join(JOIN_CHUNK));
       g_est_reruns.fetch_add(1);
       VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) { return exact_pass(tag, p * lw); }));
     }
     if (p0 == pfirst && flags[0] && p1 < npass) {  // give up on the estimate for this call
+      if (second != JOIN_CHUNK) VR_TRY(join(JOIN_CHUNK));
       return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
         for (int64_t p = p1; p < npass; ++p) VR_TRY(exact_pass(tag, p * lw));
         return VR_OK;
