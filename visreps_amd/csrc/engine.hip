@@ -157,11 +157,11 @@ struct EngineWs {
   uint32_t* segA_tot;   // [nw * 64]
   uint64_t* segA_part;  // [PA_N][nw][64]  tie term sum (k^3 - k)
   uint32_t* segA_pre;   // [nw * 64]
-  uint32_t* segB_tot;   // [nw * 64]
-  uint64_t* segB_part;  // [PB_N][nw][64]  sum S y'_B, sum S, tie term
-  uint32_t* segB_pre;   // [nw * 64]
+  size_t useg;          // nw * 64: unit stride of the B segment partials
+  uint32_t* segB_tot;   // [units][nw * 64]
+  uint64_t* segB_part;  // [units][PB_N][nw][64]  sum S y'_B, sum S, tie term
   uint32_t* bsum;       // [scan_blocks * 64] scan scratch
-  uint64_t* fpart;      // [scan_blocks][6][64] final-fold partials
+  uint64_t* fpart;      // [min(units, 64)][scan_blocks][FP_N][64] tail partials
   uint32_t* totA;       // [64] included pairs per subset
   uint32_t* c0rel;      // [EST_NC][64]     EST: that count relative to its segment
   uint32_t* c0seg;      // [EST_NC]         EST: the segment holding each boundary
@@ -171,7 +171,7 @@ struct EngineWs {
 
 constexpr int EST_MAX_PASSES = 512;  // passes between two checks of the EST flags
 
-static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t* bytes) {
+static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t* bytes, int64_t units = 1) {
   const int64_t M = pairs_of(n);
   const size_t nch = plan_nchunks(M);
   const size_t nsb = scan_blocks((uint32_t)nwaves);
@@ -190,11 +190,12 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
   e.segA_tot = c.take<uint32_t>((size_t)nwaves * LANES);
   e.segA_part = c.take<uint64_t>((size_t)nwaves * LANES * PA_N);
   e.segA_pre = c.take<uint32_t>((size_t)nwaves * LANES);
-  e.segB_tot = c.take<uint32_t>((size_t)nwaves * LANES);
-  e.segB_part = c.take<uint64_t>((size_t)nwaves * LANES * PB_N);
-  e.segB_pre = c.take<uint32_t>((size_t)nwaves * LANES);
+  units = std::max<int64_t>(units, 1);
+  e.useg = (size_t)nwaves * LANES;
+  e.segB_tot = c.take<uint32_t>(e.useg * (size_t)units);
+  e.segB_part = c.take<uint64_t>(e.useg * PB_N * (size_t)units);
   e.bsum = c.take<uint32_t>(nsb * LANES);
-  e.fpart = c.take<uint64_t>(nsb * 6 * LANES);
+  e.fpart = c.take<uint64_t>((size_t)std::min<int64_t>(units, 64) * nsb * 8 * LANES);
   e.totA = c.take<uint32_t>(LANES);
   if (bytes) *bytes = c.bytes();
   return e;
@@ -1045,61 +1046,83 @@ __device__ inline u128 ld128(const uint64_t* p, size_t lo, size_t hi) {
   return ((u128)p[hi] << 64) | p[lo];
 }
 
-// Per block of SCAN_SEGS segments, reduced in a fixed order:
-//   tA = sum (k^3 - k) over A groups,  tB = same over B groups,
-//   ab = sum yA yB = sum_seg (acc + 2 bB St)  (bB = B segment base)
-__global__ __launch_bounds__(1024) void k_final_part(
-    const uint64_t* __restrict__ segA_part, const uint64_t* __restrict__ segB_part,
-    const uint32_t* __restrict__ segB_pre, uint32_t nseg, uint64_t* __restrict__ fpart) {
+// Tail of a pass for units u = blockIdx.y (all B walks of the pass first, one tail for all
+// of them). Per block of SCAN_SEGS B segments, in segment order:
+//   tA = sum (k^3 - k) over A groups,  tB = same over B groups,  T = included pairs,
+//   S = sum St,  X = sum_seg (acc + 2 P St)  with P the included pairs of the block's
+//   segments before this one
+// so that ab = sum yA yB = sum_blk (X_blk + 2 P_blk S_blk) with P_blk the pairs of the
+// blocks before (k_tail_top): no separate scan of the segment counts.
+constexpr int FP_N = 8;  // fpart fields: tA lo/hi, tB lo/hi, X lo/hi, T, S
+__global__ __launch_bounds__(1024) void k_tail_part(
+    const uint64_t* __restrict__ segA_part, const uint64_t* __restrict__ segB_part0,
+    const uint32_t* __restrict__ segB_tot0, uint32_t nseg, size_t ustride, uint64_t* __restrict__ fpart0) {
   __shared__ u128 red[3][16][LANES];
+  __shared__ uint64_t red64[2][16][LANES];
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const size_t fs = (size_t)nseg * LANES;
+  const uint64_t* segB_part = segB_part0 + blockIdx.y * ustride * PB_N;
+  const uint32_t* segB_tot = segB_tot0 + blockIdx.y * ustride;
   constexpr int PER = SCAN_SEGS / 16;
   const uint32_t s0 = blockIdx.x * SCAN_SEGS + v * PER;
-  const size_t fs = (size_t)nseg * LANES;
-  u128 tA = 0, ab = 0, tB = 0;
+  u128 tA = 0, tB = 0, X = 0;
+  uint64_t T = 0, S = 0;
   for (int i = 0; i < PER; ++i) {
     if (s0 + i >= nseg) break;
     const size_t o = (size_t)(s0 + i) * LANES + lane;
+    const uint64_t st = segB_part[PB_ST * fs + o];
     tA += ld128(segA_part, PA_TIEL * fs + o, PA_TIEH * fs + o);
     tB += ld128(segB_part, PB_TIEL * fs + o, PB_TIEH * fs + o);
-    ab += ld128(segB_part, PB_ACCL * fs + o, PB_ACCH * fs + o) +
-          2 * (u128)segB_pre[o] * (u128)segB_part[PB_ST * fs + o];
+    X += ld128(segB_part, PB_ACCL * fs + o, PB_ACCH * fs + o) + 2 * (u128)T * st;
+    S += st;
+    T += segB_tot[o];
   }
   red[0][v][lane] = tA;
-  red[1][v][lane] = ab;
-  red[2][v][lane] = tB;
+  red[1][v][lane] = tB;
+  red[2][v][lane] = X;
+  red64[0][v][lane] = T;
+  red64[1][v][lane] = S;
   __syncthreads();
   if (v != 0) return;
-  for (int u = 1; u < 16; ++u) {
+  for (int u = 1; u < 16; ++u) {  // waves in segment order
     tA += red[0][u][lane];
-    ab += red[1][u][lane];
-    tB += red[2][u][lane];
+    tB += red[1][u][lane];
+    X += red[2][u][lane] + 2 * (u128)T * red64[1][u][lane];
+    S += red64[1][u][lane];
+    T += red64[0][u][lane];
   }
-  uint64_t* f = fpart + (size_t)blockIdx.x * 6 * LANES + lane;
+  uint64_t* f = fpart0 + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * FP_N * LANES + lane;
   f[0 * LANES] = (uint64_t)tA;
   f[1 * LANES] = (uint64_t)(tA >> 64);
-  f[2 * LANES] = (uint64_t)ab;
-  f[3 * LANES] = (uint64_t)(ab >> 64);
-  f[4 * LANES] = (uint64_t)tB;
-  f[5 * LANES] = (uint64_t)(tB >> 64);
+  f[2 * LANES] = (uint64_t)tB;
+  f[3 * LANES] = (uint64_t)(tB >> 64);
+  f[4 * LANES] = (uint64_t)X;
+  f[5 * LANES] = (uint64_t)(X >> 64);
+  f[6 * LANES] = T;
+  f[7 * LANES] = S;
 }
 
-// rho from exact integers. With M' included pairs and doubled midranks y:
+// rho from exact integers, one block per unit. With M' included pairs and doubled midranks y:
 //   sum y = M'(M'+1),  mu = M'(M'+1)^2,
 //   sum k y^2 = 4 M'(M'+1)(2M'+1)/6 - sum_g (k^3 - k)/3   (untied squares minus tie spread)
-__global__ void k_final_top(const uint64_t* __restrict__ fpart, uint32_t nblk,
-                            const uint32_t* __restrict__ totA, const PlanHeader* __restrict__ hA,
-                            const PlanHeader* __restrict__ hB, int nl, double* __restrict__ scores) {
+// nan_units bit u: unit u's B plan has a NaN (so does every unit when a_nan).
+__global__ void k_tail_top(const uint64_t* __restrict__ fpart0, uint32_t nblk,
+                           const uint32_t* __restrict__ totA, int a_nan, uint64_t nan_units, int nl,
+                           double* __restrict__ scores0, int64_t score_ld) {
   const int lane = threadIdx.x;
-  u128 tA = 0, ab = 0, tB = 0;
+  const uint32_t u = blockIdx.x;
+  const uint64_t* fpart = fpart0 + (size_t)u * nblk * FP_N * LANES;
+  u128 tA = 0, tB = 0, ab = 0;
+  uint64_t P = 0;
   // unrolled so the loads of several partial blocks are in flight at once (the loop is
   // otherwise one L2 round trip per block)
 #pragma unroll 8
   for (uint32_t b = 0; b < nblk; ++b) {
-    const uint64_t* f = fpart + (size_t)b * 6 * LANES + lane;
+    const uint64_t* f = fpart + (size_t)b * FP_N * LANES + lane;
     tA += ((u128)f[1 * LANES] << 64) | f[0 * LANES];
-    ab += ((u128)f[3 * LANES] << 64) | f[2 * LANES];
-    tB += ((u128)f[5 * LANES] << 64) | f[4 * LANES];
+    tB += ((u128)f[3 * LANES] << 64) | f[2 * LANES];
+    ab += (((u128)f[5 * LANES] << 64) | f[4 * LANES]) + 2 * (u128)P * f[7 * LANES];
+    P += f[6 * LANES];
   }
   if (lane >= nl) return;
   const u128 Mp = totA[lane];
@@ -1109,13 +1132,13 @@ __global__ void k_final_top(const uint64_t* __restrict__ fpart, uint32_t nblk,
   const i128 va = (i128)(sq - tA / 3) - (i128)mu;
   const i128 vb = (i128)(sq - tB / 3) - (i128)mu;
   double r;
-  if (hA->has_nan || hB->has_nan || Mp < 2 || va <= 0 || vb <= 0) {
+  if (a_nan || ((nan_units >> u) & 1ull) || Mp < 2 || va <= 0 || vb <= 0) {
     r = __builtin_nan("");
   } else {
     r = i128_to_f64(num) / sqrt(i128_to_f64(va) * i128_to_f64(vb));
     r = r > 1.0 ? 1.0 : (r < -1.0 ? -1.0 : r);
   }
-  scores[lane] = r;
+  scores0[(size_t)u * score_ld + lane] = r;
 }
 
 __global__ void k_fill_nan(double* out, int64_t count) {
@@ -1193,12 +1216,11 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
   return VR_OK;
 }
 
-// B side of a pass for one B plan, joined to A by posA_byB (and chunkA_byB in the exact
-// form): the nl scores of the pass.
+// B walk of a pass for one B plan (unit slot u of the segment partials), joined to A by
+// posA_byB (and chunkA_byB: the A chunks in the exact form, EST 3's window low ends)
 template <bool LDS, bool FULL, typename TBT, bool BTB, int EST>
-static int pass_b(const PlanView& A, const PlanView& B, const uint32_t* posA_byB,
-                  const uint32_t* chunkA_byB, int64_t n, const EngineWs& E, int lw, int nl,
-                  double* scores_out, const EngineCfg& cfg, hipStream_t st) {
+static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* chunkA_byB, int64_t n,
+                  const EngineWs& E, int lw, int64_t u, const EngineCfg& cfg, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     VR_TRY(allow_big_lds(k_rankB<LDS, FULL, TBT, BTB, EST>));
@@ -1207,18 +1229,33 @@ static int pass_b(const PlanView& A, const PlanView& B, const uint32_t* posA_byB
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = (uint32_t)(EST ? cfg.est_nwaves : cfg.nwaves);
-  const int bits = EST ? cfg.est_b : 0;
-  const uint32_t rows = EST ? cfg.est_rows : 0;
+  const size_t us = (size_t)E.useg * (size_t)u;
   k_rankB<LDS, FULL, TBT, BTB, EST><<<EST ? cfg.est_grid : cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
       B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
-      posA_byB, chunkA_byB, E.baseA, E.segB_tot, E.segB_part, nseg, E.ftab, rows, bits);
+      posA_byB, chunkA_byB, E.baseA, E.segB_tot + us, E.segB_part + us * PB_N, nseg, E.ftab,
+      EST ? cfg.est_rows : 0, EST ? cfg.est_b : 0);
   VR_CHECK_LAUNCH();
-  VR_TRY(lane_scan(E.segB_tot, nseg, E.bsum, E.segB_pre, nullptr, st));
+  return VR_OK;
+}
+
+// Tail of a pass for units [0, nb) (their B walks done): the nl scores of each, unit j's at
+// scores + j * score_ld. nan_b[j]: unit j's B plan holds a NaN.
+static int tail_units(const EngineWs& E, int64_t nb, uint32_t nseg, bool a_nan, const std::vector<char>& nan_b,
+                      int nl, double* scores, int64_t score_ld, hipStream_t st) {
   const uint32_t nsb = scan_blocks(nseg);
-  k_final_part<<<nsb, 1024, 0, st>>>(E.segA_part, E.segB_part, E.segB_pre, nseg, E.fpart);
-  VR_CHECK_LAUNCH();
-  k_final_top<<<1, LANES, 0, st>>>(E.fpart, nsb, E.totA, A.hdr, B.hdr, nl, scores_out);
-  VR_CHECK_LAUNCH();
+  for (int64_t u0 = 0; u0 < nb; u0 += 64) {  // 64 units per launch (the NaN bitmask)
+    const int64_t cnt = std::min<int64_t>(64, nb - u0);
+    uint64_t nan_units = 0;
+    for (int64_t j = 0; j < cnt; ++j)
+      if (nan_b[(size_t)(u0 + j)]) nan_units |= 1ull << j;
+    const size_t us = (size_t)E.useg * (size_t)u0;
+    k_tail_part<<<dim3(nsb, (unsigned)cnt), 1024, 0, st>>>(E.segA_part, E.segB_part + us * PB_N,
+                                                            E.segB_tot + us, nseg, E.useg, E.fpart);
+    VR_CHECK_LAUNCH();
+    k_tail_top<<<(unsigned)cnt, LANES, 0, st>>>(E.fpart, nsb, E.totA, a_nan ? 1 : 0, nan_units, nl,
+                                                scores + u0 * score_ld, score_ld);
+    VR_CHECK_LAUNCH();
+  }
   return VR_OK;
 }
 
@@ -1270,6 +1307,8 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
                                 hipMemcpyDeviceToHost, st));
   VR_CHECK_HIP(hipStreamSynchronize(st));
   const bool narrow = (uint64_t)PLAN_L + h[0].max_group <= 32767u;
+  std::vector<char> nan_b((size_t)nb);
+  for (int64_t j = 0; j < nb; ++j) nan_b[(size_t)j] = h[(size_t)j + 1].has_nan != 0;
   const bool bigA = h[0].max_group >= 65536u;
   const bool est = engine_est();
   const uint2 e3 = est3_params(k, M);
@@ -1295,14 +1334,13 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
     VR_TRY((bigA ? pass_a<Tg::lds, Tg::full, TBT, true>(A, n, E, lw, cfg, st)
                  : pass_a<Tg::lds, Tg::full, TBT, false>(A, n, E, lw, cfg, st)));
     for (int64_t j = 0; j < nb; ++j) {
-      double* out = scores + j * score_ld + set0;
       const uint32_t* pj = joins[2 * j];
       const uint32_t* cj = joins[2 * j + 1];
       VR_TRY((h[(size_t)j + 1].max_group >= 65536u
-                  ? pass_b<Tg::lds, Tg::full, TBT, true, false>(A, Bs[j], pj, cj, n, E, lw, nl, out, cfg, st)
-                  : pass_b<Tg::lds, Tg::full, TBT, false, false>(A, Bs[j], pj, cj, n, E, lw, nl, out, cfg, st)));
+                  ? walk_b<Tg::lds, Tg::full, TBT, true, 0>(Bs[j], pj, cj, n, E, lw, j, cfg, st)
+                  : walk_b<Tg::lds, Tg::full, TBT, false, 0>(Bs[j], pj, cj, n, E, lw, j, cfg, st)));
     }
-    return VR_OK;
+    return tail_units(E, nb, (uint32_t)cfg.nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0, score_ld, st);
   };
   if (!est) {
     return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
@@ -1335,14 +1373,14 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
             VR_TRY((bigA ? pass_a_est<EM, Tg::lds, Tg::full, true>(A, n, E, lw, nl, cfg, e3, viol, st)
                          : pass_a_est<EM, Tg::lds, Tg::full, false>(A, n, E, lw, nl, cfg, e3, viol, st)));
             for (int64_t j = 0; j < nb; ++j) {
-              double* out = scores + j * score_ld + set0;
               const uint32_t* pj = joins[2 * j];
               const uint32_t* lj = EM == 3 ? joins[2 * j + 1] : nullptr;  // EST 3: window low ends
               VR_TRY((h[(size_t)j + 1].max_group >= 65536u
-                          ? pass_b<Tg::lds, Tg::full, uint16_t, true, EM>(A, Bs[j], pj, lj, n, E, lw, nl, out, cfg, st)
-                          : pass_b<Tg::lds, Tg::full, uint16_t, false, EM>(A, Bs[j], pj, lj, n, E, lw, nl, out, cfg, st)));
+                          ? walk_b<Tg::lds, Tg::full, uint16_t, true, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)
+                          : walk_b<Tg::lds, Tg::full, uint16_t, false, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)));
             }
-            return VR_OK;
+            return tail_units(E, nb, (uint32_t)cfg.est_nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0,
+                              score_ld, st);
           };
           VR_TRY(cfg.est_mode == 3   ? run_pass(std::integral_constant<int, 3>{})
                  : cfg.est_mode == 2 ? run_pass(std::integral_constant<int, 2>{})
@@ -1384,7 +1422,7 @@ static int run_engine(const PlanView& A, const PlanView& B, int64_t n, const int
 static size_t multi_layout(void* base, int64_t n, int64_t nb, int nwaves, EngineWs* E,
                            std::vector<uint32_t*>* joins) {
   size_t eb = 0;
-  const EngineWs e = engine_layout(base, n, LANES, nwaves, &eb);
+  const EngineWs e = engine_layout(base, n, LANES, nwaves, &eb, nb);
   const int64_t M = pairs_of(n);
   Carver c(base ? static_cast<char*>(base) + eb : nullptr);
   if (joins) joins->assign((size_t)std::max<int64_t>(nb, 1) * 2, nullptr);
