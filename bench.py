@@ -337,7 +337,9 @@ def main():
             "config": {"workload": "configs[1]: CustomCNN 14 points x 4 NSD ROIs, N=10k, 1000-bootstrap Spearman RSA",
                        "n_stimuli": N, "points": len(points), "rois": list(NSD_ROIS_4),
                        "units": len(points) * len(NSD_ROIS_4), "n_bootstrap": args.boot,
-                       "phase1": "SRP k=min(4096,D) of every point, 1000 selection stimuli, 14x4 Spearmans",
+                       "phase1": ("SRP k=min(4096,D) of every point for the 1000 selection stimuli (row-wise, so equal to "
+                                  "projecting every row and selecting, as the reference does), selection RDMs, "
+                                  "14x4 Spearmans"),
                        "index_draws": "RandomState(42) 1000 x choice(N, 0.9N) drawn inside every step",
                        "parallelism": f"stimulus-sharded extraction + block Gram, units/{world} ranks"},
             "roofline": roof,

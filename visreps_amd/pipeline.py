@@ -464,12 +464,15 @@ def phase1_select(feats: Dict[str, torch.Tensor], projectors: Dict, responses: D
                   points: Sequence[str], n: int, *, n_select: int = 1000, seed: int = 42,
                   pg=None, times: Optional[StepTimes] = None) -> Dict[str, Tuple[str, List[Dict]]]:
     """Phase-1 layer selection of the reference eval (evals.py:249-287) on stimulus-sharded
-    features: every local row of every point is projected by its SRP matrix (the bulk
-    extraction's torch.sparse.mm, models/utils.py:297-344, here vr_srp_csr_f32);
-    RandomState(seed).choice(n, n_select) picks the selection stimuli (re-created per
-    (region, subject); the regions share one subject's stimuli, so one draw serves them
-    all); selection RDMs of the projected points and of each region's responses; Spearman
-    of every point against every region; best = first strict maximum.
+    features. RandomState(seed).choice(n, n_select) picks the selection stimuli (re-created
+    per (region, subject); the regions share one subject's stimuli, so one draw serves them
+    all); each rank projects its selected rows of every point by the point's SRP matrix (the
+    bulk extraction's torch.sparse.mm, models/utils.py:297-344, here vr_srp_csr_f32). The
+    projection is row by row, so projecting the selected rows equals projecting every row
+    and selecting after, as the reference does: phase 1 reads no other projected row
+    (evals.py:254-268) and phase 2 re-extracts. Then selection RDMs of the projected points
+    and of each region's responses; Spearman of every point against every region; best =
+    first strict maximum.
     Returns {region: (best point, [{"layer", "score"} per point])} on every rank."""
     rank, world = _world(pg)
     rows = shard_rows(n, rank, world)
@@ -480,9 +483,9 @@ def phase1_select(feats: Dict[str, torch.Tensor], projectors: Dict, responses: D
     pos_t = torch.as_tensor(mine, dtype=torch.long, device=dev)
     src_t = torch.as_tensor(sel[mine] - rows.start, dtype=torch.long, device=dev)
 
-    def selected(x_local: torch.Tensor) -> torch.Tensor:  # (n_local, d) -> (k, d), every rank
-        out = torch.zeros((k, x_local.size(1)), dtype=torch.float32, device=dev)
-        out[pos_t] = x_local[src_t].float()
+    def selected(x_mine: torch.Tensor) -> torch.Tensor:  # this rank's selected rows -> (k, d), every rank
+        out = torch.zeros((k, x_mine.size(1)), dtype=torch.float32, device=dev)
+        out[pos_t] = x_mine.float()
         if world > 1:  # disjoint rows: the sum is exact
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=pg)
         return out
@@ -494,12 +497,12 @@ def phase1_select(feats: Dict[str, torch.Tensor], projectors: Dict, responses: D
 
     mplans = []
     for p in points:
-        proj = projectors[p](feats[p])  # SRP of every local stimulus, as get_activations
+        proj = projectors[p](feats[p][src_t])  # SRP of this rank's selected stimuli
         mplans.append(R.RankPlan(timed_rdm(selected(proj))))
         del proj
     out = {}
     for r, y in responses.items():
-        pn = R.RankPlan(timed_rdm(selected(y)))
+        pn = R.RankPlan(timed_rdm(selected(y[src_t])))
         sc = R.bootstrap_spearman_multi(pn, mplans, None, full_first=True)[:, 0].cpu().numpy()
         best, best_score, scores = None, -float("inf"), []
         for p, v in zip(points, sc):
