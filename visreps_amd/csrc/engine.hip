@@ -220,6 +220,13 @@ __global__ void k_join(const uint32_t* __restrict__ codesB, int64_t M, int64_t n
   if (mode == JOIN_LO) second[i] = Lu + __umulhi(pc.x << 1, Ru);
 }
 
+// JOIN_LO from the A positions already joined (no second pair-map gather)
+__global__ void k_join_lo(const uint32_t* __restrict__ posA_byB, int64_t M, uint32_t* __restrict__ second,
+                          uint32_t Lu, uint32_t Ru) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < M) second[i] = Lu + __umulhi(posA_byB[i] << 1, Ru);
+}
+
 // bit w of masks[x] <- x in subset (set0 + w); subset 0 is "all stimuli" when full_first.
 __global__ void k_masks_sets(const int32_t* __restrict__ idx, int64_t k, int64_t set0,
                              int nl, int full_first, uint64_t* __restrict__ masks) {
@@ -847,9 +854,55 @@ __device__ inline void gather_issue_t16(const uint16_t* __restrict__ TB, uint32_
 // after they are issued (no compiler code between the asm issue and the asm wait, which
 // could otherwise read the destination registers before the data lands); the window
 // low ends are computed after the wait.
+#ifndef VR_EST_PIPE
+#define VR_EST_PIPE 2  // EST: gather batches in flight per wave (software pipeline depth; 1 = none)
+#endif
+constexpr int EPS = VR_EST_PIPE;
+
+// wait until at most N of this wave's loads are outstanding; ties the EBB registers t
+template <int N>
+__device__ inline void gather_wait_n(uint32_t* t) {
+  if constexpr (EBB == 4) {
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]) : "n"(N) : "memory");
+  } else {
+    static_assert(EBB == 8, "pipelined EST batches are 4 or 8 pairs");
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7])
+                 : "n"(N)
+                 : "memory");
+  }
+}
+
+// Software-pipelined batch H of a window: batches H+1 .. H+EPS-1 are issued before it is
+// consumed, so EPS batches (EPS * EBB loads) are in flight per wave while it computes.
+template <int EST, int H, typename Fn>
+__device__ inline void pipe_batch(const uint16_t* __restrict__ TB, uint32_t stride, const EstLo& el,
+                                  uint32_t pa, uint32_t la, uint32_t lane_bt, int lane, uint32_t (&t)[EPS][EBB],
+                                  Fn&& fn) {
+  constexpr int NBT = 64 / EBB;
+  if constexpr (H + EPS - 1 < NBT) gather_issue_t(TB, stride, pa, (H + EPS - 1) * EBB, lane_bt, t[(H + EPS - 1) % EPS]);
+  constexpr int ahead = (NBT - 1 - H) < (EPS - 1) ? (NBT - 1 - H) : (EPS - 1);  // batches issued after H
+  gather_wait_n<ahead * EBB>(t[H % EPS]);
+  uint32_t y[EBB];
+#pragma unroll
+  for (int q = 0; q < EBB; ++q)
+    y[q] = est_recover(t[H % EPS][q], EST == 3 ? readlane_u32(la, H * EBB + q)
+                                                : est_lo_t<EST>(el, readlane_u32(pa, H * EBB + q), lane));
+  fn(H, y);
+  if constexpr (H + 1 < NBT) pipe_batch<EST, H + 1>(TB, stride, el, pa, la, lane_bt, lane, t, fn);
+}
+
 template <int EST, typename Fn>
 __device__ inline void gather_window_est(const uint16_t* __restrict__ TB, uint32_t stride, const EstLo& el,
                                          uint32_t pa, uint32_t la, uint32_t lane_bt, int lane, Fn&& fn) {
+  if constexpr (EPS > 1 && !VR_EST_D16) {
+    // the walk is bound by the gathers' round trip: keep EPS batches in flight
+    uint32_t t[EPS][EBB];
+#pragma unroll
+    for (int g = 0; g < EPS - 1; ++g) gather_issue_t(TB, stride, pa, g * EBB, lane_bt, t[g]);
+    pipe_batch<EST, 0>(TB, stride, el, pa, la, lane_bt, lane, t, fn);
+    return;
+  }
 #pragma unroll
   for (int h = 0; h < 64 / EBB; ++h) {
     uint32_t t[EBB];
@@ -1315,6 +1368,11 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
   int second = JOIN_NONE;  // what the joins' second arrays hold
   auto join = [&](int mode) -> int {
     for (int64_t j = 0; j < nb; ++j) {
+      if (mode == JOIN_LO && second != JOIN_NONE) {  // the A positions are already there
+        k_join_lo<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(joins[2 * j], M, joins[2 * j + 1], e3.x, e3.y);
+        VR_CHECK_LAUNCH();
+        continue;
+      }
       k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(Bs[j].codes, M, n, A.pair_map, joins[2 * j],
                                                          joins[2 * j + 1], mode, e3.x, e3.y);
       VR_CHECK_LAUNCH();
