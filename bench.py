@@ -275,19 +275,17 @@ def main():
         gram_tf = times.gram_flops / (times.gram_ms / 1e3) / 1e12 if times.gram_ms else 0.0
         traffic, tsrc = pmc_traffic()
         est = os.environ.get("VISREPS_ENGINE_EST") != "0"
-        form = ("EST (pass 0, holding the full set, in the exact chunk-base form)" if est
-                else "exact chunk-base")
+        form = "EST (one TB gather per pair)" if est else "exact chunk-base"
         roof = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(eng_gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
                 "kernel": (f"bootstrap engine call ({form} form; vr_bootstrap_spearman_multi: per pass of "
                            "64 subsets one A-side rank walk of the neural plan + one B-side walk per "
                            "model plan; k_rankB dominates)"),
                 "algorithmic_bytes_per_unit": round(times.engine_bytes / calls),
-                "algorithmic_bytes_model": (("per pair: EST passes: A side 4+4 B codes (count pre-pass "
-                                             "+ rank walk) + 128 B TB row write per pass (shared by the "
-                                             "call's units), B walk 4+4 B streams + 128 B TB row gather "
-                                             "per pass and unit; pass 0 exact: A 4 + 128 B, B 4+4+4 + "
-                                             "128 B (chunk-base rows L2-resident); join 20 B per unit")
+                "algorithmic_bytes_model": (("per pair: A side 4+4 B codes (count pre-pass + rank walk) "
+                                             "+ 128 B TB row write per pass (shared by the call's units), "
+                                             "B walk 4+4 B streams (A position, window low end) + 128 B TB "
+                                             "row gather per pass and unit; join 24 B per unit")
                                             if est else
                                             ("per pair: A walk 4 B codes + 128 B TB row write per pass "
                                              "(shared by the call's units), B walk 4+4+4 B streams + 128 B "

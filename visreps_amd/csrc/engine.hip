@@ -351,9 +351,13 @@ struct EstLo {
   float L, R;
   uint32_t Lu, Ru;
 };
+// EST 4: EST 3 with lane 0 holding the full set (pass 0 of a full_first call): its count
+// before A position pos is pos itself, so its low end is 2 pos + 1 - 2^15.
 template <int EST>
 __device__ inline uint32_t est_lo_t(const EstLo& e, uint32_t pos, int lane) {
-  if constexpr (EST == 3)
+  if constexpr (EST == 4)
+    return lane == 0 ? 2u * pos + (1u - 32768u) : e.Lu + __umulhi(pos << 1, e.Ru);
+  else if constexpr (EST == 3)
     return e.Lu + __umulhi(pos << 1, e.Ru);
   else if constexpr (EST == 2)
     return (uint32_t)(int32_t)__builtin_fmaf(e.R, (float)pos, e.L);
@@ -363,7 +367,7 @@ __device__ inline uint32_t est_lo_t(const EstLo& e, uint32_t pos, int lane) {
 template <int EST>
 __device__ inline EstLo est_setup(const uint2* __restrict__ gtab, uint32_t rows, int bits, uint2* smem) {
   EstLo e{nullptr, bits, 0.f, 0.f, 0u, 0u};
-  if constexpr (EST == 3) {
+  if constexpr (EST >= 3) {
     e.Lu = wave_uniform(sload(&gtab->x));
     e.Ru = wave_uniform(sload(&gtab->y));
   } else if constexpr (EST == 2) {
@@ -859,6 +863,21 @@ __device__ inline void gather_issue_t16(const uint16_t* __restrict__ TB, uint32_
 #endif
 constexpr int EPS = VR_EST_PIPE;
 
+// B side: the window low end of pair j of the window (lane j of pa / la holds pair j). EST 3
+// and 4 read the join's precomputed value (EST 4's lane 0: 2 posA + 1 - 2^15).
+template <int EST>
+__device__ inline uint32_t est_lo_b(const EstLo& el, uint32_t pa, uint32_t la, int j, int lane) {
+  if constexpr (EST == 4) {
+    const uint32_t l = readlane_u32(la, j);
+    const uint32_t l0 = 2u * readlane_u32(pa, j) + (1u - 32768u);
+    return lane == 0 ? l0 : l;
+  } else if constexpr (EST == 3) {
+    return readlane_u32(la, j);
+  } else {
+    return est_lo_t<EST>(el, readlane_u32(pa, j), lane);
+  }
+}
+
 // wait until at most N of this wave's loads are outstanding; ties the EBB registers t
 template <int N>
 __device__ inline void gather_wait_n(uint32_t* t) {
@@ -886,8 +905,7 @@ __device__ inline void pipe_batch(const uint16_t* __restrict__ TB, uint32_t stri
   uint32_t y[EBB];
 #pragma unroll
   for (int q = 0; q < EBB; ++q)
-    y[q] = est_recover(t[H % EPS][q], EST == 3 ? readlane_u32(la, H * EBB + q)
-                                                : est_lo_t<EST>(el, readlane_u32(pa, H * EBB + q), lane));
+    y[q] = est_recover(t[H % EPS][q], est_lo_b<EST>(el, pa, la, H * EBB + q, lane));
   fn(H, y);
   if constexpr (H + 1 < NBT) pipe_batch<EST, H + 1>(TB, stride, el, pa, la, lane_bt, lane, t, fn);
 }
@@ -927,8 +945,7 @@ __device__ inline void gather_window_est(const uint16_t* __restrict__ TB, uint32
     }
 #pragma unroll
     for (int q = 0; q < EBB; ++q)  // EST 3: the join's precomputed low end (lane j = pair j)
-      t[q] = est_recover(t[q], EST == 3 ? readlane_u32(la, h * EBB + q)
-                                        : est_lo_t<EST>(el, readlane_u32(pa, h * EBB + q), lane));
+      t[q] = est_recover(t[q], est_lo_b<EST>(el, pa, la, h * EBB + q, lane));
     fn(h, t);
   }
 }
@@ -1014,7 +1031,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       const uint32_t pos = w + (uint32_t)lane;
       const bool valid = pos >= P0 && pos < P1;
       pa = valid ? posA_byB[pos] : 0u;
-      ca = ((!EST || EST == 3) && valid) ? chunkA_byB[pos] : 0u;  // EST 3: window low end
+      ca = ((!EST || EST >= 3) && valid) ? chunkA_byB[pos] : 0u;  // EST 3/4: window low end
       cd = valid ? codes[pos] : 0u;
       f0 = sload(gflag + (w >> 5));
       f1 = sload(gflag + (w >> 5) + 1);
@@ -1254,7 +1271,7 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
       A.codes, A.gstart, A.chunk_g, nch, E.masks, n, lw, bits, E.c0rel, E.c0seg, E.segA_tot, nseg);
   VR_CHECK_LAUNCH();
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
-  if constexpr (EM == 3)
+  if constexpr (EM >= 3)
     k_c0_u<<<1, 1, 0, st>>>(e3.x, e3.y, E.ftab);
   else if constexpr (EM == 2)
     k_c0_lin<<<1, LANES, 0, st>>>(E.totA, M, E.ftab);
@@ -1380,9 +1397,7 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
     second = mode;
     return VR_OK;
   };
-  // EST 3 runs the pass holding the full set (pass 0 with full_first) in the exact form
-  const bool exact0 = est && cfg.est_mode == 3 && full_first;
-  VR_TRY(join(!est || exact0 ? JOIN_CHUNK : (cfg.est_mode == 3 ? JOIN_LO : JOIN_NONE)));
+  VR_TRY(join(!est ? JOIN_CHUNK : (cfg.est_mode == 3 ? JOIN_LO : JOIN_NONE)));
   // the exact chunk-base form of the pass starting at subset set0
   auto exact_pass = [&](auto tag, int64_t set0) -> int {
     using Tg = decltype(tag);
@@ -1407,10 +1422,7 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
     });
   }
   const int64_t npass = (total + lw - 1) / lw;
-  const int64_t pfirst = exact0 ? 1 : 0;
-  if (pfirst) {
-    VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) { return exact_pass(tag, 0); }));
-  }
+  const int64_t pfirst = 0;
   // The first EST pass runs alone: when the estimate cannot hold these A ranks (strongly
   // structured RDMs, giant tie groups) every pass is run in the exact form from there on.
   const int want = cfg.est_mode == 3 ? JOIN_LO : JOIN_NONE;  // what the EST passes read
@@ -1432,7 +1444,7 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
                          : pass_a_est<EM, Tg::lds, Tg::full, false>(A, n, E, lw, nl, cfg, e3, viol, st)));
             for (int64_t j = 0; j < nb; ++j) {
               const uint32_t* pj = joins[2 * j];
-              const uint32_t* lj = EM == 3 ? joins[2 * j + 1] : nullptr;  // EST 3: window low ends
+              const uint32_t* lj = EM >= 3 ? joins[2 * j + 1] : nullptr;  // EST 3/4: window low ends
               VR_TRY((h[(size_t)j + 1].max_group >= 65536u
                           ? walk_b<Tg::lds, Tg::full, uint16_t, true, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)
                           : walk_b<Tg::lds, Tg::full, uint16_t, false, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)));
@@ -1440,7 +1452,10 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
             return tail_units(E, nb, (uint32_t)cfg.est_nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0,
                               score_ld, st);
           };
-          VR_TRY(cfg.est_mode == 3   ? run_pass(std::integral_constant<int, 3>{})
+          // EST 3 needs every lane to hold k stimuli: the pass holding the full set runs EST 4
+          const bool full0 = full_first && p == 0;
+          VR_TRY(cfg.est_mode == 3   ? (full0 ? run_pass(std::integral_constant<int, 4>{})
+                                              : run_pass(std::integral_constant<int, 3>{}))
                  : cfg.est_mode == 2 ? run_pass(std::integral_constant<int, 2>{})
                                      : run_pass(std::integral_constant<int, 1>{}));
         }

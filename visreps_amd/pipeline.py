@@ -399,26 +399,27 @@ def engine_bytes(n: int, n_boot: int) -> float:
 # HBM bytes per pair of the engine's own passes (engine.hip). Exact chunk-base form: the A
 # walk streams its codes and writes one 128-byte TB row per pair; each B walk streams its
 # codes and the two join arrays (posA, chunkA) and gathers one TB row per pair (its 256-byte
-# chunk-base rows come from a 2 MB L2-resident table, not HBM). EST form (the default; the
-# pass holding the full set, pass 0, stays exact): the A side streams its codes twice (count
-# pre-pass + rank walk), the B walk drops the chunk array. k_join reads the B codes and one
-# 8-byte pair-map record and writes the two join arrays, once per unit.
+# chunk-base rows come from a 2 MB L2-resident table, not HBM). EST form (the default): the
+# A side streams its codes twice (count
+# pre-pass + rank walk), the B walk reads the window low ends instead of the chunk array (the
+# full-set pass 0 runs EST too, lane 0 on its own exact line). k_join reads the B codes and
+# one 8-byte pair-map record and writes the A positions, k_join_lo the low ends, per unit.
 def engine_pair_bytes(est: Optional[bool] = None) -> Tuple[int, int, int]:
     """(A walk per pass, B walk per pass and unit, join per unit) bytes per pair."""
     if est is None:
         import os
         est = os.environ.get("VISREPS_ENGINE_EST") != "0"
-    return (4 + 4 + 128, 4 + 4 + 128, 4 + 8 + 4 + 4) if est else (4 + 128, 4 + 4 + 4 + 128, 4 + 8 + 4 + 4)
+    # EST join: codes 4 + pair-map record 8 + posA write 4, then low ends: posA read 4 + write 4
+    return (4 + 4 + 128, 4 + 4 + 128, 4 + 8 + 4 + 4 + 4) if est else (4 + 128, 4 + 4 + 4 + 128, 4 + 8 + 4 + 4)
 
 
 def engine_call_bytes(n: int, subsets: int, units: int) -> float:
     """Algorithmic HBM bytes of one engine call: `units` B plans against one A plan over
-    `subsets` subsets (64 per pass, the full set first)."""
+    `subsets` subsets (64 per pass)."""
     a, b, j = engine_pair_bytes()
-    a0, b0, _ = engine_pair_bytes(est=False)
     M = n * (n - 1) // 2
     passes = -(-subsets // 64)
-    return float(M) * ((a0 + units * b0) + (passes - 1) * (a + units * b) + units * j)
+    return float(M) * (passes * (a + units * b) + units * j)
 
 
 def run_unit(plan_m: R.RankPlan, plan_n: R.RankPlan, idx: Optional[np.ndarray],
