@@ -39,7 +39,18 @@ struct PlanView {
   uint32_t* gflag;          // [(M+31)/32 + 2] bit i = position i starts a tie group
 };
 
-inline uint32_t plan_nchunks(int64_t M) { return (uint32_t)((M + PLAN_L - 1) / PLAN_L); }
+// Chunk length of a triangle of M pairs: PLAN_L, or for small triangles the length that gives
+// ~8192 chunks (one per engine wave at 2 x 16 waves on 256 CUs; 64-pair windows, so >= 64):
+// phase 1's 1000-stimulus plans (M ~ 5e5) otherwise have 82 chunks, 1 % of the waves busy.
+inline uint32_t plan_chunk_len(int64_t M) {
+  const int64_t per = (M + 8191) / 8192;
+  const int64_t L = (per + 63) / 64 * 64;
+  return (uint32_t)(L < 64 ? 64 : (L > (int64_t)PLAN_L ? (int64_t)PLAN_L : L));
+}
+inline uint32_t plan_nchunks(int64_t M) {
+  const uint32_t L = plan_chunk_len(M);
+  return (uint32_t)((M + L - 1) / L);
+}
 
 inline PlanView plan_layout(void* base, int64_t n, size_t* bytes = nullptr) {
   const int64_t M = pairs_of(n);

@@ -9,7 +9,7 @@
 //  scan            group numbering -> G
 //  k_group_starts  group start positions, largest group
 //  k_pair_maps     pair index -> sorted position, pair index -> chunk
-//  k_chunk_groups  group-aligned chunks of ~PLAN_L positions
+//  k_chunk_groups  group-aligned chunks of ~plan_chunk_len(M) positions
 //  k_pack_flags    group-start bitmask read by the engine
 #include "plan.h"
 
@@ -102,7 +102,8 @@ int build_plan(const float* rdm, int64_t n, int64_t ld, const PlanView& P, const
                hipStream_t st) {
   const int64_t M = pairs_of(n);
   const uint32_t nchunks = plan_nchunks(M);
-  k_init_header<<<1, 64, 0, st>>>(P.hdr, n, M, nchunks, PLAN_L);
+  const uint32_t L = plan_chunk_len(M);
+  k_init_header<<<1, 64, 0, st>>>(P.hdr, n, M, nchunks, L);
   VR_CHECK_LAUNCH();
   if (M == 0) {
     VR_CHECK_HIP(hipMemsetAsync(P.gstart, 0, sizeof(uint32_t), st));
@@ -122,11 +123,10 @@ int build_plan(const float* rdm, int64_t n, int64_t ld, const PlanView& P, const
   VR_CHECK_LAUNCH();
   k_group_sizes<<<gb, 256, 0, st>>>(P.gstart, P.hdr);
   VR_CHECK_LAUNCH();
-  k_pair_maps<<<gb, 256, 0, st>>>(P.codes, W.flags, W.gidx, P.gstart, M, n, PLAN_L,
-                                  P.pair_map);
+  k_pair_maps<<<gb, 256, 0, st>>>(P.codes, W.flags, W.gidx, P.gstart, M, n, L, P.pair_map);
   VR_CHECK_LAUNCH();
-  k_chunk_groups<<<(unsigned)((M + 1 + 255) / 256), 256, 0, st>>>(P.gstart, P.hdr, nchunks,
-                                                                  PLAN_L, P.chunk_g);
+  k_chunk_groups<<<(unsigned)((M + 1 + 255) / 256), 256, 0, st>>>(P.gstart, P.hdr, nchunks, L,
+                                                                  P.chunk_g);
   VR_CHECK_LAUNCH();
   const int64_t words = (M + 31) / 32 + 2;
   k_pack_flags<<<(unsigned)((words * 32 + 255) / 256), 256, 0, st>>>(W.flags, M, P.gflag, words);
