@@ -890,6 +890,19 @@ __device__ inline void p_issue(const GramParams& P, char* panel, int64_t row0, i
   }
 }
 
+// one 1-KB piece (i = 0, 1) of p_issue
+__device__ inline void p_issue1(const GramParams& P, char* panel, int64_t row0, int q, int i) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t st = q >> 1;
+  const int t = q & 1;
+  const int rbase = (wid * 2 + i) * 16;
+  const int r = rbase + (lane >> 2);
+  const int j = (lane & 3) ^ ((r >> 2) & 3);
+  const int off = ((j & 2) << 5) + 32 * t + ((j & 1) << 4);
+  const char* src = reinterpret_cast<const char*>(P.planes) + ((row0 + r) * P.nstage + st) * 128 + off;
+  __builtin_amdgcn_global_load_lds(src, panel + rbase * 64, 16, 0, 0);
+}
+
 __device__ inline bf16x8 p_frag(const char* panel, int row, int j) {
   return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(panel + row * 64 + ((j ^ ((row >> 2) & 3)) << 4)));
 }
@@ -918,6 +931,37 @@ __device__ inline void p_read(const char* As, const char* Bs, PFrag& f) {
     f.bH[nn] = p_frag(Bs, r, h);
     f.bL[nn] = p_frag(Bs, r, 2 + h);
   }
+}
+
+#ifndef VR_GRAM_ILV
+#define VR_GRAM_ILV 0  // 1: the next sub-stage's LDS-DMA pieces issued between the MFMAs (A/B)
+#endif
+
+// p_mfma with callback g(k) after the 6k-th MFMA (k = 1..3): the same MFMA order
+template <typename G>
+__device__ inline void p_mfma_ilv(const PFrag& f, f32x16 (&acc)[4][2], G&& g) {
+  int c = 0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn) {
+      acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.aH[m], f.bH[nn], acc[m][nn], 0, 0, 0);
+      if (++c % 6 == 0) g(c / 6);
+    }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn) {
+      acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.aH[m], f.bL[nn], acc[m][nn], 0, 0, 0);
+      if (++c % 6 == 0) g(c / 6);
+    }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn) {
+      acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.aL[m], f.bH[nn], acc[m][nn], 0, 0, 0);
+      if (++c % 6 == 0) g(c / 6);
+    }
 }
 
 __device__ inline void p_mfma(const PFrag& f, f32x16 (&acc)[4][2]) {
@@ -957,7 +1001,7 @@ __device__ inline void gram3p_step(const GramParams& P, char* lds, int64_t row0,
     else
       p_wait<0>();
     __builtin_amdgcn_s_barrier();
-    if (q + 3 < Q) {
+    if (!VR_GRAM_ILV && q + 3 < Q) {
       char* slot = lds + ((q + 3) & (P_SLOTS - 1)) * P_SLOT;
       p_issue(P, slot, row0, q + 3);
       if (!DIAG) p_issue(P, slot + P_PANEL, col0, q + 3);
@@ -965,7 +1009,27 @@ __device__ inline void gram3p_step(const GramParams& P, char* lds, int64_t row0,
     const char* As = lds + ((q + 1) & (P_SLOTS - 1)) * P_SLOT;
     p_read(As, DIAG ? As : As + P_PANEL, nxt);
   }
-  p_mfma(cur, acc);
+  if constexpr (VR_GRAM_ILV) {
+    // the slot of q+3 was last read in iteration q-1, before this iteration's barrier; the
+    // pieces are in flight before the next iteration's counted wait either way
+    const bool more = q + 3 < Q;
+    char* slot = lds + ((q + 3) & (P_SLOTS - 1)) * P_SLOT;
+    p_mfma_ilv(cur, acc, [&](int k) {
+      if (!more) return;
+      if (DIAG) {
+        if (k <= 2) p_issue1(P, slot, row0, q + 3, k - 1);
+      } else {
+        if (k == 1) p_issue1(P, slot, row0, q + 3, 0);
+        if (k == 2) {
+          p_issue1(P, slot, row0, q + 3, 1);
+          p_issue1(P, slot + P_PANEL, col0, q + 3, 0);
+        }
+        if (k == 3) p_issue1(P, slot + P_PANEL, col0, q + 3, 1);
+      }
+    });
+  } else {
+    p_mfma(cur, acc);
+  }
   // every P.flush stages (the same two-level sum as k_gram3w); its global loads and stores
   // drain this wave's loads in flight (the compiler waits vmcnt(0)): correct, and rare
   if (P.flush && (q & 1) && q + 1 < Q && ((q >> 1) + 1) % P.flush == 0) {
