@@ -265,6 +265,17 @@ __device__ inline void tie_add(uint64_t& t64, u128& tbig, uint32_t k) {
   }
 }
 
+#ifndef VR_TB_STORE_NT
+#define VR_TB_STORE_NT 1  // TB rows written with nontemporal stores (0: default policy, A/B)
+#endif
+template <typename T>
+__device__ inline void tb_store(T v, T* p) {
+  if constexpr (VR_TB_STORE_NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
 // rows [r0, r0 + cnt) of TB get v in this lane's column: row addresses are wave-uniform
 // (SGPR base + lane offset), four rows per step
 template <bool FULL, typename TBT>
@@ -273,12 +284,12 @@ __device__ inline void store_rows(TBT* __restrict__ TB, uint32_t stride, uint32_
   TBT* row = TB + (size_t)r0 * stride + lane;
   uint32_t i = 0;
   for (; i + 4 <= cnt; i += 4, row += 4 * (size_t)stride) {
-    __builtin_nontemporal_store(v, row);
-    __builtin_nontemporal_store(v, row + stride);
-    __builtin_nontemporal_store(v, row + 2 * stride);
-    __builtin_nontemporal_store(v, row + 3 * stride);
+    tb_store(v, row);
+    tb_store(v, row + stride);
+    tb_store(v, row + 2 * stride);
+    tb_store(v, row + 3 * stride);
   }
-  for (; i < cnt; ++i, row += stride) __builtin_nontemporal_store(v, row);
+  for (; i < cnt; ++i, row += stride) tb_store(v, row);
 }
 
 struct Segment {
@@ -489,12 +500,12 @@ __device__ inline void store_rows_est(uint16_t* __restrict__ TB, uint32_t stride
   uint16_t* row = TB + (size_t)r0 * stride + lane;
   uint32_t i = 0;
   for (; i + 4 <= cnt; i += 4, row += 4 * (size_t)stride) {
-    __builtin_nontemporal_store((uint16_t)y, row);
-    __builtin_nontemporal_store((uint16_t)y, row + stride);
-    __builtin_nontemporal_store((uint16_t)y, row + 2 * stride);
-    __builtin_nontemporal_store((uint16_t)y, row + 3 * stride);
+    tb_store((uint16_t)y, row);
+    tb_store((uint16_t)y, row + stride);
+    tb_store((uint16_t)y, row + 2 * stride);
+    tb_store((uint16_t)y, row + 3 * stride);
   }
-  for (; i < cnt; ++i, row += stride) __builtin_nontemporal_store((uint16_t)y, row);
+  for (; i < cnt; ++i, row += stride) tb_store((uint16_t)y, row);
 }
 
 // A side. Exact form (EST false): chunk-relative doubled ranks y - 2 lp (u16 or u32) and
@@ -589,7 +600,7 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
           for (int j = 0; j < 63; ++j) {
             const uint32_t bit = (uint32_t)(x >> j) & 1u;
             const uint32_t v = t + bit;
-            if (active) __builtin_nontemporal_store((TBT)v, row + (size_t)j * stride);
+            if (active) tb_store((TBT)v, row + (size_t)j * stride);
             t = v + bit;
           }
           gs = w0 + 63u;
