@@ -36,9 +36,58 @@ __device__ inline uint64_t shfl_xor64(uint64_t v, int m) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+#ifndef VR_FAST_XOR
+#define VR_FAST_XOR 1  // lane exchanges of the transpose: DPP (xor 1, 2), ds_swizzle (4, 8, 16), bpermute (32)
+#endif
+
+// v from lane (lane ^ W). W = 1, 2: DPP quad_perm on the VALU (no LDS-pipe round trip);
+// W = 4, 8, 16: ds_swizzle bit-mask mode (xor within 32 lanes, no address register);
+// W = 32: ds_bpermute.
+template <int W>
+__device__ inline uint32_t xor_lane(uint32_t v) {
+  if constexpr (!VR_FAST_XOR || W == 32) {
+    return (uint32_t)__shfl_xor((int)v, W);
+  } else if constexpr (W == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (W == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (W << 10) | 0x1F);  // and 0x1f, xor W
+  }
+}
+
+template <int W>
+__device__ inline uint64_t xor_lane64(uint64_t v) {
+  const uint32_t lo = xor_lane<W>((uint32_t)v);
+  const uint32_t hi = xor_lane<W>((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int ST>
+__device__ inline uint64_t transpose_stage(uint64_t x, int lane) {
+  constexpr uint64_t K[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
+                             0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
+  constexpr int w = 32 >> ST;
+  const uint64_t p = xor_lane64<w>(x);
+  const uint64_t hi = (x & ~K[ST]) | ((p & ~K[ST]) >> w);  // lanes with bit w set
+  const uint64_t lo = (x & K[ST]) | ((p & K[ST]) << w);
+  const uint64_t sel = 0ull - (uint64_t)((lane >> (5 - ST)) & 1);  // branch-free select
+  return (hi & sel) | (lo & ~sel);
+}
+
 // 64x64 bit-matrix transpose across the wave: on entry bit s of lane j is element (j, s);
 // on exit bit j of lane s is. Recursive block swap, 6 stages of one 64-bit exchange.
 __device__ inline uint64_t transpose64(uint64_t x, int lane) {
+  x = transpose_stage<0>(x, lane);
+  x = transpose_stage<1>(x, lane);
+  x = transpose_stage<2>(x, lane);
+  x = transpose_stage<3>(x, lane);
+  x = transpose_stage<4>(x, lane);
+  return transpose_stage<5>(x, lane);
+}
+
+// the round-1 form (every exchange a ds_bpermute): kept for reference timing
+__device__ inline uint64_t transpose64_bperm(uint64_t x, int lane) {
   constexpr uint64_t K[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
                              0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
 #pragma unroll
