@@ -37,16 +37,20 @@ __device__ inline uint64_t shfl_xor64(uint64_t v, int m) {
 }
 
 #ifndef VR_FAST_XOR
-#define VR_FAST_XOR 1  // lane exchanges of the transpose: DPP (xor 1, 2), ds_swizzle (4, 8, 16), bpermute (32)
+#define VR_FAST_XOR 1  // lane exchanges of the transpose: DPP (xor 1, 2), ds_swizzle (4, 8, 16), permlane32_swap (32)
 #endif
 
 // v from lane (lane ^ W). W = 1, 2: DPP quad_perm on the VALU (no LDS-pipe round trip);
 // W = 4, 8, 16: ds_swizzle bit-mask mode (xor within 32 lanes, no address register);
-// W = 32: ds_bpermute.
+// W = 32: v_permlane32_swap (gfx950) of v with itself: afterwards the first result holds
+// [v(0..31), v(0..31)] and the second [v(32..63), v(32..63)] across the wave.
 template <int W>
-__device__ inline uint32_t xor_lane(uint32_t v) {
-  if constexpr (!VR_FAST_XOR || W == 32) {
+__device__ inline uint32_t xor_lane(uint32_t v, int lane) {
+  if constexpr (!VR_FAST_XOR) {
     return (uint32_t)__shfl_xor((int)v, W);
+  } else if constexpr (W == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return lane < 32 ? r[1] : r[0];
   } else if constexpr (W == 1) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
   } else if constexpr (W == 2) {
@@ -57,9 +61,9 @@ __device__ inline uint32_t xor_lane(uint32_t v) {
 }
 
 template <int W>
-__device__ inline uint64_t xor_lane64(uint64_t v) {
-  const uint32_t lo = xor_lane<W>((uint32_t)v);
-  const uint32_t hi = xor_lane<W>((uint32_t)(v >> 32));
+__device__ inline uint64_t xor_lane64(uint64_t v, int lane) {
+  const uint32_t lo = xor_lane<W>((uint32_t)v, lane);
+  const uint32_t hi = xor_lane<W>((uint32_t)(v >> 32), lane);
   return ((uint64_t)hi << 32) | lo;
 }
 
@@ -68,7 +72,7 @@ __device__ inline uint64_t transpose_stage(uint64_t x, int lane) {
   constexpr uint64_t K[6] = {0x00000000FFFFFFFFull, 0x0000FFFF0000FFFFull, 0x00FF00FF00FF00FFull,
                              0x0F0F0F0F0F0F0F0Full, 0x3333333333333333ull, 0x5555555555555555ull};
   constexpr int w = 32 >> ST;
-  const uint64_t p = xor_lane64<w>(x);
+  const uint64_t p = xor_lane64<w>(x, lane);
   const uint64_t hi = (x & ~K[ST]) | ((p & ~K[ST]) >> w);  // lanes with bit w set
   const uint64_t lo = (x & K[ST]) | ((p & K[ST]) << w);
   const uint64_t sel = 0ull - (uint64_t)((lane >> (5 - ST)) & 1);  // branch-free select
