@@ -37,7 +37,8 @@ __device__ inline uint64_t shfl_xor64(uint64_t v, int m) {
 }
 
 #ifndef VR_FAST_XOR
-#define VR_FAST_XOR 1  // lane exchanges of the transpose: DPP (xor 1, 2), ds_swizzle (4, 8, 16), permlane32_swap (32)
+#define VR_FAST_XOR 1  // lane exchanges of the transpose: 1: DPP (xor 1, 2), ds_swizzle (4, 8, 16), permlane32_swap (32);
+                       // 2: DPP for 4, 8 and permlane16_swap for 16 (more VALU: measured slower); 0: ds_bpermute
 #endif
 
 // v from lane (lane ^ W). W = 1, 2: DPP quad_perm on the VALU (no LDS-pipe round trip);
@@ -55,6 +56,15 @@ __device__ inline uint32_t xor_lane(uint32_t v, int lane) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
   } else if constexpr (W == 2) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (W == 4 && VR_FAST_XOR >= 2) {
+    // i ^ 4 = half-row mirror (7 - i in 8) of the quad mirror (3 - i in 4)
+    const int m = __builtin_amdgcn_mov_dpp((int)v, 0x1B, 0xF, 0xF, false);  // quad_perm [3,2,1,0]
+    return (uint32_t)__builtin_amdgcn_mov_dpp(m, 0x141, 0xF, 0xF, false);    // row_half_mirror
+  } else if constexpr (W == 8 && VR_FAST_XOR >= 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else if constexpr (W == 16 && VR_FAST_XOR >= 2) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & 16) ? r[0] : r[1];
   } else {
     return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (W << 10) | 0x1F);  // and 0x1f, xor W
   }
