@@ -1076,12 +1076,14 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
 #pragma unroll
           for (int q = 0; q < NB; ++q) {
             const uint32_t j = h * NB + q;
-            const uint32_t b = (uint32_t)(x >> j) & 1u;
-            const uint32_t yb = b ? ya[q] : 0u;  // x is 0 on inactive lanes
+            // m = -(bit j of x): one sign-extending bit-field extract serves as the select
+            // mask and the count increment (c1 - m = c1 + bit)
+            const uint32_t m = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
+            const uint32_t yb = ya[q] & m;  // x is 0 on inactive lanes
             if (j < 63) {
               a64 += (uint64_t)yb * c1;
               St += yb;
-              c1 += b;
+              c1 -= m;
             } else {
               S = yb;
               cgs = c1 - 1u;
