@@ -9,7 +9,7 @@ import csv
 import json
 import sys
 
-ENGINE = ("k_join", "k_masks", "k_countA", "k_c0", "k_rankA", "k_lscan", "k_add_base", "k_rankB", "k_final", "k_tail")
+ENGINE = ("k_join", "k_masks", "k_countA", "k_c0", "k_rankA", "k_lscan", "k_add_base", "k_rankB", "k_tail")
 
 
 def per_kernel(path):

@@ -8,7 +8,7 @@ import csv
 import json
 import sys
 
-ENGINE = ("k_join", "k_masks", "k_rankA", "k_lscan", "k_add_base", "k_rankB", "k_final")
+ENGINE = ("k_join", "k_masks", "k_countA", "k_c0", "k_rankA", "k_lscan", "k_add_base", "k_rankB", "k_tail")
 
 
 def load(path):

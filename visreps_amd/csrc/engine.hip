@@ -19,14 +19,16 @@
 // two LDS mask reads), and a 64x64 bit transpose across the wave hands lane s the
 // inclusion bits of all 64 pairs for subset s. Counts before any position are then
 // popcounts, so a tie group [gs, ge) closes in O(1): y = c(gs) + c(ge) + 1.
-//  k_rankA   A order: per group the segment-relative y'_A; TB[pos][s] = y'_A - 2 lp_chunk
-//            written in A order (streaming rows; u16 when chunk spans fit, else u32);
-//            segment sums  sum k y', sum k y'^2;  lpA[chunk] = chunk start count
-//  scan      per-lane prefix over segments -> baseA[chunk] = segA_pre + lpA
-//  k_rankB   B order: yA = 2 baseA[chunkA] + TB[posA] gathered per pair (one 128-byte
-//            row per pair); per B group S = sum of included yA; sums S y'_B, S, k y'_B,
-//            k y'_B^2 (segment-relative)
-//  scan + k_final_part + k_final_top   combine segments with their bases -> rho per lane
+//  k_rankA   A order, one 128-byte TB row per pair written in A order. EST form (default):
+//            the absolute doubled rank mod 2^16 (k_countA first gives each segment its
+//            base), every value checked against the B side's count estimate; exact form:
+//            the chunk-relative rank (u16 when chunk spans fit, else u32), lpA[chunk] =
+//            chunk start count, then a per-lane scan -> baseA[chunk].
+//  k_rankB   B order: yA gathered per pair from its TB row (EST: recovered from its 16 bits
+//            and the window low end; exact: + 2 baseA[chunkA], a second gather); per B group
+//            S = sum of included yA; segment sums S y'_B, S, tie terms (segment-relative)
+//  k_tail_part + k_tail_top   all units of a pass at once: blockwise prefix products combine
+//            the segments -> rho per lane
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
