@@ -86,12 +86,12 @@ def pmc_traffic():
     gfx950 correction, calibrated for these 128-B row gathers in
     profiles/r2_fetch_calibration.json) + WRITE_SIZE, per unit. A PMC pass cannot share
     this timed run, so the figure comes from that separate profile."""
-    path = os.path.join(ROOT, "profiles", "r2_pmc_engine_v8.json")
+    path = os.path.join(ROOT, "profiles", "r2_pmc_engine_v10.json")
     try:
         with open(path) as f:
             d = json.load(f)
         return round(float(d["bytes_per_unit"])), (
-            f"profiles/r2_pmc_engine_v8.json: {d['source']}")
+            f"profiles/r2_pmc_engine_v10.json: {d['source']}")
     except (OSError, KeyError, ValueError):
         return None, None
 
