@@ -874,11 +874,15 @@ __device__ inline void gather_issue_t16(const uint16_t* __restrict__ TB, uint32_
   }
 }
 
-// EST: yA of the window's 64 pairs (TB row entry + the window low end from the LDS table),
-// EBB pairs per batch, handed to fn(h, ya[EBB]). The batch's loads are waited for right
-// after they are issued (no compiler code between the asm issue and the asm wait, which
-// could otherwise read the destination registers before the data lands); the window
-// low ends are computed after the wait.
+// EST: yA of the window's 64 pairs (TB row entry + the window low end), EBB pairs per
+// batch, handed to fn(h, ya[EBB]). Default (EPS > 1, pipe_batch): batch H+1's loads are
+// issued before batch H is waited for and consumed, so compiler-generated code (fn, the
+// low ends) runs while asm loads are in flight. The compiler cannot see those loads, so
+// this is correct only if that code never touches (reads, copies or spills) their
+// destination VGPRs before the asm `s_waitcnt` that retires them. Nothing in the source
+// can promise that: tests/test_isa_guard.py checks it on every build's code object
+// (control-flow dataflow over every k_rankB instantiation, and zero scratch for the
+// default forms). EPS = 1 waits for each batch right after issuing it.
 #ifndef VR_EST_PIPE
 #define VR_EST_PIPE 2  // EST: gather batches in flight per wave (software pipeline depth; 1 = none)
 #endif

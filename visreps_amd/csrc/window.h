@@ -85,8 +85,9 @@ __device__ inline uint64_t transpose_stage(uint64_t x, int lane) {
   const uint64_t p = xor_lane64<w>(x, lane);
   const uint64_t hi = (x & ~K[ST]) | ((p & ~K[ST]) >> w);  // lanes with bit w set
   const uint64_t lo = (x & K[ST]) | ((p & K[ST]) << w);
-  const uint64_t sel = 0ull - (uint64_t)((lane >> (5 - ST)) & 1);  // branch-free select
-  return (hi & sel) | (lo & ~sel);
+  // per-lane select on a lane-id bit: a v_cndmask pair on an SGPR-pair lane mask (no
+  // 64-bit all-ones/zeros VGPR constants, which the walks' 64-VGPR budget had to spill)
+  return ((lane >> (5 - ST)) & 1) ? hi : lo;
 }
 
 // 64x64 bit-matrix transpose across the wave: on entry bit s of lane j is element (j, s);
