@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import argparse
 import contextlib
+import ctypes
 import json
 import math
 import os
@@ -51,8 +52,9 @@ sys.path.insert(0, ROOT)
 from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_responses, shard_rows
 from visreps_amd.models.custom_model import CustomCNN
 from visreps_amd.models.utils import FeatureExtractor
+from visreps_amd._lib import KTIMER_KERNELS, check, ktimer_enable, ktimer_read, lib, stream_of
 from visreps_amd.pipeline import (PrefetchedRDMs, StepTimes, all_units_rsa, distributed_rdm, engine_bytes,
-                                  engine_call_bytes, phase1_select)
+                                  engine_call_bytes, engine_pair_bytes, phase1_select)
 
 METRIC = "end-to-end RSA eval sec (extract→RDM→1000-bootstrap Spearman), N=10k stimuli"
 LAYERS = ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
@@ -80,20 +82,93 @@ def extract(extractor: FeatureExtractor, images: torch.Tensor, batch: int):
     return bufs
 
 
-def pmc_traffic():
-    """HBM bytes per unit of the engine from the committed rocprofv3 --pmc passes over one
-    14-unit engine call on the bench's RDMs (scripts/gpu_pmc_engine.sh): FETCH_SIZE x 2 (the
-    gfx950 correction, calibrated for these 128-B row gathers in
-    profiles/r2_fetch_calibration.json) + WRITE_SIZE, per unit. A PMC pass cannot share
-    this timed run, so the figure comes from that separate profile."""
-    path = os.path.join(ROOT, "profiles", "r2_pmc_engine_v10.json")
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r3_pmc_engine.json")
+
+
+def pmc_traffic(n: int, est: bool):
+    """HBM bytes of the engine from the committed rocprofv3 --pmc passes over one 14-unit
+    engine call on the bench's RDMs (scripts/gpu_pmc_engine.sh): FETCH_SIZE x 2 (the gfx950
+    correction, MI355X_MICROARCH.md; calibrated for these 128-B row gathers in
+    profiles/r2_fetch_calibration.json) + WRITE_SIZE. A PMC pass cannot share this timed
+    run, so the figures come from that separate profile -- and only when it was taken on this
+    very build (library sha256), at this N and in this engine form; otherwise None."""
+    from visreps_amd._lib import build_id
+
     try:
-        with open(path) as f:
+        with open(PMC_PROFILE) as f:
             d = json.load(f)
-        return round(float(d["bytes_per_unit"])), (
-            f"profiles/r2_pmc_engine_v10.json: {d['source']}")
-    except (OSError, KeyError, ValueError):
-        return None, None
+    except (OSError, ValueError):
+        return None
+    if d.get("build_id") != build_id() or int(d.get("n", -1)) != n or bool(d.get("est", True)) != est:
+        return None
+    return d
+
+
+def kernel_table(kt: dict, steps: int, est: bool) -> dict:
+    """Per hot kernel over the timed steps (vr_ktimer): ms and launches per step, average
+    launch time, and for the engine kernels the algorithmic bytes per launch and GB/s."""
+    a_b, b_b, j_b = engine_pair_bytes(est)
+    bpp = {"k_rankB_est": engine_pair_bytes(True)[1], "k_rankB_exact": engine_pair_bytes(False)[1],
+           "k_rankA": 4 + 128, "k_countA": 4, "k_join": j_b}  # k_rankA: codes 4 + TB row write 128
+    out = {}
+    for k, (ms, n, units) in kt.items():
+        e = {"ms_per_step": round(ms / steps, 2), "launches_per_step": round(n / steps, 2),
+             "avg_us": round(1e3 * ms / n, 1) if n else None,
+             "units_per_launch": units / n if n else 0.0}
+        if k in bpp:
+            e["bytes_per_launch"] = bpp[k] * units / n if n else 0.0
+            e["gbs"] = round(bpp[k] * units / (ms / 1e3) / 1e9, 1) if ms else 0.0
+        else:  # Gram kernels: tile FLOPs
+            e["tflops"] = round(units / (ms / 1e3) / 1e12, 1) if ms else 0.0
+        out[k] = e
+    return out
+
+
+def structured_est_probe(n: int, plan_b, dev) -> dict:
+    """EST fallback cost on a strongly structured neural RDM (per-stimulus effects, as real
+    fMRI RDMs have: d_ab = u_a + u_b + noise with heavy-tailed u; tests/test_engine_est.py's
+    shape) against one of the bench's model plans, N = n, 1000 bootstraps: one unit in the
+    default EST form (whatever it re-runs exact) and forced exact. Outside the timed steps."""
+    from visreps_amd.analysis import rsa as R
+    from visreps_amd.analysis._random import bootstrap_indices
+
+    g = torch.Generator(device=dev).manual_seed(7)
+    u = torch.empty(n, device=dev).exponential_(1.0, generator=g) ** 2
+    a = u[:, None] + u[None, :] + 0.05 * torch.rand(n, n, device=dev, generator=g)
+    a = torch.triu(a, 1)
+    a = a + a.T
+    plan_a = R.RankPlan(a)
+    del a
+    idx = bootstrap_indices(42, n, int(0.9 * n), 1000)
+    L = lib()
+    out = {}
+    for form, env in (("est", None), ("exact", "0")):
+        old = os.environ.get("VISREPS_ENGINE_EST")
+        if env is None:
+            os.environ.pop("VISREPS_ENGINE_EST", None)
+        else:
+            os.environ["VISREPS_ENGINE_EST"] = env
+        try:
+            R.bootstrap_spearman_multi(plan_a, [plan_b], idx, full_first=True)  # warm
+            torch.cuda.synchronize()
+            r0 = int(L.vr_engine_est_reruns())
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            sc = R.bootstrap_spearman_multi(plan_a, [plan_b], idx, full_first=True)
+            e1.record()
+            torch.cuda.synchronize()
+            out[form] = {"unit_ms": round(e0.elapsed_time(e1), 2), "reruns": int(L.vr_engine_est_reruns()) - r0,
+                         "point": float(sc[0, 0])}
+        finally:
+            if old is None:
+                os.environ.pop("VISREPS_ENGINE_EST", None)
+            else:
+                os.environ["VISREPS_ENGINE_EST"] = old
+    out["passes"] = -(-1001 // 64)
+    out["scores_equal"] = out["est"]["point"] == out["exact"]["point"]
+    out["note"] = ("neural RDM d_ab = u_a + u_b + 0.05 noise, u ~ Exp(1)^2, vs the V1 neural plan of the bench: "
+                   "EST passes the A side flags are re-run exact (est.reruns); exact = VISREPS_ENGINE_EST=0")
+    return out
 
 
 def _time(fn):
@@ -173,6 +248,7 @@ def main():
     ap.add_argument("--boot", type=int, default=1000)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-est-probe", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -247,10 +323,14 @@ def main():
         torch.cuda.synchronize()
         log(f"[rank {rank}] warmup {w}: {time.perf_counter() - t:.2f}s")
 
+    L = lib()
     if pg is not None:
         dist.barrier()
     torch.cuda.synchronize()
     times = StepTimes()
+    reruns0 = int(L.vr_engine_est_reruns())
+    ktimer_enable(True)  # per-launch HIP events on the launch stream of the hot kernels
+    check(L.vr_trace_mark(1, 0, ctypes.c_void_p(stream_of(dev))), "vr_trace_mark")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res, neural, sel = step(times)
@@ -258,7 +338,11 @@ def main():
     if pg is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    check(L.vr_trace_mark(0, 0, ctypes.c_void_p(stream_of(dev))), "vr_trace_mark")
     times.resolve()
+    kt = {k: ktimer_read(k) for k in KTIMER_KERNELS}
+    ktimer_enable(False)
+    est_reruns = int(L.vr_engine_est_reruns()) - reruns0
     stats = torch.tensor([elapsed, times.engine_ms, times.engine_bytes, times.gram_ms,
                           times.gram_flops], dtype=torch.float64, device=dev)
     if pg is not None:
@@ -273,43 +357,69 @@ def main():
         eng_gbs = times.engine_bytes / (times.engine_ms / 1e3) / 1e9 if times.engine_ms else 0.0
         ref_gbs = times.engine_ref_bytes / (times.engine_ms / 1e3) / 1e9 if times.engine_ms else 0.0
         gram_tf = times.gram_flops / (times.gram_ms / 1e3) / 1e12 if times.gram_ms else 0.0
-        traffic, tsrc = pmc_traffic()
         est = os.environ.get("VISREPS_ENGINE_EST") != "0"
-        form = "EST (one TB gather per pair)" if est else "exact chunk-base"
-        roof = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(eng_gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-                "kernel": (f"bootstrap engine call ({form} form; vr_bootstrap_spearman_multi: per pass of "
-                           "64 subsets one A-side rank walk of the neural plan + one B-side walk per "
-                           "model plan; k_rankB dominates)"),
-                "algorithmic_bytes_per_unit": round(times.engine_bytes / calls),
-                "algorithmic_bytes_model": (("per pair: A side 4+4 B codes (count pre-pass + rank walk) "
-                                             "+ 128 B TB row write per pass (shared by the call's units), "
-                                             "B walk 4+4 B streams (A position, window low end) + 128 B TB "
-                                             "row gather per pass and unit; join 24 B per unit")
-                                            if est else
-                                            ("per pair: A walk 4 B codes + 128 B TB row write per pass "
-                                             "(shared by the call's units), B walk 4+4+4 B streams + 128 B "
-                                             "TB row gather per pass and unit (the 256-B chunk-base rows "
-                                             "are L2-resident), join 20 B per unit")),
-                "avg_unit_ms": round(unit_ms, 3),
-                "reference_equivalent_gbs": round(ref_gbs, 1),
-                "reference_equivalent_note": ("SURVEY §8(d) bytes (both fp32 triangles read once per "
-                                              "Spearman) / the same time: what the reference's "
-                                              "algorithm would have to stream; not a roofline")}
-        if traffic:  # bandwidth actually drawn: PMC bytes per unit / measured time per unit
-            drawn = traffic / (unit_ms / 1e3) / 1e9
-            roof["traffic_gbs"] = round(drawn, 1)
-            roof["traffic_frac"] = round(drawn / HBM_PEAK_GBS, 4)
+        pmc = pmc_traffic(N, est)
+        a_b, b_b, j_b = engine_pair_bytes(est)
+        kernels = kernel_table(kt, args.steps, est)
+        # `roofline`: the dominant kernel, k_rankB (the B-side rank walk), priced per launch:
+        # its algorithmic bytes (pairs walked x B/pair) / its HIP-event launch time
+        rb = kernels["k_rankB_est" if est else "k_rankB_exact"]
+        rb_pmc = (pmc or {}).get("kernels", {}).get("k_rankB")
+        roof = {"bound": "hbm", "achieved": rb["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(rb["gbs"] / HBM_PEAK_GBS, 4),
+                "traffic": round(rb_pmc["bytes_per_launch"]) if rb_pmc else None,
+                "kernel": ("k_rankB, " + ("EST 3/4 form" if est else "exact chunk-base form")
+                           + ": B-side rank walk of one unit over one pass of 64 bootstrap subsets"),
+                "algorithmic_bytes_per_launch": round(rb["bytes_per_launch"]),
+                "algorithmic_bytes_model": (f"{b_b} B per pair: codes 4 + A position 4 + window low end 4 "
+                                            "(streams) + 128 B TB row gather" if est else
+                                            f"{b_b} B per pair: codes, A position, A chunk 4 each + 128 B TB "
+                                            "row gather (the 256-B chunk-base rows are L2-resident)"),
+                "pairs_per_launch": round(rb["units_per_launch"]),
+                "launches_per_step": rb["launches_per_step"], "avg_launch_us": rb["avg_us"],
+                "timing": "HIP events around every launch on its stream (vr_ktimer), timed steps only",
+                "traffic_source": ((f"{os.path.relpath(PMC_PROFILE, ROOT)}: {pmc['source']}; bytes per "
+                                    "launch") if rb_pmc else
+                                   "null: no PMC profile of this build/N/form (scripts/gpu_pmc_engine.sh)")}
+        if rb_pmc:
+            roof["traffic_over_algorithmic"] = round(rb_pmc["bytes_per_launch"] / rb["bytes_per_launch"], 3)
+        roof_engine = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(eng_gbs / HBM_PEAK_GBS, 4),
+                       "scope": ("whole engine calls (vr_bootstrap_spearman_multi: joins, A walks, B walks, "
+                                 "tails), HIP events around each call"),
+                       "algorithmic_bytes_per_unit": round(times.engine_bytes / calls),
+                       "algorithmic_bytes_model": (f"per pair: A side {a_b} B per pass (count pre-pass codes 4, "
+                                                   "rank walk codes 4 + 128 B TB row write; shared by the "
+                                                   f"call's units), B walk {b_b} B per pass and unit, join "
+                                                   f"{j_b} B per unit"),
+                       "avg_unit_ms": round(unit_ms, 3),
+                       "traffic_per_unit": round(pmc["bytes_per_unit"]) if pmc else None,
+                       "reference_equivalent_gbs": round(ref_gbs, 1),
+                       "reference_equivalent_note": ("SURVEY §8(d) bytes (both fp32 triangles read once per "
+                                                     "Spearman) / the same time: what the reference's "
+                                                     "algorithm would have to stream; not a roofline")}
         if os.environ.get("VISREPS_GRAM") == "fp32":
             gpeak, gkern = FP32_MFMA_PEAK_TF, "k_gram (exact fp32, v_mfma_f32_32x32x2_f32)"
         else:  # 3 bf16 MFMA products per algorithmic FLOP: ceiling = bf16 dense peak / 3
             gpeak = round(BF16_MFMA_PEAK_TF / 3, 1)
             gkern = ("k_gram3p / k_gram3 (centred rows split hi+lo bf16 by k_stats_split, 3 x "
                      "v_mfma_f32_32x32x16_bf16 per k-step, fp32 accumulate; peak = bf16 dense peak / 3)")
+        gw = kernels["k_gram_wide"]
         roof_gram = {"bound": "mfma", "achieved": round(gram_tf, 2), "peak": gpeak,
                      "unit": "TFLOP/s", "frac": round(gram_tf / gpeak, 4), "kernel": gkern,
                      "algorithmic_flops": "N(N+1)D per RDM (phase-1 selection RDMs included)",
-                     "ms_per_step": round(times.gram_ms / args.steps, 2)}
+                     "ms_per_step": round(times.gram_ms / args.steps, 2),
+                     "wide_kernel": {"name": "k_gram3p (256^2 super-tiles)", "ms_per_step": gw["ms_per_step"],
+                                     "tflops_tile": gw["tflops"],
+                                     "frac_tile": round(gw["tflops"] / gpeak, 4) if gw["tflops"] else None,
+                                     "note": "tile FLOPs 2 d x 256^2 per block (diagonal super-tiles counted whole)"}}
+        est_structured = None
+        if world == 1 and N <= 65535 and not args.no_est_probe:
+            from visreps_amd.analysis.rsa import RankPlan
+
+            t = time.perf_counter()
+            est_structured = structured_est_probe(N, RankPlan(neural["V1"]), dev)
+            log(f"structured-RDM EST probe took {time.perf_counter() - t:.1f}s: {est_structured}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             t = time.perf_counter()
@@ -341,7 +451,14 @@ def main():
                        "index_draws": "RandomState(42) 1000 x choice(N, 0.9N) drawn inside every step",
                        "parallelism": f"stimulus-sharded extraction + block Gram, units/{world} ranks"},
             "roofline": roof,
+            "roofline_engine": roof_engine,
             "roofline_gram": roof_gram,
+            "kernels_per_step": {k: v for k, v in kernels.items() if v["launches_per_step"]},
+            "est_reruns": est_reruns,
+            "est_structured": est_structured,
+            "timed_region": ("bracketed by k_trace_mark_begin / k_trace_mark_end dispatches (vr_trace_mark): "
+                             "scripts/check_timed_kernels.py lists the kernels between them in a rocprofv3 "
+                             "trace (profiles/r3_timed_kernels.json)"),
             "breakdown_ms_per_step": dict(
                 {k: round(v / args.steps, 1) for k, v in times.phase_ms.items()},
                 engine=round(times.engine_ms / args.steps, 1), gram=round(times.gram_ms / args.steps, 1),

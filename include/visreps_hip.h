@@ -183,6 +183,18 @@ int vr_bootstrap_spearman_multi(const void* plan_a, const void* const* planBs, i
  * far (scores never depend on it). VISREPS_ENGINE_EST=0 forces the chunk-base form. */
 int64_t vr_engine_est_reruns(void);
 
+// Kernel-level HIP-event timing of the hot kernels, for pricing the dominant kernel against
+// its roofline on the stream it runs on (bench.py). Off by default; enabling clears the
+// totals. kernel: 0 k_rankB EST forms, 1 k_rankB exact form, 2 k_rankA, 3 k_join/k_join_lo,
+// 4 k_gram3p/k_gram3w (256^2 super-tiles), 5 k_gram3/k_gram (128^2 tiles), 6 k_countA.
+// units: pairs walked (engine kernels) or tile FLOPs 2 d x tile elements (Gram kernels).
+// No reference counterpart (the reference has no native kernels).
+int vr_ktimer_enable(int on);
+int vr_ktimer_read(int kernel, double* ms, int64_t* launches, double* units);
+// Trace marker: launches an empty kernel (k_trace_mark_begin if begin, else
+// k_trace_mark_end) on `stream`, to bracket a region in a rocprofv3 kernel trace.
+int vr_trace_mark(int begin, int tag, void* stream);
+
 /* One-shot form: builds both plans in the workspace, then runs the engine. */
 size_t vr_bootstrap_spearman_workspace(int64_t n);
 int vr_bootstrap_spearman_f32(const float* A, const float* B, int64_t n, int64_t ld,

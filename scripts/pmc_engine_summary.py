@@ -2,12 +2,18 @@
 scripts/gpu_pmc_engine.sh. FETCH_SIZE x 2 (gfx950: FETCH_SIZE reports half the bytes of
 these 128-B row gathers and of wide streams, profiles/r2_fetch_calibration.json).
 
-  python scripts/pmc_engine_summary.py gpurun_out/<tag> <units per call>
+  python scripts/pmc_engine_summary.py gpurun_out/<tag> <units per call> [n]
+
+The output carries the build (sha256 of the library), N and the engine form, so bench.py
+uses it only for the same build and configuration.
 """
 import collections
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 ENGINE = ("k_join", "k_masks", "k_countA", "k_c0", "k_rankA", "k_lscan", "k_add_base", "k_rankB", "k_tail")
 
@@ -23,7 +29,7 @@ def per_kernel(path):
     return agg
 
 
-def main(d, units):
+def main(d, units, n=10000):
     f = per_kernel(f"{d}/FETCH_SIZE/p_counter_collection.csv")
     w = per_kernel(f"{d}/WRITE_SIZE/p_counter_collection.csv")
     kern = {}
@@ -39,9 +45,12 @@ def main(d, units):
                       f"{units}-unit vr_bootstrap_spearman_multi call on the bench RDMs "
                       "(scripts/gpu_pmc_engine.sh); FETCH_SIZE x 2 (gfx950 correction)"),
            "units_per_call": units, "call_bytes": total, "bytes_per_unit": total / units,
-           "kernels": kern}
+           "kernels": kern, "n": n, "est": os.environ.get("VISREPS_ENGINE_EST") != "0",
+           "build_id": build_id()}
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]))
+    from visreps_amd._lib import build_id
+
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]) if len(sys.argv) > 3 else 10000)

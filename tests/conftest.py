@@ -51,3 +51,16 @@ def _release_device_memory(request):
     workspace.release()
     gc.collect()
     torch.cuda.empty_cache()
+
+
+def record_margin(test: str, **values) -> None:
+    """Append one measured parity margin (|dSpearman|, RDM error ...) as a JSON line to
+    gpurun_out/parity_margins.jsonl (VISREPS_MARGINS overrides the path): the numbers behind
+    each tolerance, committed under profiles/ from a GPU run."""
+    import json
+
+    path = os.environ.get("VISREPS_MARGINS", os.path.join(ROOT, "gpurun_out", "parity_margins.jsonl"))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "a") as f:
+        f.write(json.dumps({"test": test, **{k: (float(v) if hasattr(v, "__float__") else v)
+                                             for k, v in values.items()}}) + "\n")

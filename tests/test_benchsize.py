@@ -28,6 +28,8 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import record_margin
+from oracle import rsa_oracle as O
 from visreps_amd.analysis import rsa as R
 from visreps_amd.analysis._random import bootstrap_indices
 
@@ -207,7 +209,7 @@ def bench(dev):
     neural_64 = rdm_f64(y)
     with gram_mode("fp32"):
         neural_32 = R.compute_rdm(y)
-    return feats, neural_split, neural_64, neural_32
+    return feats, neural_split, neural_64, neural_32, y
 
 
 POINTS = [f"{l}_{s}" for l in ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
@@ -216,7 +218,7 @@ POINTS = [f"{l}_{s}" for l in ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1
 
 @pytest.mark.parametrize("point", POINTS)
 def test_bench_point_split_gram_parity(dev, bench, idx, point):
-    feats, neural_split, neural_64, neural_32 = bench
+    feats, neural_split, neural_64, neural_32, _ = bench
     x = feats[point]
     assert x.size(0) == N
     rdm = R.compute_rdm(x)
@@ -231,9 +233,45 @@ def test_bench_point_split_gram_parity(dev, bench, idx, point):
     s_32 = _scores(rdm32, neural_32, idx)
     d64 = float(np.max(np.abs(s_split - s_64)))
     d32 = float(np.max(np.abs(s_split - s_32)))
+    record_margin("bench_point_split_gram", point=point, d=x.size(1), rdm_err_split=err, rdm_err_fp32=err32,
+                  dspearman_split_vs_f64=d64, dspearman_split_vs_fp32=d32,
+                  dspearman_fp32_vs_f64=float(np.max(np.abs(s_32 - s_64))), n_scores=len(s_split))
     assert d64 < SPEARMAN_TOL, (point, d64)
     assert d32 < SPEARMAN_TOL, (point, d32)
     assert float(np.max(np.abs(s_32 - s_64))) < SPEARMAN_TOL
+
+
+@pytest.mark.parametrize("point", ["conv2_post", "conv5_post", "fc1_post"])
+def test_bench_point_vs_cpu_oracle(dev, bench, point):
+    """Full-size parity against the CPU oracle itself: the product's default
+    path (split-Gram RDMs on the GPU, rank-plan engine) for the point Spearman and the first
+    5 bootstraps of RandomState(42) vs O.bootstrap_rsa(O.compute_rdm(x), O.compute_rdm(y),
+    5, 42) -- numpy float32 RDMs and scipy.stats.spearmanr, the reference's arithmetic
+    (rsa.py:59-129, evals.py:341-373) -- on the bench's own N = 10k features."""
+    feats = bench[0]
+    x = feats[point]
+    gm = R.compute_rdm(x)
+    gn = R.compute_rdm(bench[4])
+    point_g, scores_g, _, _ = R.bootstrap_rsa(gm, gn, n_bootstrap=5, seed=42)
+    del gm, gn
+    torch.cuda.empty_cache()
+    om = O.compute_rdm(x.cpu().numpy())
+    on = _oracle_neural(bench)
+    point_o, scores_o, _, _ = O.bootstrap_rsa(om, on, n_bootstrap=5, seed=42)
+    dp = abs(point_g - point_o)
+    db = float(np.max(np.abs(np.asarray(scores_g) - scores_o)))
+    record_margin("bench_point_vs_cpu_oracle", point=point, d=x.size(1), point_hip=point_g, point_oracle=point_o,
+                  dspearman_point=dp, dspearman_boot5=db)
+    assert dp < SPEARMAN_TOL and db < SPEARMAN_TOL, (point, dp, db)
+
+
+_ORACLE_NEURAL = {}
+
+
+def _oracle_neural(bench):
+    if "V1" not in _ORACLE_NEURAL:
+        _ORACLE_NEURAL["V1"] = O.compute_rdm(bench[4].cpu().numpy())
+    return _ORACLE_NEURAL["V1"]
 
 
 # ------------------------------------------------------------------ §8(d) synthetic widths
@@ -251,7 +289,10 @@ def test_synthetic_width_split_gram_parity(dev, idx, d):
     assert err <= max(ROW_TOL, err32), (d, err, err32)
     s_split = _scores(rdm, R.compute_rdm(y), idx)
     s_64 = _scores(rdm_f64(x), rdm_f64(y), idx)
-    assert float(np.max(np.abs(s_split - s_64))) < SPEARMAN_TOL
+    d64 = float(np.max(np.abs(s_split - s_64)))
+    record_margin("synthetic_width_split_gram", d=d, rdm_err_split=err, rdm_err_fp32=err32,
+                  dspearman_split_vs_f64=d64)
+    assert d64 < SPEARMAN_TOL
 
 
 # ----------------------------------------------------------------------------- configs[4]

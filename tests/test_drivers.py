@@ -13,6 +13,11 @@ import torch
 from oracle import pca_oracle as P
 from oracle import rsa_oracle as O
 from visreps_amd import utils
+from conftest import record_margin
+
+# |dSpearman| between the product and the all-oracle path at these small n (each side builds
+# its own RDMs): the north-star bound, with the measured values logged by record_margin
+TOL_SMALL_N = 1e-5
 
 pytestmark = pytest.mark.gpu
 
@@ -50,30 +55,33 @@ def _exact(model, stimuli, dev, layer, ids=None):
 
 
 # --------------------------------------------------------------------------- THINGS
-def test_things_behavior_end_to_end_matches_oracle(dev):
+def _things_vs_oracle(dev, n_concepts, n_images, n_boot):
     from visreps_amd import evals
     from visreps_amd.analysis.alignment import AlignmentData, prepare_concept_alignment
     from visreps_amd.analysis.rsa import _concept_average_exact
     from visreps_amd.dataloaders.neural import _make_loader, load_things_synthetic
     from visreps_amd.models import utils as mutils
 
-    items = ["neural_dataset=things-behavior", "synthetic.things_concepts=60",
-             "synthetic.things_images=2", "n_bootstrap=15", "batchsize=64"]
+    items = ["neural_dataset=things-behavior", f"synthetic.things_concepts={n_concepts}",
+             f"synthetic.things_images={n_images}", f"n_bootstrap={n_boot}", "batchsize=128"]
     df = evals.eval(_cfg(items))
     assert len(df) == 1
     row = df.iloc[0]
     assert row["analysis"] == "rsa" and len(row["layer_selection_scores"]) == 14
-    assert len(row["bootstrap_scores"]) == 15 and row["ci_low"] <= row["ci_high"]
+    assert len(row["bootstrap_scores"]) == n_boot and row["ci_low"] <= row["ci_high"]
 
     # oracle: the same SRP concept means for selection, exact concept means for evaluation
     cfg = _cfg(items)
     model = _model(cfg, dev)
     targets, stimuli = load_things_synthetic(cfg)
-    acts, ids = mutils.get_activations(model, _make_loader(stimuli, None, 64, 0), dev,
+    assert len(stimuli) == n_concepts * n_images
+    acts, ids = mutils.get_activations(model, _make_loader(stimuli, None, 128, 0), dev,
                                        keep_on_device=True, srp_seed=cfg.srp_seed)
     conc = prepare_concept_alignment(cfg, acts, targets, ids)
-    perm = np.random.RandomState(42).permutation(60)
-    sel, ev = perm[:12], perm[12:]
+    del acts
+    perm = np.random.RandomState(42).permutation(n_concepts)
+    n_sel = int(n_concepts * 0.2)  # evals.py:111-115
+    sel, ev = perm[:n_sel], perm[n_sel:]
     concepts = conc.stimulus_ids
     sel_acts = {l: a.cpu().numpy()[sel] for l, a in conc.activations.items()}
     neural = conc.neural.numpy()
@@ -84,19 +92,35 @@ def test_things_behavior_end_to_end_matches_oracle(dev):
         def __missing__(self, layer):
             # concept means of the exact activations on the device, as the eval forms them
             # (their arithmetic: tests/test_concepts.py)
-            raw, raw_ids = _exact(model, stimuli, dev, layer)
-            out = _concept_average_exact(torch.from_numpy(raw).to(dev), raw_ids, evaluation).cpu().numpy()
+            raw, raw_ids = mutils.extract_single_layer(model, _make_loader(stimuli, None, 128, 0), dev, layer,
+                                                       keep_on_device=True)
+            out = _concept_average_exact(raw, raw_ids, evaluation).cpu().numpy()
+            del raw
             self[layer] = out
             return out
 
     ref = O.compute_rsa({"compare_method": "spearman"}, sel_acts, neural[sel], ExactMeans(),
-                        neural[ev], n_select=None, bootstrap=True, n_bootstrap=15, seed=42,
+                        neural[ev], n_select=None, bootstrap=True, n_bootstrap=n_boot, seed=42,
                         rdm_fn=_gpu_rdm(dev))[0]
     assert row["layer"] == ref["layer"]
     for g, r in zip(row["layer_selection_scores"], ref["layer_selection_scores"]):
         assert g["layer"] == r["layer"] and abs(g["score"] - r["score"]) <= 1e-12
     assert abs(row["score"] - ref["score"]) <= 1e-12
     assert np.max(np.abs(np.asarray(row["bootstrap_scores"]) - ref["bootstrap_scores"])) <= 1e-12
+    return row
+
+
+def test_things_behavior_end_to_end_matches_oracle(dev):
+    _things_vs_oracle(dev, 60, 2, 15)
+
+
+def test_things_behavior_full_size_matches_oracle(dev):
+    """BASELINE configs[3] at its stated size: THINGS' 1,854 concepts x 14 images (25,956
+    images, reference evals.py:95-155 / neural.py:313-335), 371 selection and 1,483
+    evaluation concepts, through evals.eval and re-derived by the oracle on the product's
+    RDMs (the RDM kernel itself vs numpy entry-wise, 1e-5, inside _gpu_rdm)."""
+    row = _things_vs_oracle(dev, 1854, 14, 20)
+    record_margin("things_full_size", concepts=1854, images=25956, score=row["score"])
 
 
 def test_things_behavior_encoding_refused(dev):
@@ -164,5 +188,7 @@ def test_rsa_phase2_reconstruct_from_pcs_matches_oracle(dev):
     resp = np.stack([data["neural"]["V1"][0]["test"][s] for s in data["shared_test_ids"]])
     point, scores, _, _ = O.bootstrap_rsa(O.compute_rdm(rec), O.compute_rdm(resp), 10, 42)
     # the reconstruction is fp64 on both sides; the RDMs are float32 numpy vs MFMA
-    assert abs(df.iloc[0]["score"] - point) < 1e-4
-    assert np.max(np.abs(np.asarray(df.iloc[0]["bootstrap_scores"]) - scores)) < 1e-4
+    dp = abs(df.iloc[0]["score"] - point)
+    db = float(np.max(np.abs(np.asarray(df.iloc[0]["bootstrap_scores"]) - scores)))
+    record_margin("reconstruct_from_pcs_vs_oracle", n=len(resp), dspearman_point=dp, dspearman_boot=db)
+    assert dp < TOL_SMALL_N and db < TOL_SMALL_N

@@ -11,6 +11,7 @@ import pytest
 import scipy.stats
 from sklearn.model_selection import KFold
 
+from conftest import record_margin
 from oracle import encoding_oracle as E
 
 
@@ -247,3 +248,62 @@ def test_encoding_refused_for_things_behavior(dev):
     cfg = Config({"analysis": "encoding_score", "neural_dataset": "things-behavior"})
     with pytest.raises(ValueError):
         compute_traintest_alignment(cfg, d, d)
+
+
+@pytest.mark.gpu
+def test_ridge_cv_full_size_matches_closed_form(dev):
+    """BASELINE configs[3]'s ridge at its stated size (reference encoding_score.py:47-62):
+    n = 26,000 stimuli (20,800 fit, 5,200 predicted), p = 4,096 features, 48 voxels of
+    mixed SNR. The product's primal RidgeCV (fp64 p x p Grams on the device) against an
+    independent fp64 closed form on the device: per fold and alpha a Cholesky solve of
+    (X_T^T X_T + a I) W = X_T^T Y_T, the fold-mean l2 loss, its first argmax per voxel
+    (himalaya's RidgeCV rule, parity unpinned beyond this restatement), then the refit
+    predictions X_new (X^T X + a I)^-1 X^T y."""
+    import torch
+    from visreps_amd.analysis.encoding_score import ALPHAS, kfold_splits, ridge_cv_predict_primal
+
+    n_fit, n_new, p, v = 20800, 5200, 4096, 48
+    g = torch.Generator(device=dev).manual_seed(26000)
+    Z = torch.randn(n_fit + n_new, 256, device=dev, generator=g, dtype=torch.float64)
+    X = (Z @ torch.randn(256, p, device=dev, generator=g, dtype=torch.float64)
+         + 0.5 * torch.randn(n_fit + n_new, p, device=dev, generator=g, dtype=torch.float64))
+    X = ((X - X.mean(0)) / X.std(0)).float()  # z-normalised as compute_encoding_score does
+    B = torch.randn(p, v, device=dev, generator=g, dtype=torch.float64) / 64.0
+    snr = torch.logspace(1, -2, v, device=dev, dtype=torch.float64)  # clean ... pure noise
+    Y = (X.double() @ B) * snr + torch.randn(n_fit + n_new, v, device=dev, generator=g, dtype=torch.float64)
+    Y = Y.float()
+    pred, alphas = ridge_cv_predict_primal(X[:n_fit], Y[:n_fit], X[n_fit:])
+
+    a_all = torch.as_tensor(np.asarray(ALPHAS, np.float64), device=dev)
+    Xd, Yd = X.double(), Y[:n_fit].double()
+    eye = torch.eye(p, device=dev, dtype=torch.float64)
+
+    def solve(rows, a):
+        Xt = Xd[rows]
+        L = torch.linalg.cholesky(Xt.T @ Xt + a * eye)
+        return torch.cholesky_solve(Xt.T @ Yd[rows], L)
+
+    loss = torch.zeros((len(a_all), v), device=dev, dtype=torch.float64)
+    for tr, va in kfold_splits(n_fit, 5):
+        tr_t, va_t = torch.as_tensor(tr, device=dev), torch.as_tensor(va, device=dev)
+        for j, a in enumerate(a_all):
+            err = Yd[va_t] - Xd[va_t] @ solve(tr_t, float(a))
+            loss[j] -= (err * err).sum(0)
+    loss /= 5
+    best = torch.argmax(loss, dim=0)
+    ref_alphas = a_all[best].cpu().numpy()
+    # per voxel: the chosen alpha is the closed form's, unless two alphas' CV losses tie to
+    # fp64 rounding (relative 1e-9)
+    srt = torch.sort(loss, dim=0, descending=True).values
+    tie = ((srt[0] - srt[1]).abs() <= 1e-9 * srt[0].abs()).cpu().numpy()
+    assert np.all((alphas == ref_alphas) | tie), (alphas, ref_alphas)
+    assert len(set(alphas.tolist())) >= 3  # the SNR sweep exercises several alphas
+    all_rows = torch.arange(n_fit, device=dev)
+    ref = torch.empty((n_new, v), device=dev, dtype=torch.float64)
+    for a in sorted(set(alphas.tolist())):
+        cols = torch.as_tensor(np.nonzero(alphas == a)[0], device=dev)
+        ref[:, cols] = Xd[n_fit:] @ solve(all_rows, a)[:, cols]
+    rel = float((pred.double() - ref).abs().max() / ref.abs().max())
+    record_margin("ridge_full_size_vs_closed_form", n_fit=n_fit, n_new=n_new, p=p, voxels=v, rel_err=rel,
+                  distinct_alphas=len(set(alphas.tolist())))
+    assert rel <= 1e-6, rel

@@ -14,6 +14,11 @@ import torch
 from oracle import rsa_oracle as O
 from visreps_amd import pipeline as PL
 from visreps_amd.analysis import sparse_random_projection as S
+from conftest import record_margin
+
+# |dSpearman| between the product and the all-oracle path at these small n (each side builds
+# its own RDMs): the north-star bound, with the measured values logged by record_margin
+TOL_SMALL_N = 1e-5
 
 pytestmark = pytest.mark.gpu
 
@@ -48,5 +53,7 @@ def test_phase1_select_matches_oracle(dev, tmp_path):
         assert [s["layer"] for s in scores_got] == points
         # different fp32 summation orders (CSR fma chain vs float64) move near-tied RDM
         # entries in the last bits: a few 1e-6 of rho at 44,850 pairs
-        assert np.max(np.abs(np.array([s["score"] for s in scores_got]) - np.array(scores))) < 2e-5
+        d = float(np.max(np.abs(np.array([s["score"] for s in scores_got]) - np.array(scores))))
+        record_margin("phase1_select_vs_oracle", region=r, n=n_select, dspearman=d)
+        assert d < TOL_SMALL_N
         assert best == points[int(np.argmax(scores))]

@@ -102,6 +102,10 @@ _PROTOTYPES = {
         [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _c_sz, _vp],
     ),
     "vr_engine_est_reruns": (_c_i64, []),
+    "vr_ktimer_enable": (ctypes.c_int, [ctypes.c_int]),
+    "vr_trace_mark": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp]),
+    "vr_ktimer_read": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     "vr_bootstrap_spearman_workspace": (_c_sz, [_c_i64]),
     "vr_bootstrap_spearman_f32": (
         ctypes.c_int,
@@ -232,3 +236,31 @@ class _WorkspacePool:
 
 
 workspace = _WorkspacePool()
+
+
+KTIMER_KERNELS = {"k_rankB_est": 0, "k_rankB_exact": 1, "k_rankA": 2, "k_join": 3,
+                  "k_gram_wide": 4, "k_gram_tile": 5, "k_countA": 6}
+
+
+def ktimer_enable(on: bool = True) -> None:
+    """Start (clearing the totals) or stop the library's per-launch HIP-event timing of the
+    hot kernels (vr_ktimer_enable)."""
+    check(lib().vr_ktimer_enable(1 if on else 0), "vr_ktimer_enable")
+
+
+def ktimer_read(kernel: str) -> tuple[float, int, float]:
+    """(total ms, launches, units) of one hot kernel since ktimer_enable; units are pairs
+    walked (engine kernels) or tile FLOPs (Gram kernels)."""
+    ms, n, u = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+    check(lib().vr_ktimer_read(KTIMER_KERNELS[kernel], ctypes.byref(ms), ctypes.byref(n), ctypes.byref(u)),
+          "vr_ktimer_read")
+    return ms.value, n.value, u.value
+
+
+def build_id() -> str:
+    """sha256[:16] of the loaded library file: ties a committed profile to the build it
+    measured (bench.py emits PMC-derived figures only for the same build)."""
+    import hashlib
+
+    with open(LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]

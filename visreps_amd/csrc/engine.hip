@@ -1266,10 +1266,13 @@ static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = (uint32_t)cfg.nwaves;
-  k_rankA<LDS, FULL, TBT, BTA, false><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
-      A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<TBT*>(E.TB), lw, E.lpA,
-      E.segA_tot, E.segA_part, nseg, EstA{});
-  VR_CHECK_LAUNCH();
+  {
+    KtScope kt(KT_RANKA, (double)M, st);
+    k_rankA<LDS, FULL, TBT, BTA, false><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
+        A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<TBT*>(E.TB), lw, E.lpA,
+        E.segA_tot, E.segA_part, nseg, EstA{});
+    VR_CHECK_LAUNCH();
+  }
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
   const size_t nb = ((size_t)nch * LANES + 255) / 256;
   k_add_base<<<(unsigned)nb, 256, 0, st>>>(E.lpA, E.segA_pre, nch, nseg, E.baseA);
@@ -1294,9 +1297,12 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
   const uint32_t nseg = (uint32_t)cfg.est_nwaves;
   const int bits = cfg.est_b;
   const uint32_t nc = cfg.est_rows;
-  k_countA<CL, FULL><<<cfg.est_grid, ENG_THREADS, CL ? (size_t)n * sizeof(uint64_t) : 0, st>>>(
-      A.codes, A.gstart, A.chunk_g, nch, E.masks, n, lw, bits, E.c0rel, E.c0seg, E.segA_tot, nseg);
-  VR_CHECK_LAUNCH();
+  {
+    KtScope kt(KT_COUNTA, (double)M, st);
+    k_countA<CL, FULL><<<cfg.est_grid, ENG_THREADS, CL ? (size_t)n * sizeof(uint64_t) : 0, st>>>(
+        A.codes, A.gstart, A.chunk_g, nch, E.masks, n, lw, bits, E.c0rel, E.c0seg, E.segA_tot, nseg);
+    VR_CHECK_LAUNCH();
+  }
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
   if constexpr (EM >= 3)
     k_c0_u<<<1, 1, 0, st>>>(e3.x, e3.y, E.ftab);
@@ -1306,10 +1312,13 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
     k_c0<<<nc, LANES, 0, st>>>(E.c0rel, E.c0seg, E.segA_pre, E.totA, nc, bits, M, E.ftab);
   VR_CHECK_LAUNCH();
   const EstA est{E.segA_pre, E.ftab, nc, bits, viol, nl};
-  k_rankA<CL, FULL, uint16_t, BTA, EM><<<cfg.est_grid, ENG_THREADS, cfg.tab, st>>>(
-      A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<uint16_t*>(E.TB), lw, E.lpA,
-      E.segA_tot, E.segA_part, nseg, est);
-  VR_CHECK_LAUNCH();
+  {
+    KtScope kt(KT_RANKA, (double)M, st);
+    k_rankA<CL, FULL, uint16_t, BTA, EM><<<cfg.est_grid, ENG_THREADS, cfg.tab, st>>>(
+        A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<uint16_t*>(E.TB), lw, E.lpA,
+        E.segA_tot, E.segA_part, nseg, est);
+    VR_CHECK_LAUNCH();
+  }
   return VR_OK;
 }
 
@@ -1327,11 +1336,14 @@ static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* c
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = (uint32_t)(EST ? cfg.est_nwaves : cfg.nwaves);
   const size_t us = (size_t)E.useg * (size_t)u;
-  k_rankB<LDS, FULL, TBT, BTB, EST><<<EST ? cfg.est_grid : cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
-      B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
-      posA_byB, chunkA_byB, E.baseA, E.segB_tot + us, E.segB_part + us * PB_N, nseg, E.ftab,
-      EST ? cfg.est_rows : 0, EST ? cfg.est_b : 0);
-  VR_CHECK_LAUNCH();
+  {
+    KtScope kt(EST ? KT_RANKB_EST : KT_RANKB_EXACT, (double)M, st);
+    k_rankB<LDS, FULL, TBT, BTB, EST><<<EST ? cfg.est_grid : cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
+        B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
+        posA_byB, chunkA_byB, E.baseA, E.segB_tot + us, E.segB_part + us * PB_N, nseg, E.ftab,
+        EST ? cfg.est_rows : 0, EST ? cfg.est_b : 0);
+    VR_CHECK_LAUNCH();
+  }
   return VR_OK;
 }
 
@@ -1412,6 +1424,7 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
   int second = JOIN_NONE;  // what the joins' second arrays hold
   auto join = [&](int mode) -> int {
     for (int64_t j = 0; j < nb; ++j) {
+      KtScope kt(KT_JOIN, (double)M, st);
       if (mode == JOIN_LO && second != JOIN_NONE) {  // the A positions are already there
         k_join_lo<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(joins[2 * j], M, joins[2 * j + 1], e3.x, e3.y);
         VR_CHECK_LAUNCH();

@@ -67,3 +67,28 @@ __device__ inline uint32_t f32_sort_key(float f) {
 }
 
 }  // namespace vr
+
+// ---- kernel-level HIP-event timing of the hot kernels (ktimer.cpp) -----------------
+// Off by default (vr_ktimer_enable). A KtScope records an event on the launch stream
+// before and after the one launch it brackets; vr_ktimer_read resolves them.
+namespace vr {
+enum KtKernel : int {
+  KT_RANKB_EST = 0,   // k_rankB, EST forms (3/4 and the probe forms 1/2)
+  KT_RANKB_EXACT = 1, // k_rankB, exact chunk-base form (VISREPS_ENGINE_EST=0, flagged reruns)
+  KT_RANKA = 2,       // k_rankA (both forms)
+  KT_JOIN = 3,        // k_join / k_join_lo
+  KT_GRAM_WIDE = 4,   // k_gram3p / k_gram3w (256^2 super-tiles)
+  KT_GRAM_TILE = 5,   // k_gram3 / k_gram (128^2 tiles)
+  KT_COUNTA = 6,      // k_countA
+  KT_N = 7
+};
+bool ktimer_on();
+struct KtScope {
+  KtScope(int kernel, double units, hipStream_t st);  // units: pairs (engine) or FLOPs (Gram)
+  ~KtScope();
+  int kernel;
+  double units;
+  hipStream_t st;
+  hipEvent_t e0 = nullptr;
+};
+}  // namespace vr

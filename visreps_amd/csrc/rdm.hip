@@ -1418,6 +1418,7 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
     for (int b0 = 0; b0 < nblk; b0 += gen) {
       P.blk0 = b0;
       const unsigned nb = (unsigned)std::min(gen, nblk - b0);
+      KtScope kt(KT_GRAM_TILE, 2.0 * (double)nb / P.splits * GT * GT * (double)d, st);  // tile FLOPs
       if (split3)
         k_gram3<<<nb, G_THREADS, 0, st>>>(P);
       else
@@ -1452,6 +1453,7 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   W.flush = (size_t)gen * WT * WT <= gram_fbuf_floats() ? flush_stages : 0;
   for (int b0 = 0; b0 < W.tile_count; b0 += gen) {
     W.blk0 = b0;
+    KtScope kt(KT_GRAM_WIDE, 2.0 * (double)std::min(gen, W.tile_count - b0) * WT * WT * (double)d, st);
     if (pipe)
       k_gram3p<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
     else

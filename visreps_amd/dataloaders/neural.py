@@ -9,6 +9,8 @@ with a deterministic NSD-shaped synthetic source:
       "shared_test_ids": [sid, ...]  sorted by int (neural.py:170),
       "stimuli": {sid: row},         images generated on demand
   }
+  load_tvsd_synthetic(cfg, subjects, regions) -> the load_all_tvsd_data contract
+      (neural.py:393-460): V1/V4/IT, ~22k train + 100 test stimuli per subject
   load_things_synthetic(cfg) -> (targets, stimuli), the THINGS-behaviour contract
       (neural.py:313-336): targets = {"embeddings": {concept: (66,) float32},
       "image_ids": {concept: [sid, ...]}}, stimuli = {sid: image}
@@ -32,7 +34,7 @@ import torch
 
 from . import synthetic as syn
 
-__all__ = ["SyntheticStimuli", "load_synthetic_data", "load_things_synthetic",
+__all__ = ["SyntheticStimuli", "load_synthetic_data", "load_things_synthetic", "load_tvsd_synthetic",
            "load_nsd_synthetic_test_data", "_make_loader", "StimulusLoader"]
 
 
@@ -149,6 +151,41 @@ def load_nsd_synthetic_test_data(cfg, subjects: Sequence[int], regions: Sequence
             neural[r][subj] = {s: resp[r][i] for i, s in enumerate(names)}
     return {"regions": list(regions), "subjects": list(subjects), "neural": neural,
             "stimuli": stimuli, "test_ids": sorted(names)}
+
+
+TVSD_VOXELS = {"V1": 512, "V4": 256, "IT": 256}  # MUA sites per region (synthetic counts)
+
+
+def load_tvsd_synthetic(cfg, subjects: Sequence[int], regions: Sequence[str]) -> Dict:
+    """TVSD-shaped macaque MUA data with the contract of load_all_tvsd_data
+    (reference neural.py:393-460): regions V1 / V4 / IT, subjects 0 (monkey F) and 1 (monkey
+    N), per subject "train" (cfg.synthetic.tvsd_n_train, default 22,248 THINGS images) and
+    "test" (tvsd_n_test, default 100) response dicts keyed by THINGS-style image names, and
+    shared_test_ids = the test names common to every subject, sorted as strings (neural.py:453;
+    NSD sorts its IDs as integers instead). Responses: dataloaders/synthetic.make_responses
+    with a per-subject seed and the TVSD_VOXELS site counts (cfg.synthetic.voxels overrides)."""
+    sc = cfg.get("synthetic", {}) or {}
+    n_train = int(sc.get("tvsd_n_train", 22248))
+    n_test = int(sc.get("tvsd_n_test", 100))
+    seed = int(sc.get("seed", 20260306)) + 41
+    vox_cfg = dict(sc.get("voxels", {}) or {})
+    voxels = {r: int(vox_cfg.get(r, TVSD_VOXELS.get(r, 256))) for r in regions}
+    # THINGS image names: 12 train images per concept (22,248 = 1,854 x 12), one test
+    # image per test concept; the concept order is not the name order
+    train_ids = [f"c{(c * 7919) % 1854:04d}_{j:02d}s" for c in range(-(-n_train // 12)) for j in range(12)][:n_train]
+    test_ids = [f"c{(c * 104729) % 1854:04d}_99t" for c in range(n_test)]
+    names = train_ids + test_ids
+    if len(set(names)) != len(names):
+        raise ValueError("tvsd_n_train / tvsd_n_test exceed the synthetic THINGS name space")
+    stimuli = SyntheticStimuli({s: i for i, s in enumerate(names)}, seed, _device())
+    neural: Dict = {r: {} for r in regions}
+    for subj in subjects:
+        resp = _responses(stimuli, len(names), voxels, seed + 11 * (int(subj) + 1))
+        for r in regions:
+            neural[r][subj] = {"train": {s: resp[r][i] for i, s in enumerate(train_ids)},
+                               "test": {s: resp[r][len(train_ids) + i] for i, s in enumerate(test_ids)}}
+    return {"regions": list(regions), "subjects": list(subjects), "neural": neural, "stimuli": stimuli,
+            "shared_test_ids": sorted(test_ids)}
 
 
 def load_synthetic_data(cfg, subjects: Sequence[int], regions: Sequence[str]) -> Dict:

@@ -19,6 +19,8 @@ rank-plan engine (one plan per RDM, reused across its units); there is no CPU pa
 Datasets (no on-disk data exists offline; every source is a seeded
 synthetic stand-in with the reference's data contract):
   synthetic / nsd   NSD-shaped stimuli and per-subject responses (dataloaders/neural.py)
+  tvsd              TVSD-shaped: V1/V4/IT MUA of 2 monkeys, ~22k train + 100 test THINGS
+                    images per subject, string-sorted shared test IDs (evals.py:189-190)
   things-behavior   THINGS-shaped concepts x 66-d embeddings, images per concept; 80/20
                     concept split by RandomState(42).permutation, layer selection on 20 %,
                     re-extraction without SRP + concept averaging for the 80 % (:95-155)
@@ -49,7 +51,7 @@ from .analysis.rsa import (RankPlan, _concept_average_exact, bootstrap_rsa, comp
                            compute_rdm_correlation)
 from .analysis._random import LegacyRandomState
 from .dataloaders.neural import (_make_loader, load_nsd_synthetic_test_data, load_synthetic_data,
-                                 load_things_synthetic)
+                                 load_things_synthetic, load_tvsd_synthetic)
 from .models import utils as mutils
 from . import utils as U
 from .utils import Config, get_seed_letter, rprint, save_results
@@ -104,11 +106,11 @@ def eval(cfg):  # noqa: A001  (reference name)
                f"epoch {cfg.get('epoch', '?')} | {len(subjects)} subjects x {len(regions)} regions | "
                f"seed {cfg.seed}\n", style="info")
         return _eval_rsa_nsd_synthetic(cfg, subjects, regions, dev, verbose)
-    if dataset not in ("synthetic", "nsd"):
+    if dataset not in ("synthetic", "nsd", "tvsd"):
         raise NotImplementedError(
             f"neural_dataset='{dataset}' reads the reference's on-disk data, which this build "
-            "does not ship; 'synthetic'/'nsd' (NSD-shaped), 'things-behavior' and "
-            "'nsd_synthetic' run on seeded synthetic stand-ins")
+            "does not ship; 'synthetic'/'nsd' (NSD-shaped), 'tvsd' (TVSD-shaped), "
+            "'things-behavior' and 'nsd_synthetic' run on seeded synthetic stand-ins")
 
     subjects = _listify(cfg.subject_idx)
     regions = _listify(cfg.region)
@@ -121,7 +123,10 @@ def eval(cfg):  # noqa: A001  (reference name)
     model = mutils.load_model(cfg, dev, verbose=verbose)
     model = mutils.configure_feature_extractor(cfg, model, verbose=verbose)
 
-    all_data = load_synthetic_data(cfg, subjects, regions)
+    if dataset == "tvsd":  # evals.py:189-190: the same two-phase path on TVSD's contract
+        all_data = load_tvsd_synthetic(cfg, subjects, regions)
+    else:
+        all_data = load_synthetic_data(cfg, subjects, regions)
     stimuli = all_data["stimuli"]
     rprint(f"  {len(subjects)} subjects x {len(regions)} regions, {len(stimuli)} stimuli, "
            f"{len(all_data['shared_test_ids'])} shared test IDs", style="success")

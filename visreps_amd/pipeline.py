@@ -409,8 +409,12 @@ def engine_pair_bytes(est: Optional[bool] = None) -> Tuple[int, int, int]:
     if est is None:
         import os
         est = os.environ.get("VISREPS_ENGINE_EST") != "0"
-    # EST join: codes 4 + pair-map record 8 + posA write 4, then low ends: posA read 4 + write 4
-    return (4 + 4 + 128, 4 + 4 + 128, 4 + 8 + 4 + 4 + 4) if est else (4 + 128, 4 + 4 + 4 + 128, 4 + 8 + 4 + 4)
+    # A side: codes 4 (EST: count pre-pass + rank walk, 4 each) + 128 B TB row write.
+    # B walk: codes 4 + A position 4 + second join array 4 (EST: window low end; exact: A chunk)
+    # + 128 B TB row gather (the exact form's 256-B chunk-base rows are L2-resident).
+    # Join: B codes 4 + the A map gather (EST: 4-B position map; exact: 8-B pair-map record)
+    # + posA write 4 + second array write 4.
+    return (4 + 4 + 128, 4 + 4 + 4 + 128, 4 + 4 + 4 + 4) if est else (4 + 128, 4 + 4 + 4 + 128, 4 + 8 + 4 + 4)
 
 
 def engine_call_bytes(n: int, subsets: int, units: int) -> float:
