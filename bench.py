@@ -53,8 +53,8 @@ from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_resp
 from visreps_amd.models.custom_model import CustomCNN
 from visreps_amd.models.utils import FeatureExtractor
 from visreps_amd._lib import KTIMER_KERNELS, check, ktimer_enable, ktimer_read, lib, stream_of
-from visreps_amd.pipeline import (PrefetchedRDMs, StepTimes, all_units_rsa, distributed_rdm, engine_bytes,
-                                  engine_call_bytes, engine_pair_bytes, phase1_select)
+from visreps_amd.pipeline import (ShardedRDMs, StepTimes, all_units_rsa, engine_bytes, engine_call_bytes,
+                                  engine_pair_bytes, make_schedule, phase1_select)
 
 METRIC = "end-to-end RSA eval sec (extract→RDM→1000-bootstrap Spearman), N=10k stimuli"
 LAYERS = ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
@@ -108,7 +108,8 @@ def kernel_table(kt: dict, steps: int, est: bool) -> dict:
     """Per hot kernel over the timed steps (vr_ktimer): ms and launches per step, average
     launch time, and for the engine kernels the algorithmic bytes per launch and GB/s."""
     a_b, b_b, j_b = engine_pair_bytes(est)
-    bpp = {"k_rankB_est": engine_pair_bytes(True)[1], "k_rankB_exact": engine_pair_bytes(False)[1],
+    bpp = {"k_rankB_est": engine_pair_bytes(True)[1], "k_rankB_full": engine_pair_bytes(True)[1],
+           "k_rankB_exact": engine_pair_bytes(False)[1],
            "k_rankA": 4 + 128, "k_countA": 4, "k_join": j_b}  # k_rankA: codes 4 + TB row write 128
     out = {}
     for k, (ms, n, units) in kt.items():
@@ -269,7 +270,7 @@ def main():
         else:
             dist.init_process_group(backend)
         pg = dist.group.WORLD
-        # the feature-plane exchange gets its own communicator (PrefetchedRDMs.start_all)
+        # the row exchange to the RDM owners gets its own communicator (ShardedRDMs.start)
         feat_pg = dist.new_group(list(range(world)))
     N = args.n
     rows = shard_rows(N, rank, world)
@@ -297,24 +298,33 @@ def main():
                  for d in sorted(set(dims.values()))}
     projectors = {p: proj_by_d[d] for p, d in dims.items()}
 
+    # who computes and who reads every RDM of the step (the same on every rank): owners get
+    # the full rows of their RDMs, consumers the packed tiles (pipeline.make_schedule)
+    regions = list(NSD_ROIS_4)
+    sched = make_schedule(N, dims, points, NSD_ROIS_4, world)
+
     def step(times: StepTimes):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
         ev[0].record()
         feats = extract(extractor, images, args.batch)
         ev[1].record()
-        # N > 1: every point's plane all-gather starts now, on its own communicator, and
-        # streams under phase 1, the neural RDMs and the model Grams
-        rdms = PrefetchedRDMs(feats, points, N, pg, times, exchange_pg=feat_pg)
-        rdms.start_all()
+        rows = {("m", p): feats[p] for p in points}
+        rows.update({("n", r): responses[r] for r in regions})
+        # N > 1: the row exchanges to the RDM owners start now, on their own communicator,
+        # and stream under phase 1
+        ex = ShardedRDMs(sched, rows, pg, times, exchange_pg=feat_pg)
+        ex.start()
         sel = phase1_select(feats, projectors, responses, points, N, n_select=1000, seed=42,
                             pg=pg, times=times)
         ev[2].record()
-        neural = {r: distributed_rdm(y, N, pg, times) for r, y in responses.items()}
+        rd = ex.finish()  # this rank's RDMs: its pieces' Grams + the exchange of the rest
         ev[3].record()
-        res = all_units_rsa(rdms, points, neural, N, n_boot=args.boot, seed=42, pg=pg, times=times)
+        del feats, rows, ex
+        neural = {r: rd[("n", r)] for r in regions if ("n", r) in rd}
+        res = all_units_rsa(lambda p: rd.pop(("m", p)), points, neural, N, n_boot=args.boot, seed=42, pg=pg,
+                            times=times, regions=regions)
         ev[4].record()
-        times.phases(["extract", "phase1", "neural_rdms", "units"], ev)
-        del feats, rdms
+        times.phases(["extract", "phase1", "rdms", "units"], ev)
         return res, neural, sel
 
     for w in range(args.warmup):
@@ -368,8 +378,9 @@ def main():
         roof = {"bound": "hbm", "achieved": rb["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(rb["gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": round(rb_pmc["bytes_per_launch"]) if rb_pmc else None,
-                "kernel": ("k_rankB, " + ("EST 3/4 form" if est else "exact chunk-base form")
-                           + ": B-side rank walk of one unit over one pass of 64 bootstrap subsets"),
+                "kernel": ("k_rankB, " + ("EST 3 form" if est else "exact chunk-base form")
+                           + ": B-side rank walk of one unit over one pass of 64 bootstrap subsets "
+                           "(the full-set pass 0 and phase-1 launches are k_rankB_full in kernels_per_step)"),
                 "algorithmic_bytes_per_launch": round(rb["bytes_per_launch"]),
                 "algorithmic_bytes_model": (f"{b_b} B per pair: codes 4 + A position 4 + window low end 4 "
                                             "(streams) + 128 B TB row gather" if est else
@@ -449,7 +460,8 @@ def main():
                                   "projecting every row and selecting, as the reference does), selection RDMs, "
                                   "14x4 Spearmans"),
                        "index_draws": "RandomState(42) 1000 x choice(N, 0.9N) drawn inside every step",
-                       "parallelism": f"stimulus-sharded extraction + block Gram, units/{world} ranks"},
+                       "parallelism": (f"stimulus-sharded extraction; RDMs by owner ranks (rows all_to_all to the "
+                                       f"owners, packed tiles to the consumers); units/{world} ranks")},
             "roofline": roof,
             "roofline_engine": roof_engine,
             "roofline_gram": roof_gram,
@@ -462,7 +474,8 @@ def main():
             "breakdown_ms_per_step": dict(
                 {k: round(v / args.steps, 1) for k, v in times.phase_ms.items()},
                 engine=round(times.engine_ms / args.steps, 1), gram=round(times.gram_ms / args.steps, 1),
-                note="HIP events on rank 0's compute stream; units = model RDMs + plans + engine"),
+                note=("HIP events on rank 0's compute stream; rdms = all Grams (model + neural) + exchanges, "
+                      "units = plans + engine")),
             "cpu_baseline": cpu,
             "check": {"unit": f"{points[0]} x V1", "score": first["score"],
                       "ci": [first["ci_low"], first["ci_high"]], "phase1_best": best},

@@ -62,6 +62,12 @@ int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float*
  * all-reduce. vr_rdm_tile_count(n) = number of tiles, vr_rdm_tile_cost(n, t) = distinct
  * (i <= j) entries of tile t, for balancing ranges. */
 int64_t vr_rdm_tile_count(int64_t n);
+// Super-tile rows R of the wide kernel in the full n x n launch at width d (0: the wide
+// kernel is not used), and whether the 128-tile range [tile_begin, tile_end) is cut only at
+// aligned boundaries (tri_start(2r, T), r <= R, or the end of the triangle): such a range's
+// tiles are bit-identical to the full launch's (multi-GPU RDM pieces, pipeline.py).
+int64_t vr_rdm_wide_rows(int64_t n, int64_t d);
+int vr_rdm_range_aligned(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end);
 int64_t vr_rdm_tile_cost(int64_t n, int64_t tile);
 /* Rectangle of upper-triangle tile `tile`: rows [row0, row0+rows) x cols
  * [col0, col0+cols), col0 >= row0 (a diagonal tile covers its upper half). Host only;
@@ -185,8 +191,9 @@ int64_t vr_engine_est_reruns(void);
 
 // Kernel-level HIP-event timing of the hot kernels, for pricing the dominant kernel against
 // its roofline on the stream it runs on (bench.py). Off by default; enabling clears the
-// totals. kernel: 0 k_rankB EST forms, 1 k_rankB exact form, 2 k_rankA, 3 k_join/k_join_lo,
-// 4 k_gram3p/k_gram3w (256^2 super-tiles), 5 k_gram3/k_gram (128^2 tiles), 6 k_countA.
+// totals. kernel: 0 k_rankB EST forms over bootstrap subsets, 1 k_rankB exact form, 2 k_rankA,
+// 3 k_join/k_join_lo, 4 k_gram3p/k_gram3w (256^2 super-tiles), 5 k_gram3/k_gram (128^2 tiles),
+// 6 k_countA, 7 k_rankB EST 4 (the full-set pass: point estimates, phase-1 selections).
 // units: pairs walked (engine kernels) or tile FLOPs 2 d x tile elements (Gram kernels).
 // No reference counterpart (the reference has no native kernels).
 int vr_ktimer_enable(int on);

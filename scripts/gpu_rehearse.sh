@@ -1,7 +1,8 @@
 #!/bin/bash
 # Multi-rank rehearsal on a one-GPU box: bench.py at world 2 over gloo (both ranks on
 # cuda:0; RCCL refuses two ranks on one device), then world 1 at the same N; the two
-# check fields (unit score, phase-1 choices) must agree.
+# check fields (unit score and CI, phase-1 choices) must be identical: the RDMs are
+# bit-identical at every world size (pipeline.py), and the scores exact integer statistics.
 # Usage (from the repo root, via gpurun): bash scripts/gpu_rehearse.sh [tag] [n]
 set -o pipefail
 tag=${1:-rehearse}; n=${2:-4000}
@@ -20,4 +21,5 @@ def line(f):  # gloo prints its connection lines to stdout too
 a = line(sys.argv[1] + "/w2.json"); b = line(sys.argv[1] + "/w1.json")
 print("world2", a["value"], a["check"]); print("world1", b["value"], b["check"])
 print("check equal:", a["check"] == b["check"])
+sys.exit(0 if a["check"] == b["check"] else 1)
 PY

@@ -1,18 +1,19 @@
 """Multi-GPU orchestration on CPU with gloo, world_size 2 and 3.
 
-The data path is the one bench.py runs over RCCL: each rank splits its stimulus rows
-(row statistics + centred bf16 hi/lo plane records) -> all-gather of the planes and
-statistics -> balanced upper-triangle tile ranges per rank -> packed tile ranges
-all-gathered and unpacked with their mirrors; units in contiguous ranges over ranks, one
-engine call per rank-local region group, all_gather_object merge.
+The data path is the one bench.py runs over RCCL: an RdmSchedule gives every RDM its
+owner(s) -- pieces cut at aligned tile boundaries for RDMs heavier than the per-rank mean --
+each rank sends its stimulus rows of an RDM to that RDM's owners (all_to_all_single), the
+owners compute their pieces from the full rows, and the packed pieces go only to the ranks
+whose units read the RDM; units in contiguous ranges over ranks, one engine call per
+rank-local region group, all_gather_object merge.
 
-On CPU only the device kernels are replaced: the five RdmKernels entry points
-(vr_rdm_split_rows_f32, vr_rdm_pearson_tiles_planes, vr_rdm_tiles_pack / unpack and the
-plane geometry queries) by a numpy emulation with the same record layout, and the engine
-(RankPlan / bootstrap_spearman_multi) by the oracle's midrank Spearman. Everything else
-- gathers, compaction, tile ranges, pack/unpack placement, unit grouping, the engine's
-Python wrappers and the merge - is the product code. The distributed RDMs must equal the
-emulation's single-process RDM bit for bit, and every unit the single-process oracle."""
+On CPU only the device kernels are replaced: the RdmKernels entry points (tiles from rows,
+pack, unpack) by a numpy emulation with the same tile layout, and the engine (RankPlan /
+bootstrap_spearman_multi) by the oracle's midrank Spearman. Everything else -- the
+schedule, the row and piece exchanges, unpack placement, unit grouping and the merge -- is
+the product code. Every RDM a rank holds must equal the emulation's single-process RDM bit
+for bit (the tile arithmetic does not depend on the world size), and every unit the
+single-process oracle."""
 import os
 import socket
 
@@ -30,34 +31,15 @@ from visreps_amd.dataloaders.synthetic import shard_rows
 
 
 class CpuKernels(P.RdmKernels):
-    """numpy emulation of the distributed RDM kernels, record layout included: per row,
-    per 32-feature stage, 32 bf16 hi values then 32 bf16 lo values of the centred row."""
+    """numpy emulation of the distributed RDM kernels: tiles of the float64 RDM of the
+    rows (rsa.py:76-92 arithmetic), rounded to fp32, written with their mirrors."""
 
     @staticmethod
-    def split_rows(x, correction):  # noqa: ARG004
-        rows, d = x.shape
-        ns = (d + 31) // 32
+    def tiles_from_rows(x, out, t0, t1, correction, times=None):  # noqa: ARG004
+        n, d = x.shape
         xd = x.double()
-        mean = xd.mean(1)
-        c = (xd - mean[:, None]).float()
-        std = torch.sqrt((c.double() ** 2).mean(1)).float()
-        pad = torch.zeros((rows, ns * 32), dtype=torch.float32)
-        pad[:, :d] = c
-        hi = pad.to(torch.bfloat16)
-        lo = (pad - hi.float()).to(torch.bfloat16)
-        planes = torch.zeros((rows, ns, 64), dtype=torch.int16)
-        planes[:, :, :32] = hi.view(torch.int16).view(rows, ns, 32)
-        planes[:, :, 32:] = lo.view(torch.int16).view(rows, ns, 32)
-        return planes.view(rows, ns * 64), mean.float(), std
-
-    @staticmethod
-    def tiles_from_planes(planes, mean, std, n, d, out, t0, t1, correction, times=None):  # noqa: ARG004
-        ns = (d + 31) // 32
-        pl = planes[:n].view(n, ns, 64)
-        hi = pl[:, :, :32].contiguous().view(torch.bfloat16).float()
-        lo = pl[:, :, 32:].contiguous().view(torch.bfloat16).float()
-        xc = (hi + lo).reshape(n, ns * 32)[:, :d].double()
-        s = std.double()
+        xc = xd - xd.mean(1, keepdim=True)
+        s = torch.sqrt((xc * xc).mean(1) + correction)
         for t in range(t0, t1):
             r0, c0, h, w = P.tile_rect(n, t)
             g = xc[r0:r0 + h] @ xc[c0:c0 + w].T / d
@@ -86,17 +68,11 @@ class CpuKernels(P.RdmKernels):
 
 def emulated_rdm(X: np.ndarray) -> np.ndarray:
     """The emulation's single-process RDM of all rows (one rank, every tile)."""
-    K = CpuKernels()
     x = torch.from_numpy(X)
-    n, d = x.shape
-    planes, mean, std = K.split_rows(x, 1e-12)
-    full = torch.zeros((K.plane_rows(n), planes.size(1)), dtype=torch.int16)
-    full[:n] = planes
+    n = x.size(0)
     out = torch.empty((n, n), dtype=torch.float32)
-    K.tiles_from_planes(full, mean, std, n, d, out, 0, int(P.lib().vr_rdm_tile_count(n)), 1e-12)
+    CpuKernels.tiles_from_rows(x, out, 0, int(P.lib().vr_rdm_tile_count(n)), 1e-12)
     return out.numpy()
-
-
 class _OraclePlan:
     """RankPlan stand-in: the RDM itself (n = its size)."""
 
@@ -154,53 +130,73 @@ def _data(n, d):
     return X, Y, Z
 
 
-def _worker(rank, world, port, n, d, n_boot, out_dir):
+def _row_boundaries(n, d):  # noqa: ARG001
+    """Every 128-tile row start: lets the small test RDMs be cut into pieces (the emulation
+    computes any range identically; the HIP kernel's own aligned cuts: test_gpu_distributed)."""
+    T = -(-n // P.TILE)
+    return [P._tri_start(r, T) for r in range(T)] + [int(P.lib().vr_rdm_tile_count(n))]
+
+
+def _worker(rank, world, port, n, d, n_boot, out_dir, split):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pg = dist.group.WORLD
     R.RankPlan = _OraclePlan  # the engine's kernels (see module doc)
     R.bootstrap_spearman_multi = _oracle_multi
+    if split:
+        P.aligned_boundaries = _row_boundaries
     K = CpuKernels()
     X, Y, Z = _data(n, d)
     rows = shard_rows(n, rank, world)
     loc = {k: torch.from_numpy(v[rows.start:rows.stop]) for k, v in {"x": X, "y": Y, "z": Z}.items()}
-    # as bench.py: every point's plane exchange in flight on its own group while the other
-    # collectives (neural RDMs, tile ranges, scores) run on pg
+    sched = P.make_schedule(n, {"x": d, "z": d}, ["x", "z"], {"r0": Y.shape[1], "r1": d}, world,
+                            split_factor=0.3 if split else 1.25)
+    if split:
+        assert any(len(p) > 1 for p in sched.pieces.values())
     feat_pg = dist.new_group(list(range(world)))
-    src = P.PrefetchedRDMs({"x": loc["x"], "z": loc["z"]}, ["x", "z"], n, pg, kernels=K, exchange_pg=feat_pg)
-    src.start_all()
-    rdm_y = P.distributed_rdm(loc["y"], n, pg, kernels=K)
-    res = P.all_units_rsa(src, ["x", "z"], {"r0": rdm_y, "r1": P.distributed_rdm(loc["x"], n, pg, kernels=K)},
-                          n, n_boot=n_boot, seed=42, pg=pg)
-    assert not src.pending
-    again = P.PrefetchedRDMs({"x": loc["x"]}, ["x"], n, pg, kernels=K)("x")
-    np.save(os.path.join(out_dir, f"rdm_y_{rank}.npy"), rdm_y.numpy())
-    np.save(os.path.join(out_dir, f"rdm_x_{rank}.npy"), again.numpy())
+    srcs = {("m", "x"): loc["x"], ("m", "z"): loc["z"], ("n", "r0"): loc["y"], ("n", "r1"): loc["x"]}
+    ex = P.ShardedRDMs(sched, srcs, pg, kernels=K, exchange_pg=feat_pg, window=1)
+    ex.start()
+    rd = ex.finish()
+    assert set(rd) == set(sched.needs(rank)) and not ex.pending
+    res = P.all_units_rsa(lambda p: rd[("m", p)], ["x", "z"], {r: rd[("n", r)] for r in ["r0", "r1"] if ("n", r) in rd},
+                          n, n_boot=n_boot, seed=42, pg=pg, regions=["r0", "r1"])
+    for (kind, name), m in rd.items():
+        np.save(os.path.join(out_dir, f"rdm_{kind}{name}_{rank}.npy"), m.numpy())
+    np.save(os.path.join(out_dir, f"rdm_all_{rank}.npy"), P.distributed_rdm(loc["z"], n, pg, kernels=K).numpy())
     with open(os.path.join(out_dir, f"res_{rank}.txt"), "w") as f:
         for k in sorted(res):
             f.write(f"{k[0]} {k[1]} {res[k]['score']:.17g} {res[k]['ci_low']:.17g} {res[k]['ci_high']:.17g}\n")
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,world", [(37, 2), (300, 2), (300, 3)])
-def test_gloo_distributed_rdm_and_units_match_single_process(tmp_path, n, world):
+@pytest.mark.parametrize("n,world,split", [(37, 2, False), (300, 2, False), (300, 3, False),
+                                          (300, 2, True), (400, 3, True)])
+def test_gloo_distributed_rdm_and_units_match_single_process(tmp_path, n, world, split):
     d, n_boot = 40, 6
-    mp.spawn(_worker, args=(world, _free_port(), n, d, n_boot, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, d, n_boot, str(tmp_path), split), nprocs=world, join=True)
     X, Y, Z = _data(n, d)
-    ref = {"x": emulated_rdm(X), "y": emulated_rdm(Y), "z": emulated_rdm(Z)}
-    assert np.max(np.abs(ref["x"] - O.compute_rdm(X))) < 1e-5  # the emulation is an RDM
+    ref = {"mx": emulated_rdm(X), "mz": emulated_rdm(Z), "nr0": emulated_rdm(Y), "nr1": emulated_rdm(X)}
+    assert np.max(np.abs(ref["mx"] - O.compute_rdm(X))) < 1e-5  # the emulation is an RDM
+    held = 0
     for r in range(world):
-        assert np.array_equal(np.load(tmp_path / f"rdm_y_{r}.npy"), ref["y"])
-        assert np.array_equal(np.load(tmp_path / f"rdm_x_{r}.npy"), ref["x"])
+        for key, m in ref.items():
+            f = tmp_path / f"rdm_{key}_{r}.npy"
+            if f.exists():
+                held += 1
+                assert np.array_equal(np.load(f), m), (key, r)
+        assert np.array_equal(np.load(tmp_path / f"rdm_all_{r}.npy"), ref["mz"])
+    assert held >= 4  # every RDM is held by at least one consumer
     lines = [(tmp_path / f"res_{r}.txt").read_text() for r in range(world)]
     assert all(l == lines[0] for l in lines)
     idx = bootstrap_indices(42, n, int(0.9 * n), n_boot)
-    neural = {"r0": ref["y"], "r1": ref["x"]}
+    models = {"x": ref["mx"], "z": ref["mz"]}
+    neural = {"r0": ref["nr0"], "r1": ref["nr1"]}
     got_units = set()
     for line in lines[0].splitlines():
         p, r, *vals = line.split()
         got_units.add((p, r))
-        a, b = ref[p], neural[r]
+        a, b = models[p], neural[r]
         sets = [np.arange(n)] + list(idx)
         sc = [O.midrank_spearman(a[np.ix_(s, s)][np.triu_indices(len(s), 1)],
                                  b[np.ix_(s, s)][np.triu_indices(len(s), 1)]) for s in sets]
@@ -210,10 +206,41 @@ def test_gloo_distributed_rdm_and_units_match_single_process(tmp_path, n, world)
     assert got_units == {(p, r) for p in ["x", "z"] for r in ["r0", "r1"]}
 
 
-def test_compact_and_padded_layout():
-    # rows of uneven shards land in rank order, zero tail rows after the last real one
-    sizes = [3, 2, 2]
-    full = torch.arange(9 * 2, dtype=torch.float32).view(9, 2)
-    out = P._compact(full, sizes, 9)
-    assert torch.equal(out[:3], full[0:3]) and torch.equal(out[3:5], full[3:5])
-    assert torch.equal(out[5:7], full[6:8]) and torch.all(out[7:] == 0)
+BENCH_DIMS = {"conv1_pre": 290400, "conv1_post": 290400, "conv2_pre": 186624, "conv2_post": 186624,
+              "conv3_pre": 64896, "conv3_post": 64896, "conv4_pre": 64896, "conv4_post": 64896,
+              "conv5_pre": 43264, "conv5_post": 43264, "fc1_pre": 4096, "fc1_post": 4096,
+              "fc2_pre": 4096, "fc2_post": 4096}
+BENCH_ROIS = {"V1": 2000, "V2": 2000, "V3": 2000, "hV4": 1000}
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_bench_schedule(world):
+    """The bench step's schedule (N = 10k, 14 points, 4 ROIs): every RDM is covered by its
+    pieces exactly once, pieces of one RDM sit on distinct ranks, every consumer is a rank
+    with a unit reading the RDM, units are balanced, and the Gram load per rank stays near
+    the mean (the conv1 points are cut at aligned super-tile rows when they exceed it)."""
+    n = 10000
+    s = P.make_schedule(n, BENCH_DIMS, list(BENCH_DIMS), BENCH_ROIS, world)
+    T = int(P.lib().vr_rdm_tile_count(n))
+    for name, pcs in s.pieces.items():
+        cover = sorted((pc.t0, pc.t1) for pc in pcs)
+        assert cover[0][0] == 0 and cover[-1][1] == T
+        assert all(cover[i][1] == cover[i + 1][0] for i in range(len(cover) - 1))
+        assert len({pc.owner for pc in pcs}) == len(pcs)
+    assert len(s.pieces) == 18
+    counts = [hi - lo for lo, hi in s.unit_ranges]
+    assert sum(counts) == 56 and max(counts) - min(counts) <= 1
+    for rk, (lo, hi) in enumerate(s.unit_ranges):
+        for p, r in s.units[lo:hi]:
+            assert rk in s.consumers[("m", p)] and rk in s.consumers[("n", r)]
+    mean = sum(s.load) / world
+    assert max(s.load) <= 1.35 * mean + 1e-9, (s.load, mean)
+    if world == 1:
+        assert all(len(p) == 1 for p in s.pieces.values())
+    if world >= 8:
+        assert len(s.pieces[("m", "conv1_pre")]) > 1  # the heaviest RDM is split
+
+
+def test_row_boundaries_for_split_tests_are_a_partition():
+    b = _row_boundaries(300, 40)
+    assert b[0] == 0 and b[-1] == int(P.lib().vr_rdm_tile_count(300)) and b == sorted(set(b))

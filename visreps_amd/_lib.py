@@ -46,6 +46,8 @@ _PROTOTYPES = {
         [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _vp, _c_sz, _vp],
     ),
     "vr_rdm_tile_count": (_c_i64, [_c_i64]),
+    "vr_rdm_wide_rows": (_c_i64, [_c_i64, _c_i64]),
+    "vr_rdm_range_aligned": (ctypes.c_int, [_c_i64, _c_i64, _c_i64, _c_i64]),
     "vr_rdm_tile_cost": (_c_i64, [_c_i64, _c_i64]),
     "vr_rdm_tile_rect": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "vr_rdm_tiles_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64]),
@@ -239,7 +241,7 @@ workspace = _WorkspacePool()
 
 
 KTIMER_KERNELS = {"k_rankB_est": 0, "k_rankB_exact": 1, "k_rankA": 2, "k_join": 3,
-                  "k_gram_wide": 4, "k_gram_tile": 5, "k_countA": 6}
+                  "k_gram_wide": 4, "k_gram_tile": 5, "k_countA": 6, "k_rankB_full": 7}
 
 
 def ktimer_enable(on: bool = True) -> None:

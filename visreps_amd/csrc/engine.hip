@@ -1337,7 +1337,7 @@ static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* c
   const uint32_t nseg = (uint32_t)(EST ? cfg.est_nwaves : cfg.nwaves);
   const size_t us = (size_t)E.useg * (size_t)u;
   {
-    KtScope kt(EST ? KT_RANKB_EST : KT_RANKB_EXACT, (double)M, st);
+    KtScope kt(EST == 4 ? KT_RANKB_FULL : EST ? KT_RANKB_EST : KT_RANKB_EXACT, (double)M, st);
     k_rankB<LDS, FULL, TBT, BTB, EST><<<EST ? cfg.est_grid : cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
         B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
         posA_byB, chunkA_byB, E.baseA, E.segB_tot + us, E.segB_part + us * PB_N, nseg, E.ftab,

@@ -73,14 +73,15 @@ __device__ inline uint32_t f32_sort_key(float f) {
 // before and after the one launch it brackets; vr_ktimer_read resolves them.
 namespace vr {
 enum KtKernel : int {
-  KT_RANKB_EST = 0,   // k_rankB, EST forms (3/4 and the probe forms 1/2)
+  KT_RANKB_EST = 0,   // k_rankB, EST forms over bootstrap subsets (EST 3; the probe forms 1/2)
   KT_RANKB_EXACT = 1, // k_rankB, exact chunk-base form (VISREPS_ENGINE_EST=0, flagged reruns)
   KT_RANKA = 2,       // k_rankA (both forms)
   KT_JOIN = 3,        // k_join / k_join_lo
   KT_GRAM_WIDE = 4,   // k_gram3p / k_gram3w (256^2 super-tiles)
   KT_GRAM_TILE = 5,   // k_gram3 / k_gram (128^2 tiles)
   KT_COUNTA = 6,      // k_countA
-  KT_N = 7
+  KT_RANKB_FULL = 7,  // k_rankB, EST 4: the pass holding the full stimulus set (point estimates)
+  KT_N = 8
 };
 bool ktimer_on();
 struct KtScope {

@@ -777,7 +777,7 @@ __global__ __launch_bounds__(W_THREADS, 1) void k_gram3w(GramParams P) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * W_STAGE];  // [buf][A/B]
   const int id = P.blk0 + (int)xcd_remap(blockIdx.x, (uint32_t)gridDim.x);
   int bi, bj;
-  band_tile(id, 0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension here
+  band_tile(id, P.tile0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension here
   const bool diag = (bi == bj);
   const int64_t row0 = (int64_t)bi * WT, col0 = (int64_t)bj * WT;
   const int ns = (int)P.nstage;
@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(W_THREADS, 1) void k_gram3p(GramParams P) {
   __shared__ __attribute__((aligned(16))) char lds[P_SLOTS * P_SLOT];
   const int id = P.blk0 + (int)xcd_remap(blockIdx.x, (uint32_t)gridDim.x);
   int bi, bj;
-  band_tile(id, 0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension here
+  band_tile(id, P.tile0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension here
   const bool diag = (bi == bj);
   const int64_t row0 = (int64_t)bi * WT, col0 = (int64_t)bj * WT;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1220,12 +1220,12 @@ static size_t range_partial(int64_t n, int64_t d, int64_t count, bool fit_one = 
 
 static int64_t tri_start(int64_t r, int64_t T) { return r * T - r * (r - 1) / 2; }
 
-// Super-tile rows [0, R) of the wide split kernel for a full-RDM launch (0: not used).
+// Super-tile rows [0, R) of the wide split kernel in a full-RDM launch (0: not used).
 // R is the largest whose super-tile count fits whole generations of one block per CU;
 // the 128-tile rows [2R, T) below them run on k_gram3 (generations + tail split).
 // VISREPS_GRAM_WIDE=0 turns the wide kernel off (A/B timing).
-static int gram_wide_rows(int64_t n, int64_t d, int64_t count, bool split3) {
-  if (!split3 || count != gram_tiles(n)) return 0;
+static int gram_wide_rows(int64_t n, int64_t d, bool split3) {
+  if (!split3) return 0;
   if (const char* e = getenv("VISREPS_GRAM_WIDE"))
     if (strcmp(e, "0") == 0) return 0;
   const int64_t T2 = (n + WT - 1) / WT, gen = num_cus();
@@ -1235,6 +1235,43 @@ static int gram_wide_rows(int64_t n, int64_t d, int64_t count, bool split3) {
   while (R + 1 <= T2 && tri_start(R + 1, T2) <= full) ++R;
   (void)d;
   return (int)R;
+}
+
+// How a launch over 128-tiles [t0, t1) runs. Every tile of an RDM is computed the same way
+// whatever range it is launched in -- the full-RDM decomposition (super-tile rows [0, R) on
+// the wide kernel, whole depth per tile; the remainder rows [2R, T) as one run_split) --
+// so a range whose ends are super-tile row starts (tri_start(2r, T), r <= R) or the end of
+// the triangle gives tiles bit-identical to the full launch: the multi-GPU path splits an
+// RDM only at those boundaries (vr_rdm_range_aligned). Other ranges (legacy callers) run
+// as one run_split of their own (split-K geometry of the range: last-bit differences).
+struct RangePlan {
+  bool wide = false;
+  int64_t s0 = 0, s1 = 0;          // super-tiles [s0, s1) of the wide kernel
+  int64_t rem0 = 0, rem_count = 0;  // 128-tiles of the run_split part
+  bool rem_fit = false;             // run_split's fit_one
+};
+
+static RangePlan plan_range(int64_t n, int64_t d, int64_t t0, int64_t t1, bool split3) {
+  RangePlan rp;
+  const int64_t total = gram_tiles(n), T = (n + GT - 1) / GT, T2 = (n + WT - 1) / WT;
+  const int R = gram_wide_rows(n, d, split3);
+  rp.rem0 = t0;
+  rp.rem_count = t1 - t0;
+  if (R == 0 || t1 <= t0) return rp;
+  int64_t r0 = -1, r1 = -1;
+  for (int64_t r = 0; r <= R; ++r) {
+    if (tri_start(2 * r, T) == t0) r0 = r;
+    if (tri_start(2 * r, T) == t1) r1 = r;
+  }
+  if (r0 < 0 || (t1 != total && r1 < 0)) return rp;  // not aligned: legacy run_split
+  const int64_t trem = tri_start(2 * (int64_t)R, T);
+  rp.wide = true;
+  rp.s0 = tri_start(r0, T2);
+  rp.s1 = t1 == total ? tri_start(R, T2) : tri_start(r1, T2);
+  rp.rem0 = trem;
+  rp.rem_count = t1 == total ? total - trem : 0;
+  rp.rem_fit = true;
+  return rp;
 }
 
 // Scratch of one RDM launch over `count` tiles: row stats, split-K partial tiles, and the
@@ -1251,13 +1288,11 @@ static size_t gram_fbuf_floats() {
   return std::max<size_t>((size_t)2 * num_cus() * GT * GT, (size_t)num_cus() * WT * WT);
 }
 
-static size_t gram_ws(int64_t n, int64_t d, int64_t count, bool split3, void* base, float** mean,
+static size_t gram_ws(int64_t n, int64_t d, int64_t t0, int64_t t1, bool split3, void* base, float** mean,
                       float** stdv, float** partial, uint16_t** planes, float** fbuf = nullptr,
                       bool own_planes = true) {
-  const int64_t T = (n + GT - 1) / GT;
-  const int R = gram_wide_rows(n, d, count, split3);
-  const int64_t rest = R > 0 ? count - tri_start(2 * (int64_t)R, T) : count;
-  const size_t part = range_partial(n, d, rest, R > 0);
+  const RangePlan rp = plan_range(n, d, t0, t1, split3);
+  const size_t part = range_partial(n, d, rp.rem_count, rp.rem_fit);
   Carver c(base);
   float* m = c.take<float>((size_t)n);
   float* s = c.take<float>((size_t)n);
@@ -1283,16 +1318,27 @@ extern "C" {
 
 size_t vr_rdm_pearson_workspace(int64_t n, int64_t d) {
   if (n <= 0 || d <= 0) return 256;
-  return gram_ws(n, d, gram_tiles(n), gram_split(n, d), nullptr, nullptr, nullptr, nullptr, nullptr);
+  return gram_ws(n, d, 0, gram_tiles(n), gram_split(n, d), nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
 size_t vr_rdm_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
   if (n <= 0 || d <= 0 || tile_end <= tile_begin) return 256;
-  return gram_ws(n, d, tile_end - tile_begin, gram_split(n, d), nullptr, nullptr, nullptr, nullptr,
+  return gram_ws(n, d, tile_begin, tile_end, gram_split(n, d), nullptr, nullptr, nullptr, nullptr,
                  nullptr);
 }
 
 int64_t vr_rdm_tile_count(int64_t n) { return n > 0 ? gram_tiles(n) : 0; }
+
+int64_t vr_rdm_wide_rows(int64_t n, int64_t d) {
+  return n > 0 && d > 0 ? gram_wide_rows(n, d, gram_split(n, d)) : 0;
+}
+
+int vr_rdm_range_aligned(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
+  if (n <= 0 || d <= 0 || tile_begin < 0 || tile_end > gram_tiles(n) || tile_end < tile_begin) return 0;
+  if (tile_begin == tile_end) return 1;
+  if (tile_begin == 0 && tile_end == gram_tiles(n)) return 1;
+  return plan_range(n, d, tile_begin, tile_end, gram_split(n, d)).wide ? 1 : 0;
+}
 
 int64_t vr_rdm_tile_cost(int64_t n, int64_t tile) {
   // elements of the tile on or above the diagonal (the work the balancer spreads)
@@ -1369,7 +1415,7 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   const bool split3 = bf16 || pre.planes || gram_split(n, d);
   float *mean, *stdv;
   uint16_t* planes;
-  gram_ws(n, d, tile_end - tile_begin, split3, ws, &mean, &stdv, &P.partial, &planes, &P.fbuf,
+  gram_ws(n, d, tile_begin, tile_end, split3, ws, &mean, &stdv, &P.partial, &planes, &P.fbuf,
           pre.planes == nullptr);
   const int flush_stages = P.fbuf ? gram_flush_stages() : 0;
   P.raw = raw ? 1 : 0;
@@ -1439,14 +1485,14 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
     VR_TRY(run_range(t0, count - tail, false));
     return run_range(t0 + count - tail, tail, true);
   };
-  const int64_t count = tile_end - tile_begin;
-  const int R = gram_wide_rows(n, d, count, split3);
-  if (R == 0) return run_split(tile_begin, count, false);
-  // wide super-tiles over rows [0, 2R * 128), then the 128-tile rows below them
+  const RangePlan rp = plan_range(n, d, tile_begin, tile_end, split3);
+  if (!rp.wide) return run_split(tile_begin, tile_end - tile_begin, false);
+  // wide super-tiles [s0, s1) (rows of the full RDM's wide part), then the 128-tile rows
+  // below them when the range holds them
   GramParams W = P;
   W.T = (int)((n + WT - 1) / WT);
-  W.tile0 = 0;
-  W.tile_count = (int)tri_start(R, W.T);
+  W.tile0 = (int)rp.s0;
+  W.tile_count = (int)(rp.s1 - rp.s0);
   W.splits = 1;
   const int gen = num_cus();
   const bool pipe = gram_pipe();
@@ -1460,8 +1506,7 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
       k_gram3w<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
     VR_CHECK_LAUNCH();
   }
-  const int64_t t0 = tri_start(2 * (int64_t)R, P.T);
-  return run_split(t0, gram_tiles(n) - t0, true);
+  return run_split(rp.rem0, rp.rem_count, true);
 }
 
 int vr_rdm_pearson_f32(const float* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
@@ -1494,7 +1539,7 @@ int vr_rdm_pearson_tiles_f32(const float* X, int64_t n, int64_t d, int64_t ldx, 
 
 size_t vr_rdm_bf16_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
   if (n <= 0 || d <= 0 || tile_end <= tile_begin) return 256;
-  return gram_ws(n, d, tile_end - tile_begin, true, nullptr, nullptr, nullptr, nullptr, nullptr);
+  return gram_ws(n, d, tile_begin, tile_end, true, nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
 int vr_rdm_pearson_tiles_bf16(const uint16_t* X, int64_t n, int64_t d, int64_t ldx, float* rdm,
@@ -1551,7 +1596,7 @@ int vr_rdm_split_rows_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, 
 
 size_t vr_rdm_planes_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end) {
   if (n <= 0 || d <= 0 || tile_end <= tile_begin) return 256;
-  return gram_ws(n, d, tile_end - tile_begin, true, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+  return gram_ws(n, d, tile_begin, tile_end, true, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                  false);
 }
 

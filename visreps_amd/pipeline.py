@@ -4,11 +4,12 @@ multi-GPU path of the eval driver).
 Per step (BASELINE.json configs[1]: CustomCNN points x NSD ROIs, N stimuli, 1000 boots):
   1. extraction   each rank forwards its stimulus shard; the 14 hooked points are
                   flattened into per-point (n_local, D) HBM buffers;
-  2. RDMs         per point / ROI: each rank splits its own rows (row statistics +
-                  centred bf16 hi/lo planes), RCCL all-gathers the planes (the one
-                  feature exchange), computes a cost-balanced range of the 128x128
-                  upper-triangle Gram tiles, and the packed tile ranges are all-gathered
-                  and unpacked (with their mirrors) into every rank's RDM;
+  2. RDMs         an RdmSchedule (the same on every rank) gives every RDM (14 points, 4
+                  ROIs) an owner, or, for an RDM heavier than the per-rank mean, a few
+                  owners of pieces cut at the wide kernel's super-tile rows. Each rank
+                  sends its rows of an RDM to that RDM's owners only (all_to_all_single
+                  over RCCL), each owner computes its pieces with the one-GPU kernel path,
+                  and the packed pieces go only to the ranks whose units read the RDM;
   3. rank plans   each rank sorts the triangles of the RDMs its units use;
   4. units        (point, ROI) units listed ROI-major, one contiguous range per rank; a
                   rank's units sharing a ROI are one engine call (vr_bootstrap_spearman_multi:
@@ -16,11 +17,10 @@ Per step (BASELINE.json configs[1]: CustomCNN points x NSD ROIs, N stimuli, 1000
                   is the point estimate + n_boot subsets (evals.py:341-373 semantics,
                   RandomState(seed) per unit);
   5. gather       per-unit score vectors are gathered to every rank.
-Given the RDMs, scores are exact-integer Spearman values and do not depend on how units
-are split over ranks. The RDM entries themselves can differ in the last fp32 bits between
-world sizes: the Gram's split-K factor and the wide 256x256 kernel are chosen per launched
-tile range (csrc/rdm.hip), so a rank's range may sum a tile in another order than the
-one-GPU launch (tests/test_gpu_parity.py::test_rdm_tile_ranges_wide_d_match_within_rounding).
+Every tile of an RDM is computed by the same kernel, over the same depth order, whatever
+rank computes it (pieces are cut only at aligned boundaries, csrc/rdm.hip plan_range), so
+the RDMs -- and, the statistic being exact integer arithmetic, the scores -- are bit-identical
+at every world size (tests/test_distributed.py, tests/test_gpu_distributed.py).
 """
 from __future__ import annotations
 
@@ -154,46 +154,12 @@ def _gram_exact_fp32() -> bool:
 class RdmKernels:
     """The HIP entry points of the distributed RDM (csrc/rdm.hip). The orchestration below
     calls nothing else on the device, so the gloo tests substitute a CPU emulation of
-    exactly these five calls and run the orchestration itself unchanged."""
+    exactly these calls and run the orchestration itself unchanged."""
 
     @staticmethod
-    def plane_rows(n: int) -> int:
-        return int(lib().vr_rdm_plane_rows(n))
-
-    @staticmethod
-    def plane_elems(d: int) -> int:  # uint16 elements per row of plane records
-        return int(lib().vr_rdm_plane_row_bytes(d)) // 2
-
-    @staticmethod
-    def split_rows(x: torch.Tensor, correction: float):
-        """(planes (rows, plane_elems) int16, mean (rows,), std (rows,)) of local rows."""
-        rows, d = x.shape
-        planes = torch.empty((rows, RdmKernels.plane_elems(d)), dtype=torch.int16, device=x.device)
-        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
-        std = torch.empty(rows, dtype=torch.float32, device=x.device)
-        if rows:
-            check(lib().vr_rdm_split_rows_f32(x.data_ptr(), rows, d, x.stride(0), float(correction),
-                                              mean.data_ptr(), std.data_ptr(), planes.data_ptr(),
-                                              stream_of(x.device)), "vr_rdm_split_rows_f32")
-        return planes, mean, std
-
-    @staticmethod
-    def tiles_from_planes(planes, mean, std, n: int, d: int, out: torch.Tensor, t0: int, t1: int,
-                          correction: float, times: Optional[StepTimes] = None) -> None:
-        if t1 <= t0:
-            return
-        L = lib()
-        ws = workspace.get(out.device, L.vr_rdm_planes_tiles_workspace(n, d, t0, t1), "rdm")
-        ev = None
-        if times is not None:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
-        check(L.vr_rdm_pearson_tiles_planes(planes.data_ptr(), mean.data_ptr(), std.data_ptr(), n, d,
-                                            out.data_ptr(), n, float(correction), t0, t1, ws.data_ptr(),
-                                            ws.numel(), stream_of(out.device)), "vr_rdm_pearson_tiles_planes")
-        if times is not None:
-            ev[1].record()
-            times.record("gram", ev[0], ev[1], _gram_flops(n, d) * _tile_fraction(n, t0, t1))
+    def tiles_from_rows(x, out, t0, t1, correction, times=None) -> None:
+        """Gram tiles [t0, t1) of x's RDM (+ mirrors) into out (vr_rdm_pearson_tiles_f32)."""
+        rdm_tiles_into(x, out, t0, t1, correction, times)
 
     @staticmethod
     def pack(out: torch.Tensor, n: int, t0: int, t1: int, packed: torch.Tensor) -> None:
@@ -205,184 +171,276 @@ class RdmKernels:
         check(lib().vr_rdm_tiles_unpack(packed.data_ptr(), n, t0, t1, out.data_ptr(), n,
                                         stream_of(out.device)), "vr_rdm_tiles_unpack")
 
-    @staticmethod
-    def tiles_from_rows(x, out, t0, t1, correction, times=None) -> None:
-        rdm_tiles_into(x, out, t0, t1, correction, times)
-
 
 KERNELS = RdmKernels()
 TILE = 128  # floats per packed tile edge (csrc/rdm.hip GT)
 
 
-def _all_gather_padded(t: torch.Tensor, sizes: Sequence[int], pg, async_op: bool = False):
-    """All-gather of a rank-local (sizes[rank], ...) tensor, padded to max(sizes) rows;
-    returns (work, buffer (world * per, ...), send buffer)."""
-    world = len(sizes)
-    per = max(sizes)
-    send = torch.zeros((per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    send[: t.size(0)] = t
-    full = torch.empty((world * per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    if dist.get_backend(pg) == "nccl":
-        work = dist.all_gather_into_tensor(full, send, group=pg, async_op=async_op)
-    else:  # gloo: the CPU tests of the orchestration
-        work = dist.all_gather(list(full.chunk(world)), send, group=pg, async_op=async_op)
-    return work, full, send
+def _tri_start(r: int, t: int) -> int:
+    return r * t - r * (r - 1) // 2
 
 
-def _compact(full: torch.Tensor, sizes: Sequence[int], rows_out: int) -> torch.Tensor:
-    """Rows of every rank's slot of a padded gather, in rank order, into (rows_out, ...)
-    with zero rows after the last real one."""
-    per = max(sizes)
-    out = torch.zeros((rows_out,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
-    at = 0
-    for r, sz in enumerate(sizes):
-        out[at:at + sz] = full[r * per: r * per + sz]
-        at += sz
-    return out
+def aligned_boundaries(n: int, d: int) -> List[int]:
+    """128-tile indices where an RDM may be cut so that every piece's tiles are
+    bit-identical to the one-launch RDM (csrc/rdm.hip plan_range): the starts of the wide
+    kernel's super-tile rows, tri_start(2r, T) for r <= R, and the end of the triangle (the
+    remainder rows below 2R travel with the last piece)."""
+    total = int(lib().vr_rdm_tile_count(n))
+    R = int(lib().vr_rdm_wide_rows(n, d)) if d > 0 else 0
+    T = -(-n // TILE)
+    b = [_tri_start(2 * r, T) for r in range(R + 1)] if R > 0 else [0]
+    return sorted(set(b + [total]))
 
 
-class _Gathered:
-    """The exchanged rows of one point, ready for the rank's tile range."""
+@dataclass(frozen=True)
+class GramPiece:
+    """Tiles [t0, t1) of one RDM, computed by rank `owner`."""
 
-    def __init__(self, kind: str, n: int, d: int, **parts):
-        self.kind, self.n, self.d, self.parts = kind, n, d, parts
-
-
-def gather_point_async(x_local: torch.Tensor, n: int, pg, correction: float = 1e-12,
-                       kernels: RdmKernels = None):
-    """Start one point's feature exchange; returns finish() -> _Gathered.
-
-    Split path (default): the rank splits its OWN rows (row statistics + centred bf16
-    hi/lo plane records, vr_rdm_split_rows_f32) and the planes and statistics are
-    all-gathered, so no rank recomputes another rank's prepass. Exact-fp32 Gram
-    (VISREPS_GRAM=fp32): the fp32 rows themselves. The collective runs on the
-    communicator's stream, so work already queued on the compute stream overlaps it."""
-    K = kernels or KERNELS
-    rank, world = _world(pg)
-    x_local = x_local.float().contiguous()
-    d = x_local.size(1)
-    sizes = [len(shard_rows(n, r, world)) for r in range(world)]
-    if _gram_exact_fp32():
-        work, full, send = _all_gather_padded(x_local, sizes, pg, async_op=True)
-
-        def finish_rows(_keep=send) -> _Gathered:
-            work.wait()
-            return _Gathered("rows", n, d, x=_compact(full, sizes, n))
-
-        return finish_rows
-    planes, mean, std = K.split_rows(x_local, correction)
-    stats = torch.stack([mean, std], dim=1)
-    # plane records travel as 8-byte words (RCCL and gloo have no 16-bit integer type; a
-    # row is nstage x 128 B, and 8-B elements keep the element count of a 10k x 290,400
-    # point (11.6 GB) below 2^31)
-    w1, pfull, s1 = _all_gather_padded(planes.view(torch.int64), sizes, pg, async_op=True)
-    w2, sfull, s2 = _all_gather_padded(stats, sizes, pg, async_op=True)
-
-    def finish_planes(_keep=(s1, s2)) -> _Gathered:
-        w1.wait()
-        w2.wait()
-        st = _compact(sfull, sizes, n)
-        return _Gathered("planes", n, d, planes=_compact(pfull, sizes, K.plane_rows(n)).view(torch.int16),
-                         mean=st[:, 0].contiguous(), std=st[:, 1].contiguous())
-
-    return finish_planes
+    owner: int
+    t0: int
+    t1: int
 
 
-def rdm_from_gathered(g: _Gathered, pg, times: Optional[StepTimes] = None, correction: float = 1e-12,
-                      kernels: RdmKernels = None) -> torch.Tensor:
-    """Every rank computes its balanced tile range (tile_ranges) into the (n, n) RDM, packs
-    it (128 x 128 floats per tile), and the packed ranges are all-gathered and unpacked
-    (tile + mirror) into every rank's RDM. Every entry is written by exactly one rank's
-    tile, so there is no zero fill and no sum: each rank receives about n^2/2 floats
-    instead of the 2 n^2 a ring sum all-reduce of the full matrix moves."""
-    K = kernels or KERNELS
-    rank, world = _world(pg)
-    n = g.n
-    dev = g.parts["planes"].device if g.kind == "planes" else g.parts["x"].device
-    out = torch.empty((n, n), dtype=torch.float32, device=dev)
-    ranges = tile_ranges(n, world) if world > 1 else [(0, int(lib().vr_rdm_tile_count(n)))]
-    t0, t1 = ranges[rank]
-    if g.kind == "planes":
-        K.tiles_from_planes(g.parts["planes"], g.parts["mean"], g.parts["std"], n, g.d, out, t0, t1,
-                            correction, times)
-    else:
-        K.tiles_from_rows(g.parts["x"], out, t0, t1, correction, times)
-    if world == 1:
-        return out
-    counts = [b - a for a, b in ranges]
-    packed = torch.empty((t1 - t0, TILE * TILE), dtype=torch.float32, device=dev)
-    if t1 > t0:
-        K.pack(out, n, t0, t1, packed)
-    _, allp, _keep = _all_gather_padded(packed, counts, pg)
-    per = max(counts)
-    for r, (a, b) in enumerate(ranges):
-        if r != rank and b > a:
-            K.unpack(allp[r * per: r * per + (b - a)], n, a, b, out)
-    return out
+@dataclass
+class RdmSchedule:
+    """Who computes and who needs every RDM of a step (pure function of the shapes and the
+    world size: every rank builds the same one).
+
+    units      (point, region) pairs, region-major; rank r runs units[lo:hi] of unit_ranges[r]
+    consumers  name -> ranks whose units read that RDM (name = ("m", point) / ("n", region))
+    pieces     name -> Gram pieces (owner, 128-tile range), cut only at aligned boundaries
+    load       per-rank Gram cost (n(n+1)d-proportional tile elements x d)"""
+
+    world: int
+    n: int
+    units: List[Tuple[str, str]]
+    unit_ranges: List[Tuple[int, int]]
+    consumers: Dict[Tuple[str, str], List[int]]
+    pieces: Dict[Tuple[str, str], List[GramPiece]]
+    load: List[float]
+
+    def needs(self, rank: int) -> List[Tuple[str, str]]:
+        return [k for k, c in self.consumers.items() if rank in c]
+
+    def owners(self, name) -> List[int]:
+        return sorted({p.owner for p in self.pieces[name]})
 
 
-def gather_rows(x_local: torch.Tensor, n: int, pg) -> torch.Tensor:
-    """RCCL all-gather of every rank's stimulus rows into the full (n, d) matrix."""
-    rank, world = _world(pg)
-    if world == 1:
-        return x_local
-    sizes = [len(shard_rows(n, r, world)) for r in range(world)]
-    work, full, _keep = _all_gather_padded(x_local, sizes, pg)
-    return _compact(full, sizes, n)
+def make_schedule(n: int, dims: Dict[str, int], points: Sequence[str], regions: Dict[str, int],
+                  world: int, split_factor: float = 1.25) -> RdmSchedule:
+    """Units: region-major, one contiguous range per rank (unit_split), so a rank's units
+    share their neural RDM (one A walk per engine call). Grams: one owner per RDM, longest
+    first onto the least-loaded rank (a consumer of the RDM when it is within 2 % of the
+    least load, which saves one transfer); an RDM costing more than split_factor x the
+    per-rank mean is cut at aligned boundaries into that many near-equal pieces on distinct
+    ranks. Each owner receives the full rows of its RDMs; consumers receive the packed
+    tiles of the pieces they lack."""
+    units = [(p, r) for r in regions for p in points]
+    ranges = unit_split(units, world)
+    consumers: Dict[Tuple[str, str], List[int]] = {}
+    for rk, (lo, hi) in enumerate(ranges):
+        for p, r in units[lo:hi]:
+            consumers.setdefault(("m", p), [])
+            consumers.setdefault(("n", r), [])
+            if rk not in consumers[("m", p)]:
+                consumers[("m", p)].append(rk)
+            if rk not in consumers[("n", r)]:
+                consumers[("n", r)].append(rk)
+    width = {("m", p): int(dims[p]) for p in points}
+    width.update({("n", r): int(v) for r, v in regions.items()})
+    pieces, load = assign_grams(n, {k: w for k, w in width.items() if k in consumers}, consumers, world,
+                                split_factor)
+    return RdmSchedule(world, n, units, ranges, consumers, pieces, load)
 
 
-class PrefetchedRDMs:
-    """RDM source for all_units_rsa over stimulus-sharded features: asking for point
-    points[i] first starts the exchange of points[i + 1] (gather_point_async), so the next
-    point's plane all-gather overlaps this point's Gram. Every rank asks for the points in
-    the same order (all_units_rsa walks `points`), so the collectives are issued in one
-    order.
+def assign_grams(n: int, width: Dict, consumers: Dict, world: int, split_factor: float = 1.25):
+    """Gram pieces of the RDMs `width` (name -> feature width) over `world` ranks (see
+    make_schedule). Returns (pieces {name: [GramPiece]}, per-rank load)."""
+    cum = _tile_cum_cost(n)
+    cost = {k: float(cum[-1]) * w for k, w in width.items()}
+    mean = sum(cost.values()) / world
+    load = [0.0] * world
+    pieces: Dict = {}
+    for k in sorted(cost, key=lambda x: (-cost[x], x)):
+        npieces = 1
+        if world > 1 and cost[k] > split_factor * mean:
+            npieces = min(world, max(2, int(math.ceil(cost[k] / mean - 1e-9))))
+        cuts = [0, len(cum) - 1]
+        if npieces > 1:
+            bnd = aligned_boundaries(n, width[k])
+            cuts = [0]
+            for j in range(1, npieces):
+                target = cum[-1] * j / npieces
+                b = min(bnd, key=lambda t: abs(cum[t] - target))
+                if cuts[-1] < b < bnd[-1]:
+                    cuts.append(b)
+            cuts.append(len(cum) - 1)
+        used: List[int] = []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            c = cost[k] * (cum[b] - cum[a]) / cum[-1]
+            free = [rk for rk in range(world) if rk not in used]
+            least = min(load[rk] for rk in free)
+            near = [rk for rk in free if rk in consumers.get(k, []) and load[rk] <= least + 0.02 * mean]
+            rk = near[0] if near else min(free, key=lambda q: (load[q], q))
+            used.append(rk)
+            load[rk] += c
+            pieces.setdefault(k, []).append(GramPiece(rk, int(a), int(b)))
+    return pieces, load
 
-    exchange_pg: a second process group (its own RCCL communicator and stream) for the
-    plane all-gathers. With it, start_all() issues every point's exchange at once: they
-    stream over xGMI while phase 1, the neural RDMs and the first points' Grams run, and
-    the collectives on `pg` (phase-1 rows, packed tile ranges, scores) do not queue
-    behind them. All ranks call start_all() at the same point of the step."""
 
-    def __init__(self, feats: Dict[str, torch.Tensor], points: Sequence[str], n: int, pg=None,
-                 times: Optional[StepTimes] = None, kernels: RdmKernels = None, exchange_pg=None):
-        self.feats, self.points, self.n, self.pg, self.times = feats, list(points), n, pg, times
+def _all_to_all_rows(send_parts: List[Optional[torch.Tensor]], recv_rows: List[int], row_shape, dtype,
+                     device, pg, async_op: bool = False):
+    """all_to_all_single of row blocks: send_parts[j] (rows, ...) goes to rank j (None = 0
+    rows); returns (work, recv (sum(recv_rows), ...)) with rank i's block at its offset."""
+    world = len(recv_rows)
+    empty = torch.empty((0,) + tuple(row_shape), dtype=dtype, device=device)
+    parts = [pt if pt is not None else empty for pt in send_parts]
+    inp = torch.cat(parts, 0) if any(pt.size(0) for pt in parts) else empty
+    out = torch.empty((sum(recv_rows),) + tuple(row_shape), dtype=dtype, device=device)
+    in_splits = [int(pt.size(0)) for pt in parts]
+    if inp.is_cuda and dist.get_backend(pg) != "nccl":
+        # gloo has no all-to-all of device tensors: only the one-GPU rehearsal of the multi-rank
+        # path takes this (scripts/gpu_rehearse.sh); RCCL moves device memory directly
+        host = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(host, inp.cpu(), output_split_sizes=list(recv_rows), input_split_sizes=in_splits,
+                               group=pg)
+        out.copy_(host)
+        return _Done(), out, inp
+    work = dist.all_to_all_single(out, inp, output_split_sizes=list(recv_rows), input_split_sizes=in_splits,
+                                  group=pg, async_op=async_op)
+    return work, out, inp
+
+
+class _Done:
+    def wait(self):
+        return True
+
+
+class ShardedRDMs:
+    """The step's RDMs over stimulus-sharded rows (RdmSchedule):
+
+      start()   issues the row exchanges: every rank sends its rows of each RDM to that
+                RDM's owner(s) (all_to_all_single on exchange_pg; at most `window` RDMs'
+                rows in flight per rank, the rest issued as Grams complete);
+      finish()  each owner computes its pieces from the full rows (tiles bit-identical to the
+                one-GPU launch), the packed pieces go to the consumers that lack them
+                (all_to_all_single), and each consumer unpacks only the RDMs its units read.
+    Returns {name: (n, n) RDM} for this rank's names. One rank: every RDM is one launch."""
+
+    def __init__(self, sched: RdmSchedule, rows: Dict[Tuple[str, str], torch.Tensor], pg=None,
+                 times: Optional[StepTimes] = None, kernels: RdmKernels = None, exchange_pg=None,
+                 window: int = 4, correction: float = 1e-12):
+        self.sched, self.rows, self.pg, self.times = sched, rows, pg, times
         self.kernels = kernels or KERNELS
         self.exchange_pg = exchange_pg if exchange_pg is not None else pg
-        self.pending: Dict[str, Callable[[], _Gathered]] = {}
+        self.window, self.correction = max(1, int(window)), correction
+        self.rank, self.world = _world(pg)
+        # exchange order: longest Gram first, so the big owners start first
+        self.order = sorted(sched.pieces, key=lambda k: (-sum(pc.t1 - pc.t0 for pc in sched.pieces[k])
+                                                          * int(rows[k].size(1)), k))
+        self.pending: Dict[Tuple[str, str], Callable[[], Optional[torch.Tensor]]] = {}
+        self._next = 0
 
-    def _start(self, p: str) -> None:
-        if p not in self.pending:
-            self.pending[p] = gather_point_async(self.feats[p], self.n, self.exchange_pg, kernels=self.kernels)
+    def _issue(self) -> None:
+        k = self.order[self._next]
+        self._next += 1
+        x = self.rows[k].float().contiguous()
+        n, world = self.sched.n, self.world
+        owners = self.sched.owners(k)
+        sizes = [len(shard_rows(n, r, world)) for r in range(world)]
+        send = [x if r in owners else None for r in range(world)]
+        recv = sizes if self.rank in owners else [0] * world
+        work, full, keep = _all_to_all_rows(send, recv, x.shape[1:], x.dtype, x.device, self.exchange_pg,
+                                            async_op=True)
 
-    def start_all(self) -> None:
-        if _world(self.pg)[1] > 1:
-            for p in self.points:
-                self._start(p)
+        def done(_keep=keep):
+            work.wait()
+            return full if self.rank in owners else None
 
-    def __call__(self, p: str) -> torch.Tensor:
-        if _world(self.pg)[1] == 1:  # one GPU: the single-launch RDM (no exchange, no prepass split)
-            return distributed_rdm(self.feats[p], self.n, None, self.times)
-        self._start(p)
-        i = self.points.index(p)
-        if i + 1 < len(self.points):
-            self._start(self.points[i + 1])
-        g = self.pending.pop(p)()
-        return rdm_from_gathered(g, self.pg, self.times, kernels=self.kernels)
+        self.pending[k] = done
+
+    def start(self) -> None:
+        if self.world > 1:
+            while self._next < len(self.order) and len(self.pending) < self.window:
+                self._issue()
+
+    def finish(self) -> Dict[Tuple[str, str], torch.Tensor]:
+        n, K, rank = self.sched.n, self.kernels, self.rank
+        mine = set(self.sched.needs(rank))
+        if self.world == 1:
+            out = {}
+            for k in self.order:
+                x = self.rows[k].float().contiguous()
+                o = torch.empty((n, n), dtype=torch.float32, device=x.device)
+                K.tiles_from_rows(x, o, 0, int(lib().vr_rdm_tile_count(n)), self.correction, self.times)
+                out[k] = o
+            return out
+        self.start()
+        dev = next(iter(self.rows.values())).device
+        bufs: Dict[Tuple[str, str], torch.Tensor] = {}
+        # 1. every owned piece, in exchange order (rows of later RDMs arriving meanwhile)
+        for k in self.order:
+            while k not in self.pending:
+                self._issue()
+            full = self.pending.pop(k)()
+            if self._next < len(self.order):
+                self._issue()  # keep the window full
+            mine_pieces = [pc for pc in self.sched.pieces[k] if pc.owner == rank]
+            if not mine_pieces:
+                continue
+            o = bufs.setdefault(k, torch.empty((n, n), dtype=torch.float32, device=dev))
+            for pc in mine_pieces:
+                K.tiles_from_rows(full, o, pc.t0, pc.t1, self.correction, self.times)
+            del full
+        # 2. packed pieces to the consumers that lack them; unpack only what this rank reads
+        out = {}
+        for k in self.order:
+            pcs = self.sched.pieces[k]
+            cons = self.sched.consumers[k]
+            send: List[Optional[torch.Tensor]] = [None] * self.world
+            recv = [0] * self.world
+            for pc in pcs:
+                if pc.owner == rank:
+                    packed = torch.empty((pc.t1 - pc.t0, TILE * TILE), dtype=torch.float32, device=dev)
+                    K.pack(bufs[k], n, pc.t0, pc.t1, packed)
+                    for c in cons:
+                        if c != rank:
+                            send[c] = packed if send[c] is None else torch.cat([send[c], packed], 0)
+                if rank in cons and pc.owner != rank:
+                    recv[pc.owner] += pc.t1 - pc.t0
+            if any(x is not None for x in send) or any(recv):
+                pass  # every rank joins every RDM's exchange (collective order)
+            _, got, _ = _all_to_all_rows(send, recv, (TILE * TILE,), torch.float32, dev, self.pg)
+            if k in mine:
+                o = bufs.pop(k, None)
+                if o is None:
+                    o = torch.empty((n, n), dtype=torch.float32, device=dev)
+                at = 0
+                for pc in sorted(pcs, key=lambda q: (q.owner, q.t0)):
+                    if pc.owner != rank:
+                        K.unpack(got[at: at + pc.t1 - pc.t0], n, pc.t0, pc.t1, o)
+                        at += pc.t1 - pc.t0
+                out[k] = o
+            else:
+                bufs.pop(k, None)
+        return out
 
 
 def distributed_rdm(x_local: torch.Tensor, n: int, pg=None, times: Optional[StepTimes] = None,
                     kernels: RdmKernels = None) -> torch.Tensor:
-    """Full (n, n) RDM on every rank from each rank's stimulus rows (gather_point_async +
-    rdm_from_gathered). One GPU: the single-launch RDM of the local rows."""
+    """Full (n, n) RDM on every rank from each rank's stimulus rows: one RDM scheduled as a
+    region every rank consumes (ShardedRDMs). One GPU: the single-launch RDM."""
     rank, world = _world(pg)
     if world == 1:
         x = x_local.float().contiguous()
         out = torch.empty((n, n), dtype=torch.float32, device=x.device)
-        rdm_tiles_into(x, out, 0, int(lib().vr_rdm_tile_count(n)), times=times)
+        (kernels or KERNELS).tiles_from_rows(x, out, 0, int(lib().vr_rdm_tile_count(n)), 1e-12, times)
         return out
-    g = gather_point_async(x_local, n, pg, kernels=kernels)()
-    return rdm_from_gathered(g, pg, times, kernels=kernels)
+    name = ("n", "x")
+    cons = {name: list(range(world))}
+    pieces, load = assign_grams(n, {name: int(x_local.size(1))}, cons, world)
+    sched = RdmSchedule(world, n, [], [(0, 0)] * world, cons, pieces, load)
+    return ShardedRDMs(sched, {name: x_local}, pg, times, kernels).finish()[name]
 
 
 # ---------------------------------------------------------------------------------------
@@ -532,16 +590,18 @@ def summarize(scores: np.ndarray, bootstrap: bool) -> Dict:
 def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[str],
                   neural_rdms: Dict[str, torch.Tensor], n: int, *, n_boot: int = 1000,
                   seed: int = 42, pg=None, times: Optional[StepTimes] = None,
-                  keep_plans: bool = False, plan_fn=None, unit_fn=None, group_fn=None
-                  ) -> Dict[Tuple[str, str], Dict]:
+                  keep_plans: bool = False, plan_fn=None, unit_fn=None, group_fn=None,
+                  regions: Optional[Sequence[str]] = None) -> Dict[Tuple[str, str], Dict]:
     """Point + bootstrap Spearman RSA for every (point, region) unit; returns the
     per-unit results on every rank.
 
-    Units are listed region-major and cut into one contiguous range per rank, so a
-    rank's units come in groups that share a neural RDM; each group is one engine call
-    (run_group: the neural plan's rank walk is shared by the group's layers). plan_fn /
-    group_fn default to RankPlan / run_group (the HIP engine); a per-unit unit_fn(model
-    plan, neural plan, idx, times) may be given instead of group_fn."""
+    Units are listed region-major and cut into one contiguous range per rank (the
+    RdmSchedule's unit_ranges), so a rank's units come in groups that share a neural RDM;
+    each group is one engine call (run_group: the neural plan's rank walk is shared by the
+    group's layers). model_rdm_fn(p) is asked only for the points of this rank's units, and
+    neural_rdms needs only this rank's regions (`regions` lists all of them; default: the
+    keys of neural_rdms). plan_fn / group_fn default to RankPlan / run_group (the HIP
+    engine); a per-unit unit_fn(model plan, neural plan, idx, times) may be given instead."""
     plan_fn = plan_fn or R.RankPlan
     if group_fn is None:
         if unit_fn is not None:
@@ -550,25 +610,23 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
         else:
             group_fn = run_group
     rank, world = _world(pg)
-    regions = list(neural_rdms)
+    regions = list(regions) if regions is not None else list(neural_rdms)
     units = [(p, r) for r in regions for p in points]
     lo, hi = unit_split(units, world)[rank]
     mine = units[lo:hi]
     k = int(0.9 * n)
     idx = None
-    if n_boot > 0:
+    if n_boot > 0 and mine:
         # RandomState(seed) is re-created per (region, subject) (evals.py:356), so every unit
         # draws the same (n_boot, k) index sets: drawn once per call (host MT19937), one upload
-        dev = next(iter(neural_rdms.values())).device
+        dev = neural_rdms[mine[0][1]].device
         idx = torch.from_numpy(draw_bootstrap_indices(seed, n, k, n_boot)).to(dev)
     local: Dict[Tuple[str, str], np.ndarray] = {}
     need = {p for p, _ in mine}
     mplans = {}
     for p in points:
-        rdm = model_rdm_fn(p)  # collective: every rank takes part in every point's RDM
         if p in need:
-            mplans[p] = plan_fn(rdm)
-        del rdm
+            mplans[p] = plan_fn(model_rdm_fn(p))
     by_region: Dict[str, List[str]] = {}
     for p, r in mine:
         by_region.setdefault(r, []).append(p)
