@@ -161,7 +161,10 @@ def test_batched_pca_matches_oracle(dev):
     assert abs(total - rt) <= 1e-10 * rt
     # the top 8 eigenvalues are well separated (8 latent factors): vectors agree up to sign
     assert np.all(np.abs(np.abs(np.sum(comps[:, :8] * rc[:, :8], axis=0)) - 1) < 1e-8)
-    assert np.all(np.abs(comps).max(axis=0) == comps.max(axis=0))  # sign convention
+    # opt-in sign convention (the default keeps the solver's signs, as the reference does)
+    cn, vn, _, _ = C.batched_pca(x, 20, normalize_signs=True)
+    assert np.all(np.abs(cn).max(axis=0) == cn.max(axis=0))
+    assert np.array_equal(np.abs(cn), np.abs(comps)) and np.array_equal(vn, vals)
 
 
 @pytest.mark.gpu

@@ -15,9 +15,13 @@ Device path (csrc/cov.hip):
               row slices, so entries agree to fp64 rounding (~1e-15 relative), and
               ``batch_size`` only names the reference's batching;
   eigh        torch.linalg.eigh (rocSOLVER, fp64) of the p x p covariance.
-Eigenvector signs are LAPACK-implementation-defined in the reference too (numpy's eigh
-makes no sign promise); they are normalised here so each vector's largest-|.| component is
-positive (``sign_convention``), and tests compare vectors up to sign.
+Eigenvector signs are solver-defined (numpy's LAPACK eigh in the reference, rocSOLVER here;
+neither makes a sign promise) and are returned raw by default, as the reference does. The
+coarse PCA labels depend on the sign of each projection, so labels derived from these
+vectors and from reference-produced eigenvectors_*.npz may differ by a per-component flip;
+``normalize_signs=True`` flips each vector so its largest-|.| component is positive
+(``sign_convention``), a reproducible convention for both sides. Tests compare vectors up to
+sign.
 
 Multi-GPU (``batched_pca_sharded``): rows sharded over ranks in order. The float32 column
 sum is a chain over ranks (rank r continues rank r-1's running sum: the same sequence of
@@ -106,28 +110,34 @@ def sign_convention(vecs: torch.Tensor) -> torch.Tensor:
     return vecs * s
 
 
-def eig_top(cov: torch.Tensor, n_components: int):
+def eig_top(cov: torch.Tensor, n_components: int, normalize_signs: bool = False):
     """compute_eigenvectors.py:39-44: eigh, the n_components largest eigenvalues in
-    descending order, their vectors, and the sum of all eigenvalues."""
+    descending order, their vectors (solver signs unless normalize_signs), and the sum of
+    all eigenvalues."""
     vals, vecs = torch.linalg.eigh(cov)
     vals_h = vals.cpu().numpy()
     idx = np.argsort(vals_h)[::-1][:n_components]
     top = torch.as_tensor(idx.copy(), device=cov.device)
-    comps = sign_convention(vecs[:, top])
+    comps = vecs[:, top]
+    if normalize_signs:
+        comps = sign_convention(comps)
     return comps.cpu().numpy(), vals_h[idx], float(vals_h.sum())
 
 
-def batched_pca(X, n_components: int, batch_size: int = 10000, device: Optional[torch.device] = None):
+def batched_pca(X, n_components: int, batch_size: int = 10000, device: Optional[torch.device] = None,
+                normalize_signs: bool = False):
     """Drop-in for compute_eigenvectors.batched_pca (:23-44): (components (p, k) float64,
-    eigenvalues (k,) float64, mean (p,) float32, total variance)."""
+    eigenvalues (k,) float64, mean (p,) float32, total variance). Component signs are the
+    solver's (see the module doc; normalize_signs=True for the largest-|.|-positive
+    convention)."""
     if batch_size <= 0:
         raise ValueError("batch_size must be positive")
     mean, cov = pca_mean_cov(X, device)
-    comps, vals, total = eig_top(cov, n_components)
+    comps, vals, total = eig_top(cov, n_components, normalize_signs)
     return comps, vals, mean.cpu().numpy(), np.float64(total)
 
 
-def batched_pca_sharded(x_local: torch.Tensor, n_components: int, pg=None):
+def batched_pca_sharded(x_local: torch.Tensor, n_components: int, pg=None, normalize_signs: bool = False):
     """batched_pca over row shards (rank r holds rows [sum of earlier shards, +n_r), in
     order). Every rank returns the same (components, eigenvalues, mean, total variance)."""
     x = _device_rows(x_local, None)
@@ -152,7 +162,7 @@ def batched_pca_sharded(x_local: torch.Tensor, n_components: int, pg=None):
     dist.all_reduce(part, group=pg)
     # true division (torch divides by a Python scalar as a multiply by its reciprocal)
     cov = part / torch.full_like(part, float(n - 1))
-    comps, vals, total = eig_top(cov, n_components)
+    comps, vals, total = eig_top(cov, n_components, normalize_signs)
     return comps, vals, mean.cpu().numpy(), np.float64(total)
 
 
