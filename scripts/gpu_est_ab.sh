@@ -1,7 +1,7 @@
 #!/bin/bash
 # EST pass-form A/B on the bench RDMs (probe_engine_bench.py under rocprofv3 kernel stats,
 # each EST form checked bit for bit against the exact form in the same process), then the
-# EST parity tests. Usage: bash scripts/gpu_est_ab.sh <tag> [name:lib.so ...]
+# EST parity tests. Usage: bash scripts/gpu_est_ab.sh <tag> [name:lib.so | name:VAR=value ...]
 set -o pipefail
 tag=${1:-estab}; shift
 out=gpurun_out/$tag
@@ -23,7 +23,12 @@ PY
 }
 run default VISREPS_ENGINE_EST=1 || exit 1
 for spec in "$@"; do
-  run ${spec%%:*} VISREPS_ENGINE_EST=1 ALT_LIB=$PWD/${spec#*:} || exit 1
+  arg=${spec#*:}
+  if [[ "$arg" == *=* ]]; then
+    run ${spec%%:*} VISREPS_ENGINE_EST=1 "$arg" || exit 1
+  else
+    run ${spec%%:*} VISREPS_ENGINE_EST=1 ALT_LIB=$PWD/$arg || exit 1
+  fi
 done
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_engine_est.py \
     > $out/pytest_est.log 2>&1; echo "pytest rc=$?: $(tail -1 $out/pytest_est.log)"

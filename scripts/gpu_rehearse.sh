@@ -1,8 +1,7 @@
 #!/bin/bash
 # Multi-rank rehearsal on a one-GPU box: bench.py at world 2 over gloo (both ranks on
 # cuda:0; RCCL refuses two ranks on one device), then world 1 at the same N; the two
-# check fields (unit score and CI, phase-1 choices) must be identical: the RDMs are
-# bit-identical at every world size (pipeline.py), and the scores exact integer statistics.
+# check fields must agree: phase-1 choices equal, unit score and CI within 1e-8 (see below).
 # Usage (from the repo root, via gpurun): bash scripts/gpu_rehearse.sh [tag] [n]
 set -o pipefail
 tag=${1:-rehearse}; n=${2:-4000}
@@ -20,6 +19,12 @@ def line(f):  # gloo prints its connection lines to stdout too
     return json.loads([l for l in open(f) if l.startswith('{"metric"')][-1])
 a = line(sys.argv[1] + "/w2.json"); b = line(sys.argv[1] + "/w1.json")
 print("world2", a["value"], a["check"]); print("world1", b["value"], b["check"])
-print("check equal:", a["check"] == b["check"])
-sys.exit(0 if a["check"] == b["check"] else 1)
+# RDMs are bit-identical for identical rows at any world size (tests/test_gpu_distributed.py);
+# the extracted features are not: MIOpen / rocBLAS pick kernels by batch shape (a shard's
+# last batch differs), so the rows may differ in their last bits between shardings
+ca, cb = a["check"], b["check"]
+same_phase1 = ca["phase1_best"] == cb["phase1_best"]
+d = max(abs(ca["score"] - cb["score"]), *(abs(x - y) for x, y in zip(ca["ci"], cb["ci"])))
+print("phase-1 choices equal:", same_phase1, " max |d| score/ci:", d, " bit-equal:", ca == cb)
+sys.exit(0 if same_phase1 and d < 1e-8 else 1)
 PY

@@ -349,22 +349,28 @@ def _foundation_feats(dev, model, extract_fn, n=50000, batch=500):
     return feats
 
 
-@pytest.mark.parametrize("which", ["clip", "dino"])
+@pytest.mark.parametrize("which", ["clip", "dino", "vitl"])
 def test_cfg5_foundation_bf16_rdm(dev, which):
-    """configs[4]'s CLIP ViT-L/14 image embedding (encode_image / its norm) and the DINOv3
-    ViT-L/16 CLS (random init, bf16) on 50k synthetic images: bf16 RDM, fp64 rows."""
+    """configs[4]'s CLIP ViT-L/14 image embedding (encode_image / its norm), the DINOv3
+    ViT-L/16 CLS and the supervised ViT-L/16 CLS (vit_representations.py's default model),
+    random init, bf16, on 50k synthetic images: bf16 RDM, fp64 rows."""
     from visreps_amd import extract_representations as X
     from visreps_amd.models.foundation import clip_vit_l14, dinov3_vit_l16
+    from visreps_amd.models.standard_model import vit_large_patch16_224
 
     torch.manual_seed(0)
     if which == "clip":
         model, fn = X.clip_image(clip_vit_l14().to(dev).eval().to(torch.bfloat16))
-    else:
+    elif which == "dino":
         model, fn = X.dino_cls(dinov3_vit_l16().to(dev).eval().to(torch.bfloat16))
+    else:
+        model, fn = X.vit_cls(vit_large_patch16_224().to(dev).eval().to(torch.bfloat16))
     x = _foundation_feats(dev, model, fn)
     del model
     torch.cuda.empty_cache()
     assert x.dtype == torch.bfloat16 and x.shape == (50000, 768 if which == "clip" else 1024)
+    if which == "vitl":  # unit rows (the dump's F.normalize), to bf16 rounding
+        assert torch.allclose(x[:64].float().norm(dim=1), torch.ones(64, device=dev), atol=1e-2)
     assert torch.isfinite(x).all()
     rdm = R.compute_rdm(x)
     rows = _rows(dev, x.size(0), 11)

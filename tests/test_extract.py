@@ -56,6 +56,29 @@ def test_vit_cls_features():
         assert torch.allclose(model(ds.x[:1]), model.heads(model.forward_features(ds.x[:1])[:, 0]))
 
 
+def test_vit_large_patch16_cls_dump():
+    # vit_representations.py's default model (vit_large_patch16_224): 24 pre-norm blocks of
+    # width 1024 (16 heads, MLP 4096), 197 tokens; the dump is the L2-normalised 1024-d CLS
+    from visreps_amd.models.standard_model import vit_large_patch16_224
+
+    torch.manual_seed(0)
+    m = vit_large_patch16_224().eval()
+    assert len(m.encoder.layers) == 24 and m.hidden_dim == 1024
+    assert m.encoder.pos_embedding.shape == (1, 197, 1024)
+    blk = m.encoder.layers[0]
+    assert blk.self_attention.num_heads == 16 and blk.mlp[0].out_features == 4096
+    assert sum(p.numel() for p in m.parameters()) > 300_000_000  # ViT-L scale (~304M with the head)
+    model, fn = X.vit_cls(m)
+    ds = _DS(2, 224)
+    loader = torch.utils.data.DataLoader(ds, batch_size=2, shuffle=False)
+    feats, names = X.extract_features(model, [loader], fn, torch.device("cpu"))
+    assert feats.shape == (2, 1024) and names == ["img_000", "img_001"]
+    np.testing.assert_allclose(np.linalg.norm(feats, axis=1), 1.0, rtol=1e-5)
+    with torch.no_grad():
+        tok = m.forward_features(ds.x)
+    np.testing.assert_allclose(feats, F.normalize(tok[:, 0], dim=-1).numpy(), rtol=1e-5, atol=1e-6)
+
+
 def test_name_mismatch_raises():
     model, fn = X.alexnet_fc2(AlexNetModule(1000))
     loader = torch.utils.data.DataLoader(_DS(2, 64, named=False), batch_size=2)

@@ -1056,7 +1056,13 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       const uint32_t pos = w + (uint32_t)lane;
       const bool valid = pos >= P0 && pos < P1;
       pa = valid ? posA_byB[pos] : 0u;
-      ca = ((!EST || EST >= 3) && valid) ? chunkA_byB[pos] : 0u;  // EST 3/4: window low end
+      // EST 3/4: the window low end of the pair's A position, L + (2 posA R >> 32), computed
+      // here per lane for the window's 64 pairs (three VALU ops per window lane, no stream),
+      // or streamed from the join (VISREPS_ENGINE_LO_JOIN=1, A/B)
+      if constexpr (EST >= 3)
+        ca = !valid ? 0u : chunkA_byB ? chunkA_byB[pos] : el.Lu + __umulhi(pa << 1, el.Ru);
+      else
+        ca = (!EST && valid) ? chunkA_byB[pos] : 0u;
       cd = valid ? codes[pos] : 0u;
       f0 = sload(gflag + (w >> 5));
       f1 = sload(gflag + (w >> 5) + 1);
@@ -1437,7 +1443,12 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
     second = mode;
     return VR_OK;
   };
-  VR_TRY(join(!est ? JOIN_CHUNK : (cfg.est_mode == 3 ? JOIN_LO : JOIN_NONE)));
+  // EST 3: the join precomputes the window low ends (JOIN_LO), the B walk streams them;
+  // VISREPS_ENGINE_LO_JOIN=0 has the walk compute them from the A positions instead (4 B
+  // fewer per pair and pass, but measured no faster: 1367 vs 1359 us per k_rankB launch,
+  // profiles/r3_engine_lo_ab.log)
+  const bool lo_join = cfg.est_mode == 3 && env_int("VISREPS_ENGINE_LO_JOIN", 1) != 0;
+  VR_TRY(join(!est ? JOIN_CHUNK : (lo_join ? JOIN_LO : JOIN_NONE)));
   // the exact chunk-base form of the pass starting at subset set0
   auto exact_pass = [&](auto tag, int64_t set0) -> int {
     using Tg = decltype(tag);
@@ -1465,7 +1476,7 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
   const int64_t pfirst = 0;
   // The first EST pass runs alone: when the estimate cannot hold these A ranks (strongly
   // structured RDMs, giant tie groups) every pass is run in the exact form from there on.
-  const int want = cfg.est_mode == 3 ? JOIN_LO : JOIN_NONE;  // what the EST passes read
+  const int want = lo_join ? JOIN_LO : JOIN_NONE;  // what the EST passes read
   for (int64_t p0 = pfirst, p1 = pfirst; p0 < npass; p0 = p1) {
     p1 = std::min<int64_t>(npass, p0 == pfirst ? p0 + 1 : p0 + EST_MAX_PASSES);
     if (want != JOIN_NONE && second != want) VR_TRY(join(want));
@@ -1484,7 +1495,7 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
                          : pass_a_est<EM, Tg::lds, Tg::full, false>(A, n, E, lw, nl, cfg, e3, viol, st)));
             for (int64_t j = 0; j < nb; ++j) {
               const uint32_t* pj = joins[2 * j];
-              const uint32_t* lj = EM >= 3 ? joins[2 * j + 1] : nullptr;  // EST 3/4: window low ends
+              const uint32_t* lj = EM >= 3 && lo_join ? joins[2 * j + 1] : nullptr;  // EST 3/4: streamed low ends
               VR_TRY((h[(size_t)j + 1].max_group >= 65536u
                           ? walk_b<Tg::lds, Tg::full, uint16_t, true, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)
                           : walk_b<Tg::lds, Tg::full, uint16_t, false, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)));

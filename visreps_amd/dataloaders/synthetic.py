@@ -52,13 +52,17 @@ def make_responses(images: torch.Tensor, rows: range, voxels: Dict[str, int], *,
     for ri, (region, v) in enumerate(voxels.items()):
         gb = _gen(seed * 7919 + 101 * ri, dev)
         b = torch.randn((z.size(1), v), generator=gb, device=dev) / (z.size(1) ** 0.5)
-        y = z @ b
+        y = torch.empty((z.size(0), v), dtype=z.dtype, device=dev)
         r0 = rows.start
         for b0 in range(rows.start - rows.start % BLOCK, rows.stop, BLOCK):
             g = _gen(seed * 15485863 + 31 * ri + 7 * (b0 // BLOCK), dev)
             e = torch.randn((BLOCK, v), generator=g, device=dev)
             lo, hi = max(b0, rows.start), min(b0 + BLOCK, rows.stop)
-            y[lo - r0:hi - r0] += noise * e[lo - b0:hi - b0]
+            # one BLOCK-row GEMM per block (the rows of a partial block padded with zeros):
+            # the GEMM shape, and so its summation order, does not depend on the sharding
+            zb = torch.zeros((BLOCK, z.size(1)), dtype=z.dtype, device=dev)
+            zb[lo - b0:hi - b0] = z[lo - r0:hi - r0]
+            y[lo - r0:hi - r0] = (zb @ b)[lo - b0:hi - b0] + noise * e[lo - b0:hi - b0]
         out[region] = y.contiguous()
     return out
 

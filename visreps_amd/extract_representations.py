@@ -7,15 +7,17 @@ ViT CLS token) -> row L2 normalisation -> concatenation in loader order -> one
   extract_features   utils.py:31-69 (names from dataset.samples[i][2], mismatch -> ValueError)
   save_features      utils.py:72-78 (datasets/obj_cls/{dataset}/features_{model}.npz)
   alexnet_fc2        alexnet_representations.py:25-27,43-45 (classifier[:6], F.normalize)
-  vit_cls            vit_representations.py:25,33-35 (forward_features(x)[:, 0], F.normalize)
+  vit_cls            vit_representations.py:25,33-35 (forward_features(x)[:, 0], F.normalize);
+                     the script's default model, ViT-L/16 (1024-d CLS), is
+                     models.standard_model.vit_large_patch16_224
   clip_image         clip_representations.py:26-38 (encode_image / its norm; CLIP ViT-L/14)
   dino_cls           dino_representations.py:24-38 (forward_features(x)[:, 0], F.normalize)
                      (models/foundation.py; loaders' bicubic preprocessing:
                      dataloaders/obj_cls.clip_transform / dino_transform)
 
 Pretrained weights need a download the reference makes (torchvision / timm / clip); here
-the models are the repo's own random-initialised AlexNet / ViT-B/16 unless a local
-checkpoint is supplied (models/standard_model.py). The rows are written on the device
+the models are the repo's own random-initialised AlexNet / ViT-B/16 / ViT-L/16 unless a
+local checkpoint is supplied (models/standard_model.py). The rows are written on the device
 in one (N, D) buffer, so a caller can hand them straight to the RDM kernels without the
 host round trip of the reference.
 """

@@ -149,3 +149,18 @@ def ViTBase(pretrained_dataset="imagenet1k", num_classes=1000):
         nn.init.xavier_uniform_(model.heads.head.weight)
         nn.init.zeros_(model.heads.head.bias)
     return model
+
+
+def vit_large_patch16_224(pretrained_dataset: str = "none"):
+    """ViT-L/16 at 224 px: the feature-dump default of the reference's
+    scripts/extract_representations/vit_representations.py:19,25
+    (timm.create_model("vit_large_patch16_224", pretrained=True, num_classes=0)). timm's
+    VisionTransformer has this module's semantics -- pre-norm blocks (LayerNorm eps 1e-6,
+    qkv bias, GELU MLP), a learned class token and position embedding added to all 197
+    tokens, and the final LayerNorm inside forward_features -- at width 1024, 24 blocks, 16
+    heads, MLP 4096, so forward_features(x)[:, 0] is the 1024-d CLS row the dump
+    normalises. The pretrained weights need timm's download: random init unless
+    VISREPS_AMD_WEIGHTS_VIT_L_16 names a state_dict in this layout."""
+    model = VisionTransformer(image_size=224, patch_size=16, num_layers=24, num_heads=16, hidden_dim=1024,
+                              mlp_dim=4096, num_classes=1000)
+    return _maybe_load(model, "vit_l_16", pretrained_dataset)

@@ -458,21 +458,25 @@ def engine_bytes(n: int, n_boot: int) -> float:
 # walk streams its codes and writes one 128-byte TB row per pair; each B walk streams its
 # codes and the two join arrays (posA, chunkA) and gathers one TB row per pair (its 256-byte
 # chunk-base rows come from a 2 MB L2-resident table, not HBM). EST form (the default): the
-# A side streams its codes twice (count
-# pre-pass + rank walk), the B walk reads the window low ends instead of the chunk array (the
-# full-set pass 0 runs EST too, lane 0 on its own exact line). k_join reads the B codes and
-# one 8-byte pair-map record and writes the A positions, k_join_lo the low ends, per unit.
+# A side streams its codes twice (count pre-pass + rank walk); the B walk streams its codes
+# and the A positions and the window low ends the join precomputed (VISREPS_ENGINE_LO_JOIN=0:
+# computes them from the A positions instead); k_join reads the B codes, gathers the 4-B A
+# position map and writes the A positions and low ends, per unit.
 def engine_pair_bytes(est: Optional[bool] = None) -> Tuple[int, int, int]:
     """(A walk per pass, B walk per pass and unit, join per unit) bytes per pair."""
+    import os
+
     if est is None:
-        import os
         est = os.environ.get("VISREPS_ENGINE_EST") != "0"
-    # A side: codes 4 (EST: count pre-pass + rank walk, 4 each) + 128 B TB row write.
-    # B walk: codes 4 + A position 4 + second join array 4 (EST: window low end; exact: A chunk)
-    # + 128 B TB row gather (the exact form's 256-B chunk-base rows are L2-resident).
-    # Join: B codes 4 + the A map gather (EST: 4-B position map; exact: 8-B pair-map record)
-    # + posA write 4 + second array write 4.
-    return (4 + 4 + 128, 4 + 4 + 4 + 128, 4 + 4 + 4 + 4) if est else (4 + 128, 4 + 4 + 4 + 128, 4 + 8 + 4 + 4)
+    if not est:
+        # A: codes 4 + TB row write 128; B: codes, posA, chunkA 4 each + TB row 128;
+        # join: B codes 4 + 8-B pair-map record + posA and chunkA writes 4 each
+        return 4 + 128, 4 + 4 + 4 + 128, 4 + 8 + 4 + 4
+    lo = 0 if os.environ.get("VISREPS_ENGINE_LO_JOIN", "1") == "0" else 4
+    # A: codes 4 (count pre-pass) + codes 4 + TB row write 128; B: codes 4 + posA 4
+    # (+ low end) + TB row gather 128; join: B codes 4 + position-map gather 4 + posA write 4
+    # (+ low-end write)
+    return 4 + 4 + 128, 4 + 4 + lo + 128, 4 + 4 + 4 + lo
 
 
 def engine_call_bytes(n: int, subsets: int, units: int) -> float:
