@@ -53,8 +53,8 @@ from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_resp
 from visreps_amd.models.custom_model import CustomCNN
 from visreps_amd.models.utils import FeatureExtractor
 from visreps_amd._lib import KTIMER_KERNELS, check, ktimer_enable, ktimer_read, lib, stream_of
-from visreps_amd.pipeline import (ShardedRDMs, StepTimes, all_units_rsa, engine_bytes, engine_call_bytes,
-                                  engine_pair_bytes, make_schedule, phase1_select)
+from visreps_amd.pipeline import (KERNELS, ShardedRDMs, StepTimes, all_units_rsa, engine_bytes, engine_call_bytes,
+                                  engine_pair_bytes, make_schedule, phase1_rows, phase1_select)
 
 METRIC = "end-to-end RSA eval sec (extract→RDM→1000-bootstrap Spearman), N=10k stimuli"
 LAYERS = ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
@@ -80,6 +80,46 @@ def extract(extractor: FeatureExtractor, images: torch.Tensor, batch: int):
         for k, v in feats.items():
             bufs[k][b0:b0 + v.size(0)] = v.reshape(v.size(0), -1)
     return bufs
+
+
+@torch.no_grad()
+def extract_split(extractor: FeatureExtractor, images: torch.Tensor, batch: int, keep: np.ndarray,
+                  correction: float = 1e-12):
+    """bench.extract with the Gram prepass fused in: every batch's hooked outputs are split
+    straight into per-point SplitRows (row statistics + bf16 hi/lo records,
+    vr_rdm_split_rows_f32) -- no fp32 copy of the features is made -- and only the local
+    rows `keep` (phase 1's selection stimuli, pipeline.phase1_rows order) are kept in fp32.
+    Returns ({point: SplitRows}, {point: (len(keep), D) fp32 rows})."""
+    n, dev = images.size(0), images.device
+    K = KERNELS
+    out = sel = None
+    keep = np.asarray(keep, dtype=np.int64)
+    for b0 in range(0, n, batch):
+        feats = extractor(images[b0:b0 + batch])
+        if out is None:
+            out = {k: K.empty_split(n, v[0].numel(), dev) for k, v in feats.items()}
+            sel = {k: torch.empty((len(keep), v[0].numel()), dtype=torch.float32, device=dev) for k, v in feats.items()}
+        b1 = min(n, b0 + batch)
+        at = np.flatnonzero((keep >= b0) & (keep < b1))  # host-side: no device sync per batch
+        at_t = torch.as_tensor(at, dtype=torch.long, device=dev)
+        src_t = torch.as_tensor(keep[at] - b0, dtype=torch.long, device=dev)
+        for k, v in feats.items():
+            x = v.reshape(v.size(0), -1)
+            sr = out[k]
+            K.split_rows_into(x, correction, sr.planes[b0:b1], sr.mean[b0:b1], sr.std[b0:b1])
+            if len(at):
+                sel[k][at_t] = x[src_t].float()
+    return out, sel
+
+
+def split_mode(n: int, dims: dict) -> bool:
+    """The bench Grams all take the bf16 split kernel (n^2 d >= 1e10 for every point, or
+    VISREPS_GRAM=split); then extraction writes split rows directly. VISREPS_GRAM=fp32
+    keeps fp32 feature buffers for the exact-fp32 kernel."""
+    mode = os.environ.get("VISREPS_GRAM")
+    if mode == "fp32":
+        return False
+    return mode == "split" or all(float(n) * n * d >= 1e10 for d in dims.values())
 
 
 PMC_PROFILE = os.path.join(ROOT, "profiles", "r3_pmc_engine.json")
@@ -303,10 +343,16 @@ def main():
     regions = list(NSD_ROIS_4)
     sched = make_schedule(N, dims, points, NSD_ROIS_4, world)
 
+    split = split_mode(N, dims)
+    _, _, keep = phase1_rows(N, 1000, 42, rank, world)
+
     def step(times: StepTimes):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
         ev[0].record()
-        feats = extract(extractor, images, args.batch)
+        if split:  # the Gram prepass fused into extraction (bench.extract_split)
+            feats, sel_rows = extract_split(extractor, images, args.batch, keep)
+        else:
+            feats, sel_rows = extract(extractor, images, args.batch), None
         ev[1].record()
         rows = {("m", p): feats[p] for p in points}
         rows.update({("n", r): responses[r] for r in regions})
@@ -315,11 +361,11 @@ def main():
         ex = ShardedRDMs(sched, rows, pg, times, exchange_pg=feat_pg)
         ex.start()
         sel = phase1_select(feats, projectors, responses, points, N, n_select=1000, seed=42,
-                            pg=pg, times=times)
+                            pg=pg, times=times, selected_rows=sel_rows)
         ev[2].record()
         rd = ex.finish()  # this rank's RDMs: its pieces' Grams + the exchange of the rest
         ev[3].record()
-        del feats, rows, ex
+        del feats, rows, ex, sel_rows
         neural = {r: rd[("n", r)] for r in regions if ("n", r) in rd}
         res = all_units_rsa(lambda p: rd.pop(("m", p)), points, neural, N, n_boot=args.boot, seed=42, pg=pg,
                             times=times, regions=regions)
@@ -382,8 +428,9 @@ def main():
                            + ": B-side rank walk of one unit over one pass of 64 bootstrap subsets "
                            "(the full-set pass 0 and phase-1 launches are k_rankB_full in kernels_per_step)"),
                 "algorithmic_bytes_per_launch": round(rb["bytes_per_launch"]),
-                "algorithmic_bytes_model": (f"{b_b} B per pair: codes 4 + A position 4 + window low end 4 "
-                                            "(streams) + 128 B TB row gather" if est else
+                "algorithmic_bytes_model": (f"{b_b} B per pair: codes 4 + A position 4 (streams"
+                                            + (" + window low end 4" if b_b > 136 else "; the window low end is "
+                                               "computed from the A position") + ") + 128 B TB row gather" if est else
                                             f"{b_b} B per pair: codes, A position, A chunk 4 each + 128 B TB "
                                             "row gather (the 256-B chunk-base rows are L2-resident)"),
                 "pairs_per_launch": round(rb["units_per_launch"]),

@@ -51,6 +51,46 @@ class CpuKernels(P.RdmKernels):
             out[c0:c0 + w, r0:r0 + h] = blk.T
 
     @staticmethod
+    def plane_elems(d):  # emulated record: per 32-feature stage 32 bf16 hi then 32 bf16 lo
+        return (d + 31) // 32 * 64
+
+    @staticmethod
+    def split_rows_into(x, correction, planes, mean, std):  # noqa: ARG004
+        rows, d = x.shape
+        ns = (d + 31) // 32
+        xd = x.double()
+        m = xd.mean(1)
+        c = (xd - m[:, None]).float()
+        pad = torch.zeros((rows, ns * 32), dtype=torch.float32)
+        pad[:, :d] = c
+        hi = pad.to(torch.bfloat16)
+        lo = (pad - hi.float()).to(torch.bfloat16)
+        pl = planes[:rows].view(rows, ns, 64)
+        pl[:, :, :32] = hi.view(torch.int16).view(rows, ns, 32)
+        pl[:, :, 32:] = lo.view(torch.int16).view(rows, ns, 32)
+        mean.copy_(m.float())
+        std.copy_(torch.sqrt((c.double() ** 2).mean(1)).float())
+
+    @staticmethod
+    def tiles_from_planes(sr, n, out, t0, t1, correction, times=None):  # noqa: ARG004
+        d = sr.d
+        ns = (d + 31) // 32
+        pl = sr.planes[:n].view(n, ns, 64)
+        hi = pl[:, :, :32].contiguous().view(torch.bfloat16).float()
+        lo = pl[:, :, 32:].contiguous().view(torch.bfloat16).float()
+        xc = (hi + lo).reshape(n, ns * 32)[:, :d].double()
+        s = sr.std.double()
+        for t in range(t0, t1):
+            r0, c0, h, w = P.tile_rect(n, t)
+            g = xc[r0:r0 + h] @ xc[c0:c0 + w].T / d
+            corr = (g / (s[r0:r0 + h, None] * s[None, c0:c0 + w] + correction)).clamp(-1, 1)
+            blk = (1 - corr).float()
+            if r0 == c0:
+                blk.fill_diagonal_(0)
+            out[r0:r0 + h, c0:c0 + w] = blk
+            out[c0:c0 + w, r0:r0 + h] = blk.T
+
+    @staticmethod
     def pack(out, n, t0, t1, packed):
         for t in range(t0, t1):
             r0, c0, h, w = P.tile_rect(n, t)
@@ -66,12 +106,19 @@ class CpuKernels(P.RdmKernels):
             out[c0:c0 + w, r0:r0 + h] = blk.T
 
 
-def emulated_rdm(X: np.ndarray) -> np.ndarray:
-    """The emulation's single-process RDM of all rows (one rank, every tile)."""
+def emulated_rdm(X: np.ndarray, split: bool = False) -> np.ndarray:
+    """The emulation's single-process RDM of all rows (one rank, every tile), from the rows
+    or from their split records."""
+    K = CpuKernels()
     x = torch.from_numpy(X)
     n = x.size(0)
     out = torch.empty((n, n), dtype=torch.float32)
-    CpuKernels.tiles_from_rows(x, out, 0, int(P.lib().vr_rdm_tile_count(n)), 1e-12)
+    if split:
+        sr = K.empty_split(n, x.size(1), "cpu")
+        K.split_rows_into(x, 1e-12, sr.planes, sr.mean, sr.std)
+        K.tiles_from_planes(sr, n, out, 0, int(P.lib().vr_rdm_tile_count(n)), 1e-12)
+    else:
+        K.tiles_from_rows(x, out, 0, int(P.lib().vr_rdm_tile_count(n)), 1e-12)
     return out.numpy()
 class _OraclePlan:
     """RankPlan stand-in: the RDM itself (n = its size)."""
@@ -137,7 +184,13 @@ def _row_boundaries(n, d):  # noqa: ARG001
     return [P._tri_start(r, T) for r in range(T)] + [int(P.lib().vr_rdm_tile_count(n))]
 
 
-def _worker(rank, world, port, n, d, n_boot, out_dir, split):
+def _local_split(K, x):
+    sr = K.empty_split(x.size(0), x.size(1), "cpu")
+    K.split_rows_into(x, 1e-12, sr.planes, sr.mean, sr.std)
+    return sr
+
+
+def _worker(rank, world, port, n, d, n_boot, out_dir, split, presplit):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pg = dist.group.WORLD
@@ -155,6 +208,8 @@ def _worker(rank, world, port, n, d, n_boot, out_dir, split):
         assert any(len(p) > 1 for p in sched.pieces.values())
     feat_pg = dist.new_group(list(range(world)))
     srcs = {("m", "x"): loc["x"], ("m", "z"): loc["z"], ("n", "r0"): loc["y"], ("n", "r1"): loc["x"]}
+    if presplit:  # bench.extract_split: the model points arrive as split rows
+        srcs[("m", "x")], srcs[("m", "z")] = _local_split(K, loc["x"]), _local_split(K, loc["z"])
     ex = P.ShardedRDMs(sched, srcs, pg, kernels=K, exchange_pg=feat_pg, window=1)
     ex.start()
     rd = ex.finish()
@@ -170,13 +225,16 @@ def _worker(rank, world, port, n, d, n_boot, out_dir, split):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,world,split", [(37, 2, False), (300, 2, False), (300, 3, False),
-                                          (300, 2, True), (400, 3, True)])
-def test_gloo_distributed_rdm_and_units_match_single_process(tmp_path, n, world, split):
+@pytest.mark.parametrize("n,world,split,presplit", [(37, 2, False, False), (300, 2, False, False),
+                                                   (300, 3, False, False), (300, 2, True, False),
+                                                   (400, 3, True, False), (300, 3, True, True)])
+def test_gloo_distributed_rdm_and_units_match_single_process(tmp_path, n, world, split, presplit):
     d, n_boot = 40, 6
-    mp.spawn(_worker, args=(world, _free_port(), n, d, n_boot, str(tmp_path), split), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, d, n_boot, str(tmp_path), split, presplit), nprocs=world,
+             join=True)
     X, Y, Z = _data(n, d)
-    ref = {"mx": emulated_rdm(X), "mz": emulated_rdm(Z), "nr0": emulated_rdm(Y), "nr1": emulated_rdm(X)}
+    ref = {"mx": emulated_rdm(X, presplit), "mz": emulated_rdm(Z, presplit), "nr0": emulated_rdm(Y),
+           "nr1": emulated_rdm(X)}
     assert np.max(np.abs(ref["mx"] - O.compute_rdm(X))) < 1e-5  # the emulation is an RDM
     held = 0
     for r in range(world):
@@ -185,12 +243,14 @@ def test_gloo_distributed_rdm_and_units_match_single_process(tmp_path, n, world,
             if f.exists():
                 held += 1
                 assert np.array_equal(np.load(f), m), (key, r)
-        assert np.array_equal(np.load(tmp_path / f"rdm_all_{r}.npy"), ref["mz"])
+        assert np.array_equal(np.load(tmp_path / f"rdm_all_{r}.npy"), emulated_rdm(Z))
     assert held >= 4  # every RDM is held by at least one consumer
     lines = [(tmp_path / f"res_{r}.txt").read_text() for r in range(world)]
     assert all(l == lines[0] for l in lines)
     idx = bootstrap_indices(42, n, int(0.9 * n), n_boot)
     models = {"x": ref["mx"], "z": ref["mz"]}
+    if presplit:
+        assert not np.array_equal(ref["mx"], ref["nr1"])  # the split path is the one compared
     neural = {"r0": ref["nr0"], "r1": ref["nr1"]}
     got_units = set()
     for line in lines[0].splitlines():

@@ -112,3 +112,31 @@ def test_presplit_planes_equal_row_tiles(dev, n, d, world, monkeypatch):
         P.rdm_tiles_into(x, ref, t0, t1)
         assert torch.equal(torch.nan_to_num(got, nan=-7.0), torch.nan_to_num(ref, nan=-7.0))
     assert np.isfinite(std.cpu().numpy()).all()
+
+
+def test_bench_extract_split_equals_fp32_path(dev, monkeypatch):
+    """bench.extract_split (the Gram prepass fused into extraction): the RDMs from its split
+    rows equal the RDMs of bench.extract's fp32 feature buffers bit for bit, and the kept
+    phase-1 rows equal the fp32 rows."""
+    monkeypatch.setenv("VISREPS_GRAM", "split")
+    import bench
+    from visreps_amd.dataloaders.synthetic import make_images
+    from visreps_amd.models.custom_model import CustomCNN
+    from visreps_amd.models.utils import FeatureExtractor
+
+    torch.manual_seed(0)
+    model = CustomCNN(num_classes=1000).to(dev).eval()
+    ex = FeatureExtractor(model, ["conv5", "fc1"], extract_pre_and_post=True)
+    n = 300
+    images = make_images(range(n), device=dev)
+    keep = np.array([3, 77, 150, 299, 0])
+    full = bench.extract(ex, images, 64)
+    split, sel = bench.extract_split(ex, images, 64, keep)
+    total = int(lib().vr_rdm_tile_count(n))
+    for p, x in full.items():
+        assert torch.equal(sel[p], x[torch.as_tensor(keep, device=dev)])
+        one = torch.empty((n, n), device=dev)
+        P.rdm_tiles_into(x, one, 0, total)
+        got = torch.empty((n, n), device=dev)
+        P.KERNELS.tiles_from_planes(split[p], n, got, 0, total, 1e-12)
+        assert torch.equal(got, one), p

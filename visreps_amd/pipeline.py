@@ -151,6 +151,29 @@ def _gram_exact_fp32() -> bool:
     return os.environ.get("VISREPS_GRAM") == "fp32"
 
 
+@dataclass
+class SplitRows:
+    """Stimulus rows of one point already split for the Gram (vr_rdm_split_rows_f32): per
+    row the float32 mean and std of the reference's compute_rdm (rsa.py:80-87) and the bf16
+    hi/lo records of the centred row (planes: (rows_padded, plane_elems) int16, rows past
+    `rows` zero). bench.extract writes these straight from the forward hooks, so the Grams
+    need no prepass over fp32 copies of the features; the tiles computed from them equal the
+    tiles computed from the raw rows bit for bit (tests/test_gpu_distributed.py)."""
+
+    planes: torch.Tensor
+    mean: torch.Tensor
+    std: torch.Tensor
+    rows: int
+    d: int
+
+    def size(self, dim: int) -> int:
+        return self.rows if dim == 0 else self.d
+
+    @property
+    def device(self):
+        return self.planes.device
+
+
 class RdmKernels:
     """The HIP entry points of the distributed RDM (csrc/rdm.hip). The orchestration below
     calls nothing else on the device, so the gloo tests substitute a CPU emulation of
@@ -160,6 +183,50 @@ class RdmKernels:
     def tiles_from_rows(x, out, t0, t1, correction, times=None) -> None:
         """Gram tiles [t0, t1) of x's RDM (+ mirrors) into out (vr_rdm_pearson_tiles_f32)."""
         rdm_tiles_into(x, out, t0, t1, correction, times)
+
+    @staticmethod
+    def plane_rows(n: int) -> int:
+        return int(lib().vr_rdm_plane_rows(n))
+
+    @staticmethod
+    def plane_elems(d: int) -> int:  # int16 elements per row of plane records
+        return int(lib().vr_rdm_plane_row_bytes(d)) // 2
+
+    @staticmethod
+    def split_rows_into(x: torch.Tensor, correction: float, planes: torch.Tensor, mean: torch.Tensor,
+                        std: torch.Tensor) -> None:
+        """Row statistics + hi/lo records of x's rows into the given buffers (contiguous,
+        row-aligned views of a SplitRows' tensors)."""
+        rows, d = x.shape
+        if rows:
+            check(lib().vr_rdm_split_rows_f32(x.data_ptr(), rows, d, x.stride(0), float(correction),
+                                              mean.data_ptr(), std.data_ptr(), planes.data_ptr(),
+                                              stream_of(x.device)), "vr_rdm_split_rows_f32")
+
+    @staticmethod
+    def tiles_from_planes(sr: SplitRows, n: int, out: torch.Tensor, t0: int, t1: int, correction: float,
+                          times: Optional[StepTimes] = None) -> None:
+        """Gram tiles [t0, t1) from pre-split rows (vr_rdm_pearson_tiles_planes)."""
+        if t1 <= t0:
+            return
+        L = lib()
+        d = sr.d
+        ws = workspace.get(out.device, L.vr_rdm_planes_tiles_workspace(n, d, t0, t1), "rdm")
+        ev = None
+        if times is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        check(L.vr_rdm_pearson_tiles_planes(sr.planes.data_ptr(), sr.mean.data_ptr(), sr.std.data_ptr(), n, d,
+                                            out.data_ptr(), n, float(correction), t0, t1, ws.data_ptr(),
+                                            ws.numel(), stream_of(out.device)), "vr_rdm_pearson_tiles_planes")
+        if times is not None:
+            ev[1].record()
+            times.record("gram", ev[0], ev[1], _gram_flops(n, d) * _tile_fraction(n, t0, t1))
+
+    def empty_split(self, rows: int, d: int, device) -> SplitRows:
+        return SplitRows(torch.zeros((self.plane_rows(rows), self.plane_elems(d)), dtype=torch.int16, device=device),
+                         torch.empty(rows, dtype=torch.float32, device=device),
+                         torch.empty(rows, dtype=torch.float32, device=device), rows, d)
 
     @staticmethod
     def pack(out: torch.Tensor, n: int, t0: int, t1: int, packed: torch.Tensor) -> None:
@@ -335,21 +402,47 @@ class ShardedRDMs:
         self.exchange_pg = exchange_pg if exchange_pg is not None else pg
         self.window, self.correction = max(1, int(window)), correction
         self.rank, self.world = _world(pg)
-        # exchange order: longest Gram first, so the big owners start first
-        self.order = sorted(sched.pieces, key=lambda k: (-sum(pc.t1 - pc.t0 for pc in sched.pieces[k])
-                                                          * int(rows[k].size(1)), k))
+        # exchange order: widest RDM first, so the big owners start first
+        self.order = sorted(sched.pieces, key=lambda k: (-int(rows[k].size(1)), k))
         self.pending: Dict[Tuple[str, str], Callable[[], Optional[torch.Tensor]]] = {}
         self._next = 0
 
     def _issue(self) -> None:
         k = self.order[self._next]
         self._next += 1
-        x = self.rows[k].float().contiguous()
         n, world = self.sched.n, self.world
         owners = self.sched.owners(k)
         sizes = [len(shard_rows(n, r, world)) for r in range(world)]
-        send = [x if r in owners else None for r in range(world)]
         recv = sizes if self.rank in owners else [0] * world
+        src = self.rows[k]
+        if isinstance(src, SplitRows):
+            # plane records travel as 8-byte words (no 16-bit integer type in RCCL or gloo),
+            # the row statistics as (rows, 2) floats; the owner's planes buffer is padded to
+            # the super-tile edge with zero rows, as the kernels read it
+            K = self.kernels
+            pl = src.planes[:src.rows].view(torch.int64)
+            stats = torch.stack([src.mean, src.std], dim=1)
+            w1, pfull, k1 = _all_to_all_rows([pl if r in owners else None for r in range(world)], recv,
+                                             pl.shape[1:], pl.dtype, pl.device, self.exchange_pg, async_op=True)
+            w2, sfull, k2 = _all_to_all_rows([stats if r in owners else None for r in range(world)], recv,
+                                             stats.shape[1:], stats.dtype, stats.device, self.exchange_pg,
+                                             async_op=True)
+
+            def done_split(_keep=(k1, k2)):
+                w1.wait()
+                w2.wait()
+                if self.rank not in owners:
+                    return None
+                out = K.empty_split(n, src.d, pfull.device)
+                out.planes[:n].view(torch.int64).copy_(pfull)
+                out.mean.copy_(sfull[:, 0])
+                out.std.copy_(sfull[:, 1])
+                return out
+
+            self.pending[k] = done_split
+            return
+        x = src.float().contiguous()
+        send = [x if r in owners else None for r in range(world)]
         work, full, keep = _all_to_all_rows(send, recv, x.shape[1:], x.dtype, x.device, self.exchange_pg,
                                             async_op=True)
 
@@ -358,6 +451,12 @@ class ShardedRDMs:
             return full if self.rank in owners else None
 
         self.pending[k] = done
+
+    def _tiles(self, src, out: torch.Tensor, t0: int, t1: int) -> None:
+        if isinstance(src, SplitRows):
+            self.kernels.tiles_from_planes(src, self.sched.n, out, t0, t1, self.correction, self.times)
+        else:
+            self.kernels.tiles_from_rows(src.float().contiguous(), out, t0, t1, self.correction, self.times)
 
     def start(self) -> None:
         if self.world > 1:
@@ -370,10 +469,8 @@ class ShardedRDMs:
         if self.world == 1:
             out = {}
             for k in self.order:
-                x = self.rows[k].float().contiguous()
-                o = torch.empty((n, n), dtype=torch.float32, device=x.device)
-                K.tiles_from_rows(x, o, 0, int(lib().vr_rdm_tile_count(n)), self.correction, self.times)
-                out[k] = o
+                out[k] = o = torch.empty((n, n), dtype=torch.float32, device=self.rows[k].device)
+                self._tiles(self.rows[k], o, 0, int(lib().vr_rdm_tile_count(n)))
             return out
         self.start()
         dev = next(iter(self.rows.values())).device
@@ -390,7 +487,7 @@ class ShardedRDMs:
                 continue
             o = bufs.setdefault(k, torch.empty((n, n), dtype=torch.float32, device=dev))
             for pc in mine_pieces:
-                K.tiles_from_rows(full, o, pc.t0, pc.t1, self.correction, self.times)
+                self._tiles(full, o, pc.t0, pc.t1)
             del full
         # 2. packed pieces to the consumers that lack them; unpack only what this rank reads
         out = {}
@@ -527,9 +624,20 @@ def unit_split(units: Sequence, world: int) -> List[Tuple[int, int]]:
     return [(b[r], b[r + 1]) for r in range(world)]
 
 
+def phase1_rows(n: int, n_select: Optional[int], seed: int, rank: int, world: int):
+    """The phase-1 selection of evals.py:259-263 seen from one rank: (k, positions in the
+    selection list held by this rank, their local row indices in the rank's shard)."""
+    rows = shard_rows(n, rank, world)
+    k = min(int(n_select), n) if n_select is not None else n
+    sel = (LegacyRandomState(seed).choice(n, k, replace=False) if k < n else np.arange(n))
+    mine = np.flatnonzero((sel >= rows.start) & (sel < rows.stop))
+    return k, mine, sel[mine] - rows.start
+
+
 def phase1_select(feats: Dict[str, torch.Tensor], projectors: Dict, responses: Dict[str, torch.Tensor],
                   points: Sequence[str], n: int, *, n_select: int = 1000, seed: int = 42,
-                  pg=None, times: Optional[StepTimes] = None) -> Dict[str, Tuple[str, List[Dict]]]:
+                  pg=None, times: Optional[StepTimes] = None,
+                  selected_rows: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, Tuple[str, List[Dict]]]:
     """Phase-1 layer selection of the reference eval (evals.py:249-287) on stimulus-sharded
     features. RandomState(seed).choice(n, n_select) picks the selection stimuli (re-created
     per (region, subject); the regions share one subject's stimuli, so one draw serves them
@@ -539,16 +647,14 @@ def phase1_select(feats: Dict[str, torch.Tensor], projectors: Dict, responses: D
     and selecting after, as the reference does: phase 1 reads no other projected row
     (evals.py:254-268) and phase 2 re-extracts. Then selection RDMs of the projected points
     and of each region's responses; Spearman of every point against every region; best =
-    first strict maximum.
+    first strict maximum. selected_rows[p] (optional) holds this rank's selected rows of
+    point p in phase1_rows order, kept during extraction instead of all of feats[p].
     Returns {region: (best point, [{"layer", "score"} per point])} on every rank."""
     rank, world = _world(pg)
-    rows = shard_rows(n, rank, world)
-    k = min(int(n_select), n) if n_select is not None else n
-    sel = (LegacyRandomState(seed).choice(n, k, replace=False) if k < n else np.arange(n))
-    mine = np.flatnonzero((sel >= rows.start) & (sel < rows.stop))
+    k, mine, src = phase1_rows(n, n_select, seed, rank, world)
     dev = next(iter(responses.values())).device
     pos_t = torch.as_tensor(mine, dtype=torch.long, device=dev)
-    src_t = torch.as_tensor(sel[mine] - rows.start, dtype=torch.long, device=dev)
+    src_t = torch.as_tensor(src, dtype=torch.long, device=dev)
 
     def selected(x_mine: torch.Tensor) -> torch.Tensor:  # this rank's selected rows -> (k, d), every rank
         out = torch.zeros((k, x_mine.size(1)), dtype=torch.float32, device=dev)
@@ -564,7 +670,8 @@ def phase1_select(feats: Dict[str, torch.Tensor], projectors: Dict, responses: D
 
     mplans = []
     for p in points:
-        proj = projectors[p](feats[p][src_t])  # SRP of this rank's selected stimuli
+        rows_p = selected_rows[p] if selected_rows is not None else feats[p][src_t]
+        proj = projectors[p](rows_p)  # SRP of this rank's selected stimuli
         mplans.append(R.RankPlan(timed_rdm(selected(proj))))
         del proj
     out = {}
