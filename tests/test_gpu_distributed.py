@@ -118,8 +118,18 @@ def test_bench_extract_split_equals_fp32_path(dev, monkeypatch):
     """bench.extract_split (the Gram prepass fused into extraction): the RDMs from its split
     rows equal the RDMs of bench.extract's fp32 feature buffers bit for bit, and the kept
     phase-1 rows equal the fp32 rows."""
+    import os
+
     monkeypatch.setenv("VISREPS_GRAM", "split")
+    # bench.py turns on cudnn.benchmark and MIOpen's find mode at import; the two extractions
+    # below must run the same convolution algorithms (as tests/test_benchsize.py's fixture)
+    prev = torch.backends.cudnn.benchmark, os.environ.get("MIOPEN_FIND_MODE")
     import bench
+    torch.backends.cudnn.benchmark = prev[0]
+    if prev[1] is None:
+        os.environ.pop("MIOPEN_FIND_MODE", None)
+    else:
+        os.environ["MIOPEN_FIND_MODE"] = prev[1]
     from visreps_amd.dataloaders.synthetic import make_images
     from visreps_amd.models.custom_model import CustomCNN
     from visreps_amd.models.utils import FeatureExtractor
