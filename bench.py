@@ -103,11 +103,12 @@ def extract_split(extractor: FeatureExtractor, images: torch.Tensor, batch: int,
         at = np.flatnonzero((keep >= b0) & (keep < b1))  # host-side: no device sync per batch
         at_t = torch.as_tensor(at, dtype=torch.long, device=dev)
         src_t = torch.as_tensor(keep[at] - b0, dtype=torch.long, device=dev)
-        for k, v in feats.items():
-            x = v.reshape(v.size(0), -1)
-            sr = out[k]
-            K.split_rows_into(x, correction, sr.planes[b0:b1], sr.mean[b0:b1], sr.std[b0:b1])
-            if len(at):
+        xs = {k: v.reshape(v.size(0), -1) for k, v in feats.items()}
+        # every point of the batch in one launch (rows x points blocks: a batch's rows alone
+        # would leave most CUs idle)
+        K.split_rows_multi(list(xs.values()), correction, [out[k] for k in xs], b0)
+        if len(at):
+            for k, x in xs.items():
                 sel[k][at_t] = x[src_t].float()
     return out, sel
 

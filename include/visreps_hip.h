@@ -281,6 +281,12 @@ int64_t vr_rdm_plane_rows(int64_t n);
 size_t vr_rdm_plane_row_bytes(int64_t d);
 int vr_rdm_split_rows_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, float correction,
                           float* mean, float* stdv, uint16_t* planes, void* stream);
+/* The same split for the same `rows` rows of npts points (<= 32) in one launch (rows x npts
+ * blocks): X[p] (rows, d[p]) with row stride ldx[p], outputs mean[p], stdv[p], planes[p].
+ * Host arrays of device pointers. Used by bench.extract_split on each extraction batch. */
+int vr_rdm_split_rows_multi_f32(int npts, const float* const* X, const int64_t* d, const int64_t* ldx,
+                                int64_t rows, float correction, float* const* mean, float* const* stdv,
+                                uint16_t* const* planes, void* stream);
 size_t vr_rdm_planes_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end);
 int vr_rdm_pearson_tiles_planes(const uint16_t* planes, const float* mean, const float* stdv,
                                 int64_t n, int64_t d, float* rdm, int64_t ldr, float correction,

@@ -209,23 +209,28 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
 // The second array: the A chunk (exact form, JOIN_CHUNK) or the EST 3 window low end of the
 // A position, L + (2 posA R >> 32) (JOIN_LO): the B walk then reads it instead of computing it.
 enum { JOIN_NONE = 0, JOIN_CHUNK = 1, JOIN_LO = 2 };
-// JOIN_CHUNK gathers the 8-B (position, chunk) records; the EST joins only the 4-B
-// positions (posMapA), a table the MALL can keep across the joins of one A plan.
+// Every join gathers the 4-B A positions (posMapA), a table the MALL can keep across the
+// joins of one A plan. JOIN_CHUNK also needs the A chunk of the position: chunks are
+// group-aligned, chunk c starting at the first group start >= c L, so the chunk of a
+// position is the last c <= pos / L whose start is <= pos -- one step down per chunk a
+// tie group spans (the exact form is the rare path: VISREPS_ENGINE_EST=0, flagged passes).
 __global__ void k_join(const uint32_t* __restrict__ codesB, int64_t M, int64_t n,
-                       const uint2* __restrict__ pairMapA, const uint32_t* __restrict__ posMapA,
+                       const uint32_t* __restrict__ gstartA, const uint32_t* __restrict__ chunk_gA,
+                       uint32_t L, uint32_t nchA, const uint32_t* __restrict__ posMapA,
                        uint32_t* __restrict__ posA_byB, uint32_t* __restrict__ second, int mode,
                        uint32_t Lu, uint32_t Ru) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M) return;
   const uint32_t cb = __builtin_nontemporal_load(codesB + i);
   const uint64_t t = tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n);
+  const uint32_t pa = posMapA[t];
   if (mode == JOIN_CHUNK) {
-    const uint2 pc = pairMapA[t];
-    posA_byB[i] = pc.x;
-    second[i] = pc.y;
+    uint32_t c = min(pa / L, nchA - 1u);
+    while (c > 0 && gstartA[chunk_gA[c]] > pa) --c;
+    posA_byB[i] = pa;
+    second[i] = c;
     return;
   }
-  const uint32_t pa = posMapA[t];
   __builtin_nontemporal_store(pa, posA_byB + i);
   if (mode == JOIN_LO) __builtin_nontemporal_store(Lu + __umulhi(pa << 1, Ru), second + i);
 }
@@ -1436,7 +1441,8 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
         VR_CHECK_LAUNCH();
         continue;
       }
-      k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(Bs[j].codes, M, n, A.pair_map, A.pos_map,
+      k_join<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(Bs[j].codes, M, n, A.gstart, A.chunk_g,
+                                                         plan_chunk_len(M), plan_nchunks(M), A.pos_map,
                                                          joins[2 * j], joins[2 * j + 1], mode, e3.x, e3.y);
       VR_CHECK_LAUNCH();
     }

@@ -148,13 +148,13 @@ __global__ void k_group_index(const uint32_t* __restrict__ gflag, const uint32_t
 // B position i -> (key = A group of its pair, value = i); sorting stably by key from B
 // order gives the (x, y)-lexicographic order of scipy's kendalltau
 __global__ void k_kendall_keys(const uint32_t* __restrict__ codesB, int64_t M, int64_t n,
-                               const uint2* __restrict__ pairMapA,
+                               const uint32_t* __restrict__ posMapA,
                                const uint32_t* __restrict__ gidxA, uint32_t* __restrict__ keys,
                                uint32_t* __restrict__ vals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M) return;
   const uint32_t cb = codesB[i];
-  keys[i] = gidxA[pairMapA[tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n)].x];
+  keys[i] = gidxA[posMapA[tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n)]];
   vals[i] = (uint32_t)i;
 }
 
@@ -469,7 +469,7 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
   VR_TRY(group_index(A, M, W, W.gidxA, st));
   VR_TRY(group_index(B, M, W, W.gidxB, st));
   // (x, y)-lexicographic order: stable sort of B order by A group
-  k_kendall_keys<<<gbM, 256, 0, st>>>(B.codes, M, n, A.pair_map, W.gidxA, W.keys, W.vals);
+  k_kendall_keys<<<gbM, 256, 0, st>>>(B.codes, M, n, A.pos_map, W.gidxA, W.keys, W.vals);
   VR_CHECK_LAUNCH();
   VR_TRY(radix_sort_kv(W.keys, W.vals, W.keys_alt, W.vals_alt, M, W.radix, st));
   k_kendall_elems<<<gbM, 256, 0, st>>>(W.vals, B.codes, W.gidxB, M, W.ecode[0], W.ey[0]);

@@ -33,11 +33,10 @@ struct PlanView {
   PlanHeader* hdr;
   uint32_t* codes;          // [M]    (a << 16) | b, sorted by value
   uint32_t* gstart;         // [M+1]  first G+1 valid: group start positions, gstart[G] = M
-  uint2* pair_map;          // [M]    triangle index -> (sorted position, chunk of it):
-                            //        one 8-B record, so a join gathers one sector per pair
-  uint32_t* pos_map;        // [M]    triangle index -> sorted position alone (4 B: the EST
-                            //        joins' gather table, 200 MB at N = 10k, which the 256-MB
-                            //        MALL can hold across the joins that share this plan)
+  uint32_t* pos_map;        // [M]    triangle index -> sorted position (4 B: the joins'
+                            //        gather table, 200 MB at N = 10k, which the 256-MB MALL
+                            //        can hold across the joins that share this plan; the exact
+                            //        form's A chunk follows from the position, k_join)
   uint32_t* chunk_g;        // [nchunks+1] first group of each chunk
   uint32_t* gflag;          // [(M+31)/32 + 2] bit i = position i starts a tie group
 };
@@ -62,7 +61,6 @@ inline PlanView plan_layout(void* base, int64_t n, size_t* bytes = nullptr) {
   v.hdr = c.take<PlanHeader>(1);
   v.codes = c.take<uint32_t>((size_t)M);
   v.gstart = c.take<uint32_t>((size_t)M + 1);
-  v.pair_map = c.take<uint2>((size_t)M);
   v.pos_map = c.take<uint32_t>((size_t)M);
   v.chunk_g = c.take<uint32_t>((size_t)plan_nchunks(M) + 1);
   v.gflag = c.take<uint32_t>((size_t)(M + 31) / 32 + 2);

@@ -8,7 +8,7 @@
 //  k_group_flags   tie-group starts (equal keys; -0.0 == +0.0 by the key transform)
 //  scan            group numbering -> G
 //  k_group_starts  group start positions, largest group
-//  k_pair_maps     pair index -> sorted position, pair index -> chunk
+//  k_pos_map       pair index -> sorted position
 //  k_chunk_groups  group-aligned chunks of ~plan_chunk_len(M) positions
 //  k_pack_flags    group-start bitmask read by the engine
 #include "plan.h"
@@ -64,17 +64,12 @@ __global__ void k_group_sizes(const uint32_t* __restrict__ gstart, PlanHeader* h
   if (sz > 1) atomicMax(&hdr->max_group, sz);
 }
 
-__global__ void k_pair_maps(const uint32_t* __restrict__ codes, const uint32_t* __restrict__ flags,
-                            const uint32_t* __restrict__ gidx, const uint32_t* __restrict__ gstart,
-                            int64_t M, int64_t n, uint32_t L, uint2* __restrict__ pair_map,
-                            uint32_t* __restrict__ pos_map) {
+__global__ void k_pos_map(const uint32_t* __restrict__ codes, int64_t M, int64_t n,
+                          uint32_t* __restrict__ pos_map) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M) return;
   const uint32_t c = codes[i];
-  const uint64_t t = tri_index(c >> 16, c & 0xffffu, (uint64_t)n);
-  const uint32_t g = gidx[i] + flags[i] - 1u;
-  pair_map[t] = make_uint2((uint32_t)i, gstart[g] / L);  // a group's chunk: that of its start
-  pos_map[t] = (uint32_t)i;
+  pos_map[tri_index(c >> 16, c & 0xffffu, (uint64_t)n)] = (uint32_t)i;
 }
 
 // chunk_g[c] = first group whose start position is >= c*L (group-aligned chunks).
@@ -125,7 +120,7 @@ int build_plan(const float* rdm, int64_t n, int64_t ld, const PlanView& P, const
   VR_CHECK_LAUNCH();
   k_group_sizes<<<gb, 256, 0, st>>>(P.gstart, P.hdr);
   VR_CHECK_LAUNCH();
-  k_pair_maps<<<gb, 256, 0, st>>>(P.codes, W.flags, W.gidx, P.gstart, M, n, L, P.pair_map, P.pos_map);
+  k_pos_map<<<gb, 256, 0, st>>>(P.codes, M, n, P.pos_map);
   VR_CHECK_LAUNCH();
   k_chunk_groups<<<(unsigned)((M + 1 + 255) / 256), 256, 0, st>>>(P.gstart, P.hdr, nchunks, L,
                                                                   P.chunk_g);

@@ -514,13 +514,15 @@ __device__ inline void split_store1(uint16_t* prow, int64_t k, float v) {
   prow[(k >> 5) * 64 + 32 + (k & 31)] = l;
 }
 
+// One row of k_stats_split (one block per row): fp64 row sum -> fp32 mean, then the centred
+// values -> fp64 sum of squares (std, with the reference's zero-variance guard) and their
+// bf16 hi/lo records, in the same pass.
 template <typename T>
-__global__ __launch_bounds__(RSTAT_BS) void k_stats_split(const T* __restrict__ X, int64_t n, int64_t d,
-                                                          int64_t ldx, int64_t nstage, float correction, int vec,
-                                                          float* __restrict__ mean, float* __restrict__ stdv,
-                                                          uint16_t* __restrict__ planes) {
-  __shared__ double lds[RSTAT_BS / 64 + 1];
-  const int64_t r = blockIdx.x, kp = nstage * GK;
+__device__ inline void stats_split_row(const T* __restrict__ X, int64_t n, int64_t d, int64_t ldx, int64_t nstage,
+                                       float correction, int vec, float* __restrict__ mean,
+                                       float* __restrict__ stdv, uint16_t* __restrict__ planes, int64_t r,
+                                       double* lds) {
+  const int64_t kp = nstage * GK;
   uint16_t* prow = planes + r * nstage * 64;
   if (r >= n) {  // padding row
     for (int64_t i = threadIdx.x; i < kp / 4; i += RSTAT_BS) split_store4(prow, i, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -572,6 +574,35 @@ __global__ __launch_bounds__(RSTAT_BS) void k_stats_split(const T* __restrict__ 
     mean[r] = m;
     stdv[r] = sd;
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(RSTAT_BS) void k_stats_split(const T* __restrict__ X, int64_t n, int64_t d,
+                                                          int64_t ldx, int64_t nstage, float correction, int vec,
+                                                          float* __restrict__ mean, float* __restrict__ stdv,
+                                                          uint16_t* __restrict__ planes) {
+  __shared__ double lds[RSTAT_BS / 64 + 1];
+  stats_split_row<T>(X, n, d, ldx, nstage, correction, vec, mean, stdv, planes, blockIdx.x, lds);
+}
+
+// The same rows of several points in one launch (blockIdx.y = point): a bench extraction
+// batch's hooked outputs split together, so the launch holds rows x points blocks.
+constexpr int SPLIT_MULTI_MAX = 32;
+struct SplitMulti {
+  const float* X[SPLIT_MULTI_MAX];
+  float* mean[SPLIT_MULTI_MAX];
+  float* stdv[SPLIT_MULTI_MAX];
+  uint16_t* planes[SPLIT_MULTI_MAX];
+  int64_t d[SPLIT_MULTI_MAX];
+  int64_t ldx[SPLIT_MULTI_MAX];
+  int vec[SPLIT_MULTI_MAX];
+};
+
+__global__ __launch_bounds__(RSTAT_BS) void k_stats_split_multi(SplitMulti S, int64_t rows, float correction) {
+  __shared__ double lds[RSTAT_BS / 64 + 1];
+  const int p = blockIdx.y;
+  stats_split_row<float>(S.X[p], rows, S.d[p], S.ldx[p], (S.d[p] + GK - 1) / GK, correction, S.vec[p], S.mean[p],
+                         S.stdv[p], S.planes[p], blockIdx.x, lds);
 }
 
 template <typename T>
@@ -1583,6 +1614,30 @@ int64_t vr_rdm_plane_rows(int64_t n) { return n > 0 ? (n + WT - 1) / WT * WT : 0
 
 size_t vr_rdm_plane_row_bytes(int64_t d) {
   return d > 0 ? (size_t)((d + GK - 1) / GK) * 64 * sizeof(uint16_t) : 0;
+}
+
+int vr_rdm_split_rows_multi_f32(int npts, const float* const* X, const int64_t* d, const int64_t* ldx, int64_t rows,
+                                float correction, float* const* mean, float* const* stdv, uint16_t* const* planes,
+                                void* stream) {
+  VR_REQUIRE(npts >= 0 && npts <= SPLIT_MULTI_MAX && rows >= 0, "vr_rdm_split_rows_multi_f32: npts=%d rows=%lld",
+             npts, (long long)rows);
+  if (npts == 0 || rows == 0) return VR_OK;
+  VR_REQUIRE(X && d && ldx && mean && stdv && planes, "vr_rdm_split_rows_multi_f32: null pointer");
+  SplitMulti S{};
+  for (int p = 0; p < npts; ++p) {
+    VR_REQUIRE(X[p] && mean[p] && stdv[p] && planes[p] && d[p] > 0 && ldx[p] >= d[p],
+               "vr_rdm_split_rows_multi_f32: point %d: bad pointer or shape", p);
+    S.X[p] = X[p];
+    S.mean[p] = mean[p];
+    S.stdv[p] = stdv[p];
+    S.planes[p] = planes[p];
+    S.d[p] = d[p];
+    S.ldx[p] = ldx[p];
+    S.vec[p] = ((reinterpret_cast<uintptr_t>(X[p]) & 15) == 0) && ((ldx[p] & 3) == 0);
+  }
+  k_stats_split_multi<<<dim3((unsigned)rows, (unsigned)npts), RSTAT_BS, 0, as_stream(stream)>>>(S, rows, correction);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
 }
 
 int vr_rdm_split_rows_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, float correction,

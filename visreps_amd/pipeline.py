@@ -204,6 +204,22 @@ class RdmKernels:
                                               stream_of(x.device)), "vr_rdm_split_rows_f32")
 
     @staticmethod
+    def split_rows_multi(xs: Sequence[torch.Tensor], correction: float, outs: Sequence[SplitRows], r0: int) -> None:
+        """Rows [r0, r0 + rows) of several points' SplitRows from the (rows, d) tensors xs
+        (one launch, vr_rdm_split_rows_multi_f32; the same arithmetic as split_rows_into)."""
+        import ctypes
+
+        k = len(xs)
+        if k == 0 or xs[0].size(0) == 0:
+            return
+        P64, I64 = ctypes.c_void_p * k, ctypes.c_int64 * k
+        check(lib().vr_rdm_split_rows_multi_f32(
+            k, P64(*[x.data_ptr() for x in xs]), I64(*[x.size(1) for x in xs]), I64(*[x.stride(0) for x in xs]),
+            xs[0].size(0), float(correction), P64(*[o.mean[r0:].data_ptr() for o in outs]),
+            P64(*[o.std[r0:].data_ptr() for o in outs]), P64(*[o.planes[r0:].data_ptr() for o in outs]),
+            stream_of(xs[0].device)), "vr_rdm_split_rows_multi_f32")
+
+    @staticmethod
     def tiles_from_planes(sr: SplitRows, n: int, out: torch.Tensor, t0: int, t1: int, correction: float,
                           times: Optional[StepTimes] = None) -> None:
         """Gram tiles [t0, t1) from pre-split rows (vr_rdm_pearson_tiles_planes)."""
