@@ -743,6 +743,15 @@ constexpr int BB = 8;  // pairs per gather batch
 #ifndef VR_PROBE_NO_BASEA
 #define VR_PROBE_NO_BASEA 0
 #endif
+// timing probes of k_rankB (wrong scores; profiles/r3_engine_probes.log): VR_PROBE_WB
+// replaces the window mask lookups and transposes by a constant pattern, VR_PROBE_ACC
+// 1-3 strip the singleton accumulation (no 64-bit multiply / no St / 32-bit add only)
+#ifndef VR_PROBE_WB
+#define VR_PROBE_WB 0
+#endif
+#ifndef VR_PROBE_ACC
+#define VR_PROBE_ACC 0
+#endif
 
 // BB pairs' yA = 2 baseA[chunkA] + TB[posA] for this lane. The loads are issued in the
 // saddr form (wave-uniform 64-bit row address in SGPRs + 32-bit lane byte offset), which
@@ -1079,7 +1088,11 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       uint32_t lane_b4, lane_bt;  // opaque per window, so the base + lane sum is not hoisted
       asm("" : "=v"(lane_b4) : "0"((uint32_t)lane * 4u));
       asm("" : "=v"(lane_bt) : "0"((uint32_t)lane * (uint32_t)sizeof(TBT)));
+#if VR_PROBE_WB  // timing probe only (wrong scores): no mask lookups, no transpose
+      const uint64_t x = active ? (0xF7DFBEFDFBF7EFDFull ^ ((uint64_t)(cd & 7u) << 3)) : 0ull;
+#else
       const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+#endif
       const uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
       if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
       auto gather = [&](auto&& fn) {
@@ -1106,9 +1119,20 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
             const uint32_t m = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
             const uint32_t yb = ya[q] & m;  // x is 0 on inactive lanes
             if (j < 63) {
+#if VR_PROBE_ACC == 1
+              a64 += yb ^ c1;
+              St += yb;
+              c1 -= m;
+#elif VR_PROBE_ACC == 2
+              a64 += yb ^ c1;
+              c1 -= m;
+#elif VR_PROBE_ACC == 3
+              c1 += yb;
+#else
               a64 += (uint64_t)yb * c1;
               St += yb;
               c1 -= m;
+#endif
             } else {
               S = yb;
               cgs = c1 - 1u;
