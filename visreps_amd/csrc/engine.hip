@@ -64,6 +64,19 @@ constexpr int EST_STEP_BITS = 12;  // interpolation steps per interval: 2^12
 #ifndef VR_EST_CHECK
 #define VR_EST_CHECK 1  // 0: timing probe only (no A-side recoverability checks: unsafe)
 #endif
+// Timing probes (wrong scores; never in the default build; profiles/r3_engine_probes.log):
+// VR_PROBE_WB replaces k_rankB's window mask lookups and transposes by a constant pattern,
+// VR_PROBE_ACC 1-3 strip its singleton accumulation (no 64-bit multiply / no St / one
+// 32-bit add), VR_PROBE_STW gives k_rankA one 4-byte store per two singleton rows.
+#ifndef VR_PROBE_STW
+#define VR_PROBE_STW 0  // k_rankA timing probe: half as many (4-byte) singleton stores
+#endif
+#ifndef VR_PROBE_WB
+#define VR_PROBE_WB 0
+#endif
+#ifndef VR_PROBE_ACC
+#define VR_PROBE_ACC 0
+#endif
 static std::atomic<int64_t> g_est_reruns{0};  // passes re-run in the exact form (vr_engine_est_reruns)  // coarse intervals at most: table <= 128 x 256 B = 32 KB
 
 // log2 of the coarse interval: the smallest b >= 12 (windows of 64 never straddle a
@@ -611,6 +624,17 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
         if (cn >= sg.c1 || pn > w0 + 63u) {
           uint32_t t = EST ? y0 + 2u * cw + 1u : 2u * (cw - lp) + 1u;
           TBT* row = TB + (size_t)w0 * stride + lane;
+#if VR_PROBE_STW  // timing probe only (wrong TB layout): one 4-byte store per two rows
+          uint32_t* row2 = reinterpret_cast<uint32_t*>(TB + (size_t)w0 * stride) + lane;
+#pragma unroll
+          for (int j = 0; j < 62; j += 2) {
+            const uint32_t b0 = (uint32_t)(x >> j) & 1u, b1 = (uint32_t)(x >> (j + 1)) & 1u;
+            const uint32_t v0 = t + b0, v1 = v0 + b0 + b1;
+            if (active) __builtin_nontemporal_store(v0 | (v1 << 16), row2 + (size_t)j * stride / 2);
+            t = v1 + b1;
+          }
+          if (active) tb_store((TBT)t, row + (size_t)62 * stride);
+#else
 #pragma unroll
           for (int j = 0; j < 63; ++j) {
             const uint32_t bit = (uint32_t)(x >> j) & 1u;
@@ -618,6 +642,7 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
             if (active) tb_store((TBT)v, row + (size_t)j * stride);
             t = v + bit;
           }
+#endif
           gs = w0 + 63u;
           cgs = cw + popc64(x & lowmask(63));
           F = 0;
@@ -742,15 +767,6 @@ constexpr int BB = 8;  // pairs per gather batch
 #endif
 #ifndef VR_PROBE_NO_BASEA
 #define VR_PROBE_NO_BASEA 0
-#endif
-// timing probes of k_rankB (wrong scores; profiles/r3_engine_probes.log): VR_PROBE_WB
-// replaces the window mask lookups and transposes by a constant pattern, VR_PROBE_ACC
-// 1-3 strip the singleton accumulation (no 64-bit multiply / no St / 32-bit add only)
-#ifndef VR_PROBE_WB
-#define VR_PROBE_WB 0
-#endif
-#ifndef VR_PROBE_ACC
-#define VR_PROBE_ACC 0
 #endif
 
 // BB pairs' yA = 2 baseA[chunkA] + TB[posA] for this lane. The loads are issued in the

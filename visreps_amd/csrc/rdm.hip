@@ -903,7 +903,11 @@ __global__ __launch_bounds__(W_THREADS, 1) void k_gram3w(GramParams P) {
 #endif
 constexpr int P_PANEL = WT * 64;       // bytes of one panel sub-stage
 constexpr int P_SLOT = 2 * P_PANEL;    // A + B
-constexpr int P_SLOTS = 4;
+#ifndef VR_GRAM_SLOTS
+#define VR_GRAM_SLOTS 4  // sub-stage slots in LDS (5: 160 KB, one more sub-stage in flight; A/B)
+#endif
+constexpr int P_SLOTS = VR_GRAM_SLOTS;
+constexpr int P_AHEAD = P_SLOTS - 1;  // iteration q issues sub-stage q + P_AHEAD
 
 // this wave's two 1-KB pieces (16 rows each) of a panel sub-stage: rows [16 (2 w + i), +16)
 __device__ inline void p_issue(const GramParams& P, char* panel, int64_t row0, int q) {
@@ -1027,24 +1031,29 @@ __device__ inline void gram3p_step(const GramParams& P, char* lds, int64_t row0,
                                    const PFrag& cur, PFrag& nxt, f32x16 (&acc)[4][2]) {
   constexpr int PER = DIAG ? 2 : 4;  // glds per wave per sub-stage
   if (q + 1 < Q) {
-    if (q + 2 < Q)
+    // this wave's loads of q+1 done; those of q+2 .. q+P_AHEAD-1 (issued) may stay in flight
+    const int left = Q - 2 - q;
+    if (P_AHEAD >= 4 && left >= 2)
+      p_wait<(P_AHEAD >= 4 ? 2 : 1) * PER>();
+    else if (left >= 1)
       p_wait<PER>();
     else
       p_wait<0>();
     __builtin_amdgcn_s_barrier();
-    if (!VR_GRAM_ILV && q + 3 < Q) {
-      char* slot = lds + ((q + 3) & (P_SLOTS - 1)) * P_SLOT;
-      p_issue(P, slot, row0, q + 3);
-      if (!DIAG) p_issue(P, slot + P_PANEL, col0, q + 3);
+    if (!VR_GRAM_ILV && q + P_AHEAD < Q) {
+      char* slot = lds + ((q + P_AHEAD) % P_SLOTS) * P_SLOT;
+      p_issue(P, slot, row0, q + P_AHEAD);
+      if (!DIAG) p_issue(P, slot + P_PANEL, col0, q + P_AHEAD);
     }
-    const char* As = lds + ((q + 1) & (P_SLOTS - 1)) * P_SLOT;
+    const char* As = lds + ((q + 1) % P_SLOTS) * P_SLOT;
     p_read(As, DIAG ? As : As + P_PANEL, nxt);
   }
   if constexpr (VR_GRAM_ILV) {
     // the slot of q+3 was last read in iteration q-1, before this iteration's barrier; the
     // pieces are in flight before the next iteration's counted wait either way
+    static_assert(!VR_GRAM_ILV || P_AHEAD == 3, "interleaved issue: 4 slots");
     const bool more = q + 3 < Q;
-    char* slot = lds + ((q + 3) & (P_SLOTS - 1)) * P_SLOT;
+    char* slot = lds + ((q + 3) % P_SLOTS) * P_SLOT;
     p_mfma_ilv(cur, acc, [&](int k) {
       if (!more) return;
       if (DIAG) {
@@ -1071,19 +1080,22 @@ __device__ inline void gram3p_step(const GramParams& P, char* lds, int64_t row0,
 }
 
 template <bool DIAG>
-__device__ inline void gram3p_loop(const GramParams& P, char* lds, int64_t row0, int64_t col0,
+__device__ inline void gram3p_loop(const GramParams& P, char* lds, int64_t row0, int64_t col0, int ns,
                                    f32x16 (&acc)[4][2]) {
-  const int Q = 2 * (int)P.nstage;  // even
-  for (int q = 0; q < 3 && q < Q; ++q) {
+  const int Q = 2 * ns;  // even
+  constexpr int PER = DIAG ? 2 : 4;
+  for (int q = 0; q < P_AHEAD && q < Q; ++q) {
     char* slot = lds + q * P_SLOT;
     p_issue(P, slot, row0, q);
     if (!DIAG) p_issue(P, slot + P_PANEL, col0, q);
   }
-  // sub-stage 0 landed: loads of 1 and 2 may stay in flight
-  if (Q > 2)
-    p_wait<DIAG ? 4 : 8>();
+  // sub-stage 0 landed: the loads of 1 .. P_AHEAD-1 may stay in flight
+  if (P_AHEAD >= 4 && Q > 3)
+    p_wait<(P_AHEAD >= 4 ? 3 : 2) * PER>();
+  else if (Q > 2)
+    p_wait<2 * PER>();
   else if (Q > 1)
-    p_wait<DIAG ? 2 : 4>();
+    p_wait<PER>();
   else
     p_wait<0>();
   __builtin_amdgcn_s_barrier();
@@ -1095,16 +1107,43 @@ __device__ inline void gram3p_loop(const GramParams& P, char* lds, int64_t row0,
   }
 }
 
+// Split-K partial of one wave's 128 x 64 block: fp32 [split][super-tile][256 x 256]
+__device__ inline void gram_partial_w(const GramParams& P, f32x16 (&acc)[4][2], int split, int ltile) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3, h = lane >> 5, l32 = lane & 31;
+  float* out = P.partial + ((int64_t)split * P.tile_count + ltile) * (WT * WT);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int nn = 0; nn < 2; ++nn) {
+      const int lj = wc * 64 + nn * 32 + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int li = wr * 128 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[li * WT + lj] = acc[m][nn][r];
+      }
+    }
+}
+
+// Launch position id -> (super-tile, k split): split-major, so the blocks an XCD holds at
+// once are neighbouring tiles of one k range (shared panels in its L2). Split s covers
+// stages [s kslice / GK, min(nstage, (s + 1) kslice / GK)); one split: the whole depth.
 __global__ __launch_bounds__(W_THREADS, 1) void k_gram3p(GramParams P) {
   __shared__ __attribute__((aligned(16))) char lds[P_SLOTS * P_SLOT];
   const int id = P.blk0 + (int)xcd_remap(blockIdx.x, (uint32_t)gridDim.x);
+  const int split = id / P.tile_count, ltile = id % P.tile_count;
   int bi, bj;
-  band_tile(id, P.tile0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension here
+  band_tile(ltile, P.tile0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension here
   const bool diag = (bi == bj);
   const int64_t row0 = (int64_t)bi * WT, col0 = (int64_t)bj * WT;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   (void)lane;
+  const int64_t sper = P.kslice / GK;  // stages per split
+  const int64_t st0 = (int64_t)split * sper;
+  const int ns = (int)(P.nstage - st0 < sper ? P.nstage - st0 : sper);
+  GramParams S = P;
+  S.planes = P.planes + st0 * 64;  // records of stage st0 onwards (the row stride stays nstage)
   f32x16 acc[4][2];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -1113,12 +1152,51 @@ __global__ __launch_bounds__(W_THREADS, 1) void k_gram3p(GramParams P) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
   if (diag)
-    gram3p_loop<true>(P, lds, row0, col0, acc);
+    gram3p_loop<true>(S, lds, row0, col0, ns, acc);
   else
-    gram3p_loop<false>(P, lds, row0, col0, acc);
-  if (P.flush && (int)P.nstage > P.flush)
+    gram3p_loop<false>(S, lds, row0, col0, ns, acc);
+  if (P.flush && ns > P.flush)
     gram_unflush<WT>(acc, P.fbuf + (size_t)blockIdx.x * WT * WT, wr * 128, wc * 64);
-  gram_store_w(P, acc, row0, col0, diag);
+  if (P.splits == 1)
+    gram_store_w(P, acc, row0, col0, diag);
+  else
+    gram_partial_w(P, acc, split, ltile);
+}
+
+// Sums the split partials of one super-tile in split order and applies the epilogue
+// (k_gram_reduce for 256-tiles): block (t, strip) handles rows [32 strip, +32) of
+// super-tile t; a diagonal super-tile takes (i, j) and (j, i) from one partial entry.
+__global__ __launch_bounds__(256) void k_gram_reduce_w(GramParams P) {
+  __shared__ float tr[32][33];
+  const int ltile = blockIdx.x;
+  int bi, bj;
+  band_tile(ltile, P.tile0, P.tile_count, P.T, bi, bj);
+  const bool diag = (bi == bj);
+  const int64_t row0 = (int64_t)bi * WT, col0 = (int64_t)bj * WT;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const int si0 = blockIdx.y * 32;
+  for (int sj0 = 0; sj0 < WT; sj0 += 32) {
+    for (int yy = ty; yy < 32; yy += 8) {
+      const int li = si0 + yy, lj = sj0 + tx;
+      const int pi = (diag && li > lj) ? lj : li, pj = (diag && li > lj) ? li : lj;
+      float g = 0.f;
+      for (int s = 0; s < P.splits; ++s)
+        g += P.partial[((int64_t)s * P.tile_count + ltile) * (WT * WT) + pi * WT + pj];
+      const int64_t i = row0 + li, j = col0 + lj;
+      const float sI = (i < P.n) ? P.stdv[i] : 1.f, sJ = (j < P.n) ? P.stdv[j] : 1.f;
+      const float v = rdm_value(g, i, j, P, sI, sJ);
+      if (i < P.n && j < P.n) P.rdm[i * P.ldr + j] = v;
+      tr[yy][tx] = v;
+    }
+    __syncthreads();
+    if (!diag) {
+      for (int yy = ty; yy < 32; yy += 8) {
+        const int64_t j = col0 + sj0 + yy, i = row0 + si0 + tx;
+        if (i < P.n && j < P.n) P.rdm[j * P.ldr + i] = tr[tx][yy];
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // VISREPS_GRAM_PIPE=0: the register-staged k_gram3w (A/B timing)
@@ -1277,10 +1355,23 @@ static int gram_wide_rows(int64_t n, int64_t d, bool split3) {
 // as one run_split of their own (split-K geometry of the range: last-bit differences).
 struct RangePlan {
   bool wide = false;
-  int64_t s0 = 0, s1 = 0;          // super-tiles [s0, s1) of the wide kernel
-  int64_t rem0 = 0, rem_count = 0;  // 128-tiles of the run_split part
+  int64_t s0 = 0, s1 = 0;          // super-tiles [s0, s1) of the wide kernel, whole depth
+  int64_t r0 = 0, r_count = 0;     // super-tile rows [R, T2) (the triangle's end): wide, split-K
+  int r_splits = 1;
+  int64_t rem0 = 0, rem_count = 0;  // 128-tiles of the run_split part (unaligned ranges)
   bool rem_fit = false;             // run_split's fit_one
 };
+
+// k splits of the wide kernel's remainder launch: enough blocks for one per CU, at least
+// 8 stages per split
+static int wide_rem_splits(int64_t count, int64_t nstage) {
+  const int64_t gen = num_cus();
+  if (count <= 0 || count >= gen) return 1;
+  int64_t s = gen / count;
+  s = std::min<int64_t>(s, std::max<int64_t>(1, nstage / 8));
+  const int64_t per = (nstage + s - 1) / s;
+  return (int)((nstage + per - 1) / per);
+}
 
 static RangePlan plan_range(int64_t n, int64_t d, int64_t t0, int64_t t1, bool split3) {
   RangePlan rp;
@@ -1299,9 +1390,22 @@ static RangePlan plan_range(int64_t n, int64_t d, int64_t t0, int64_t t1, bool s
   rp.wide = true;
   rp.s0 = tri_start(r0, T2);
   rp.s1 = t1 == total ? tri_start(R, T2) : tri_start(r1, T2);
-  rp.rem0 = trem;
-  rp.rem_count = t1 == total ? total - trem : 0;
-  rp.rem_fit = true;
+  rp.rem_count = 0;
+  // VISREPS_GRAM_WIDE_REM=1: the rows below R on the same kernel split over k (one
+  // generation, k_gram_reduce_w) instead of 128-tiles (run_split). Within noise at N = 10k
+  // (profiles/r3_gram_ab.log: +0.7-1.4 % on whole RDMs in alternating rounds, -2 % across
+  // two bench runs): the wide kernel's per-CU rate is spent on +16 % work (the diagonal
+  // super-tiles' lower quadrants), 220 of 256 CUs busy and the partial round trip.
+  static const bool wide_rem = getenv("VISREPS_GRAM_WIDE_REM") && strcmp(getenv("VISREPS_GRAM_WIDE_REM"), "1") == 0;
+  if (t1 == total && !wide_rem) {
+    rp.rem0 = trem;
+    rp.rem_count = total - trem;
+    rp.rem_fit = true;
+  } else if (t1 == total) {
+    rp.r0 = tri_start(R, T2);
+    rp.r_count = T2 * (T2 + 1) / 2 - rp.r0;
+    rp.r_splits = wide_rem_splits(rp.r_count, (d + GK - 1) / GK);
+  }
   return rp;
 }
 
@@ -1323,7 +1427,8 @@ static size_t gram_ws(int64_t n, int64_t d, int64_t t0, int64_t t1, bool split3,
                       float** stdv, float** partial, uint16_t** planes, float** fbuf = nullptr,
                       bool own_planes = true) {
   const RangePlan rp = plan_range(n, d, t0, t1, split3);
-  const size_t part = range_partial(n, d, rp.rem_count, rp.rem_fit);
+  size_t part = range_partial(n, d, rp.rem_count, rp.rem_fit);
+  if (rp.r_splits > 1) part = std::max(part, (size_t)rp.r_count * rp.r_splits * WT * WT);
   Carver c(base);
   float* m = c.take<float>((size_t)n);
   float* s = c.take<float>((size_t)n);
@@ -1525,6 +1630,7 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   W.tile0 = (int)rp.s0;
   W.tile_count = (int)(rp.s1 - rp.s0);
   W.splits = 1;
+  W.kslice = P.nstage * GK;
   const int gen = num_cus();
   const bool pipe = gram_pipe();
   W.flush = (size_t)gen * WT * WT <= gram_fbuf_floats() ? flush_stages : 0;
@@ -1536,6 +1642,25 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
     else
       k_gram3w<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
     VR_CHECK_LAUNCH();
+  }
+  if (rp.r_count > 0) {  // rows [R, T2): split over k, partials summed in split order
+    GramParams Rm = W;
+    Rm.tile0 = (int)rp.r0;
+    Rm.tile_count = (int)rp.r_count;
+    Rm.splits = rp.r_splits;
+    Rm.kslice = (P.nstage + rp.r_splits - 1) / rp.r_splits * GK;
+    const int nblk = Rm.tile_count * Rm.splits;
+    for (int b0 = 0; b0 < nblk; b0 += gen) {
+      Rm.blk0 = b0;
+      const int nb = std::min(gen, nblk - b0);
+      KtScope kt(KT_GRAM_WIDE, 2.0 * (double)nb / Rm.splits * WT * WT * (double)d, st);
+      k_gram3p<<<(unsigned)nb, W_THREADS, 0, st>>>(Rm);
+      VR_CHECK_LAUNCH();
+    }
+    if (Rm.splits > 1) {
+      k_gram_reduce_w<<<dim3((unsigned)Rm.tile_count, WT / 32), 256, 0, st>>>(Rm);
+      VR_CHECK_LAUNCH();
+    }
   }
   return run_split(rp.rem0, rp.rem_count, true);
 }
