@@ -1199,6 +1199,331 @@ __global__ __launch_bounds__(256) void k_gram_reduce_w(GramParams P) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Phased wide split Gram on v_mfma_f32_16x16x32_bf16 (k_gram3e, VISREPS_GRAM_KERNEL=e).
+// The same 256 x 256 super-tiles, 8 waves as 2 x 4 and 128 x 64 wave tiles as k_gram3p,
+// the same three products per k, but whole 32-k stage records in LDS (one 128-B record
+// per row) and the 16 x 16 MFMA shape, which the chip clocks higher than 32 x 32 under
+// load (MI355X_MICROARCH.md, DVFS give-back item 7).
+// A stage is four 16-KB half-tiles (A rows 0-127 / 128-255, B the same), two stages
+// double-buffered (128 KB). A wave's 128 x 64 block is four quadrants (64-row half a0/a1
+// of its rows x 32-column half b0/b1): one phase per quadrant, 24 MFMAs each, in the
+// order (a0,b0) (a0,b1) (a1,b1) (a1,b0). Each phase first issues the LDS reads of the
+// fragments the NEXT phase needs (registers AX/AY for the A halves, BP/BQ for the B
+// halves: 96 VGPRs), then its MFMAs, which use fragments read one phase earlier:
+//   P0(t): MFMA a0 b0; read b1(t)        P1(t): MFMA a0 b1; read a1(t)
+//   P2(t): MFMA a1 b1; read a0(t+1)      P3(t): MFMA a1 b0; read b0(t+1)
+// One half-tile is staged per phase by LDS-DMA (two 1-KB pieces per wave):
+//   P0(t): A-bot(t+1)   P1(t): B-right(t+1)   P2(t): B-left(t+2)   P3(t): A-top(t+2)
+// so a buffer is restaged >= 2 phases after its last read (the reads of phase p are
+// consumed by phase p+1's MFMAs, which every wave has passed at phase p+2's barrier), and
+// each wave waits (counted vmcnt) before the barrier of the phase that first reads a
+// stage: P2(t) for the A halves of t+1 (B-right(t+1) may stay in flight), P3(t) for the B
+// halves (B-left(t+2) may). Diagonal super-tiles stage and read the A halves only.
+// LDS image of a half-tile: row r's 16-B chunk c at r * 128 + (c ^ ((r >> 1) & 7)) * 16;
+// a fragment read (16 rows of a 16-row block, one chunk per 16 lanes) then touches 16
+// distinct 16-B bank slots in each ds_read_b128 lane group.
+// ------------------------------------------------------------------------------------
+constexpr int E_HALF = 128 * 128;    // bytes of a half-tile stage (128 rows x 128 B)
+constexpr int E_STAGE = 4 * E_HALF;  // A-top, A-bot, B-left, B-right
+
+// this wave's two 1-KB pieces (rows [16 wid, +16)) of half-tile h (0/1: A rows 0-127 /
+// 128-255 of the super-tile, 2/3: B) of stage st into the stage buffer sb. The lane part
+// of the source address (row rr of the half-tile, logical chunk c) is the same for every
+// half-tile and stage: a 32-bit offset computed once (e_issue_off); the rest is uniform.
+__device__ inline uint32_t e_issue_off(const GramParams& P, int k) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int rr = wid * 16 + k * 8 + (lane >> 3);
+  const int c = (lane & 7) ^ ((rr >> 1) & 7);  // the logical chunk this lane's slot holds
+  return (uint32_t)rr * (uint32_t)P.nstage * 128u + (uint32_t)c * 16u;
+}
+__device__ inline void e_issue(const GramParams& P, char* sb, int h, int64_t row0, int64_t col0, int64_t st,
+                               const uint32_t (&io)[2]) {
+  const int wid = threadIdx.x >> 6;
+  const int64_t rbase = (h < 2 ? row0 : col0) + (h & 1) * 128;
+  const char* base = reinterpret_cast<const char*>(P.planes) + (rbase * P.nstage + st) * 128;
+  char* half = sb + h * E_HALF;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    uint32_t off = io[k];
+    asm volatile("" : "+v"(off));  // formed here: no 64-bit address per half-tile hoisted out of the loop
+    __builtin_amdgcn_global_load_lds(base + off, half + (wid * 16 + k * 8) * 128, 16, 0, 0);
+  }
+}
+
+struct EFragA {
+  bf16x8 hi[4], lo[4];  // 4 row blocks of 16
+};
+struct EFragB {
+  bf16x8 hi[2], lo[2];  // 2 column blocks of 16
+};
+
+// rows r0 + 16 m + (lane & 15) of a half-tile (r0 a multiple of 16); lane group
+// g = lane >> 4 holds k 8g..8g+7. The swizzle term of a row depends only on lane & 15, so
+// every read is this lane's constant offset (hi or lo chunk) plus a uniform immediate.
+struct ELane {
+  uint32_t hi, lo;  // byte offsets of this lane's hi / lo chunk in its row of a 16-row block
+};
+__device__ inline ELane e_lane() {
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15, swz = (l16 >> 1) & 7;
+  return ELane{(uint32_t)(l16 * 128 + ((g ^ swz) << 4)), (uint32_t)(l16 * 128 + (((4 + g) ^ swz) << 4))};
+}
+__device__ inline void e_read_a(const char* half, int r0, const ELane& o, EFragA& f) {
+  uint32_t ohi = o.hi, olo = o.lo;  // opaque per call: the read addresses are formed here
+  asm volatile("" : "+v"(ohi), "+v"(olo));
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const char* row = half + (r0 + m * 16) * 128;
+    f.hi[m] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(row + ohi));
+    f.lo[m] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(row + olo));
+  }
+}
+__device__ inline void e_read_b(const char* half, int r0, const ELane& o, EFragB& f) {
+  uint32_t ohi = o.hi, olo = o.lo;  // opaque per call: the read addresses are formed here
+  asm volatile("" : "+v"(ohi), "+v"(olo));
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const char* row = half + (r0 + n * 16) * 128;
+    f.hi[n] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(row + ohi));
+    f.lo[n] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(row + olo));
+  }
+}
+
+#ifndef VR_E_PRIO
+#define VR_E_PRIO 0  // 1: s_setprio(1) over each phase's MFMAs (A/B)
+#endif
+// quadrant (MA, NB) of the wave's block: 4 x 2 tiles of 16 x 16, hh, hl, lh products
+template <int MA, int NB>
+__device__ inline void e_mfma(const EFragA& a, const EFragB& b, f32x4 (&acc)[8][4]) {
+#if VR_E_PRIO
+  __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+      acc[MA * 4 + m][NB * 2 + n] =
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi[m], b.hi[n], acc[MA * 4 + m][NB * 2 + n], 0, 0, 0);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+      acc[MA * 4 + m][NB * 2 + n] =
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi[m], b.lo[n], acc[MA * 4 + m][NB * 2 + n], 0, 0, 0);
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+      acc[MA * 4 + m][NB * 2 + n] =
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo[m], b.hi[n], acc[MA * 4 + m][NB * 2 + n], 0, 0, 0);
+#if VR_E_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
+// 16 x 16 C/D map: col = lane & 15, row = 4 (lane >> 4) + e. Flush buffer: the block's
+// 256 x 256 fp32 tile (k_gram3p's two-level sum, same interval).
+__device__ inline float* e_flush_base(float* buf) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t off = (uint32_t)(((wid >> 2) * 128 + 4 * (lane >> 4)) * WT + (wid & 3) * 64 + (lane & 15));
+  asm volatile("" : "+v"(off));
+  return buf + off;
+}
+__device__ inline void e_flush(f32x4 (&acc)[8][4], float* buf, bool first) {
+  float* b = e_flush_base(buf);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float* p = b + (i * 16 + e) * WT + j * 16;
+        *p = first ? acc[i][j][e] : *p + acc[i][j][e];
+        acc[i][j][e] = 0.f;
+      }
+}
+__device__ inline void e_unflush(f32x4 (&acc)[8][4], const float* buf) {
+  const float* b = e_flush_base(const_cast<float*>(buf));
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[i][j][e] += b[(i * 16 + e) * WT + j * 16];
+}
+
+// Epilogue of the wave's 128 x 64 block (8 x 4 tiles of 16 x 16), as gram_store_w: a
+// diagonal super-tile writes each i < j entry from its (i, j) accumulator to both places.
+__device__ inline void e_store(const GramParams& P, f32x4 (&acc)[8][4], int64_t row0, int64_t col0, bool diag) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3, g = lane >> 4, l16 = lane & 15;
+#pragma unroll
+  for (int j4 = 0; j4 < 4; ++j4) {
+    const int64_t j = col0 + wc * 64 + j4 * 16 + l16;
+    const float sj = (j < P.n) ? P.stdv[j] : 1.f;
+#pragma unroll
+    for (int i8 = 0; i8 < 8; ++i8) {
+      const int64_t ib = row0 + wr * 128 + i8 * 16 + 4 * g;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t i = ib + e;
+        const float si = (i < P.n) ? P.stdv[i] : 1.f;
+        v[e] = rdm_value(acc[i8][j4][e], i, j, P, si, sj);
+      }
+      if (diag) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t i = ib + e;
+          if (i <= j && j < P.n) {
+            P.rdm[i * P.ldr + j] = v[e];
+            if (i < j) P.rdm[j * P.ldr + i] = v[e];
+          }
+        }
+        continue;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t i = ib + e;
+        if (i < P.n && j < P.n) P.rdm[i * P.ldr + j] = v[e];
+      }
+      if (j < P.n) {
+        float* dst = P.rdm + j * P.ldr + ib;
+        if (P.vec && ib + 3 < P.n && ((P.ldr & 3) == 0)) {
+          f32x4 w = {v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(dst) = w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (ib + e < P.n) dst[e] = v[e];
+        }
+      }
+    }
+  }
+}
+
+// One stage t of the phase loop. ODD selects the B register roles: in even stages b0
+// arrives in BP and b1 in BQ, in odd stages the other way round (see above).
+// s_barrier plus a compiler fence: no LDS read or LDS-DMA issue moves across it
+__device__ inline void e_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool DIAG, bool ODD>
+__device__ inline void e_stage(const GramParams& P, char* lds, int64_t row0, int64_t col0, int t, int ns,
+                               const ELane& o, const uint32_t (&io)[2], EFragA& AX, EFragA& AY,
+                               EFragB& BP, EFragB& BQ, f32x4 (&acc)[8][4]) {
+  const int wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  EFragB& B0 = ODD ? BQ : BP;  // b0 of this stage
+  EFragB& B1 = ODD ? BP : BQ;  // b1 of this stage, then b0 of the next
+  char* cur = lds + (t & 1) * E_STAGE;
+  char* nxt = lds + ((t + 1) & 1) * E_STAGE;
+  const int ha = wr, hb = DIAG ? (wc >> 1) : 2 + (wc >> 1);  // this wave's A / B half-tiles
+  const int rb = (wc & 1) * 64;                               // its 64 columns inside hb
+  const bool more1 = t + 1 < ns, more2 = t + 2 < ns;
+  // P0: MFMA a0 b0; read b1(t); stage A-bot(t+1)
+  e_barrier();
+  if (more1) e_issue(P, nxt, 1, row0, col0, t + 1, io);
+  e_read_b(cur + hb * E_HALF, rb + 32, o, B1);
+  e_mfma<0, 0>(AX, B0, acc);
+  // P1: MFMA a0 b1; read a1(t); stage B-right(t+1)
+  e_barrier();
+  if (!DIAG && more1) e_issue(P, nxt, 3, row0, col0, t + 1, io);
+  e_read_a(cur + ha * E_HALF, 64, o, AY);
+  e_mfma<0, 1>(AX, B1, acc);
+  // P2: MFMA a1 b1; read a0(t+1) (wait for the A halves of t+1); stage B-left(t+2)
+  if (more1) {
+    if (DIAG)
+      p_wait<0>();
+    else
+      p_wait<2>();
+  }
+  e_barrier();
+  if (!DIAG && more2) e_issue(P, cur, 2, row0, col0, t + 2, io);
+  if (more1) e_read_a(nxt + ha * E_HALF, 0, o, AX);
+  e_mfma<1, 1>(AY, B1, acc);
+  // P3: MFMA a1 b0; read b0(t+1) into B1's registers (wait for the B halves of t+1);
+  // stage A-top(t+2)
+  if (!DIAG && more1) {
+    if (more2)
+      p_wait<2>();
+    else
+      p_wait<0>();
+  }
+  e_barrier();
+  if (more2) e_issue(P, cur, 0, row0, col0, t + 2, io);
+  if (more1) e_read_b(nxt + hb * E_HALF, rb, o, B1);
+  e_mfma<1, 0>(AY, B0, acc);
+  if (P.flush && more1 && (t + 1) % P.flush == 0) e_flush(acc, P.fbuf + (size_t)blockIdx.x * WT * WT, t + 1 == P.flush);
+}
+
+template <bool DIAG>
+__device__ inline void e_loop(const GramParams& P, char* lds, int64_t row0, int64_t col0, int ns,
+                              f32x4 (&acc)[8][4]) {
+  const int wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int ha = wr, hb = DIAG ? (wc >> 1) : 2 + (wc >> 1), rb = (wc & 1) * 64;
+  const uint32_t io[2] = {e_issue_off(P, 0), e_issue_off(P, 1)};
+  // prologue: stage 0 whole, and stage 1's first two half-tiles (B-left, A-top), in the
+  // order the loop issues them
+  e_issue(P, lds, 0, row0, col0, 0, io);
+  e_issue(P, lds, 1, row0, col0, 0, io);
+  if (!DIAG) {
+    e_issue(P, lds, 2, row0, col0, 0, io);
+    e_issue(P, lds, 3, row0, col0, 0, io);
+  }
+  if (ns > 1) {
+    if (!DIAG) e_issue(P, lds + E_STAGE, 2, row0, col0, 1, io);
+    e_issue(P, lds + E_STAGE, 0, row0, col0, 1, io);
+    if (DIAG)
+      p_wait<2>();
+    else
+      p_wait<4>();
+  } else {
+    p_wait<0>();
+  }
+  e_barrier();
+  const ELane o = e_lane();
+  EFragA AX, AY;
+  EFragB BP, BQ;
+  e_read_a(lds + ha * E_HALF, 0, o, AX);
+  e_read_b(lds + hb * E_HALF, rb, o, BP);
+  for (int t = 0; t < ns; t += 2) {
+    e_stage<DIAG, false>(P, lds, row0, col0, t, ns, o, io, AX, AY, BP, BQ, acc);
+    if (t + 1 < ns) e_stage<DIAG, true>(P, lds, row0, col0, t + 1, ns, o, io, AX, AY, BP, BQ, acc);
+  }
+}
+
+__global__ __launch_bounds__(W_THREADS, 1) void k_gram3e(GramParams P) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * E_STAGE];
+  const int id = P.blk0 + (int)xcd_remap(blockIdx.x, (uint32_t)gridDim.x);
+  int bi, bj;
+  band_tile(id, P.tile0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension
+  const bool diag = (bi == bj);
+  const int64_t row0 = (int64_t)bi * WT, col0 = (int64_t)bj * WT;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ns = (int)P.nstage;
+  if (diag)
+    e_loop<true>(P, lds, row0, col0, ns, acc);
+  else
+    e_loop<false>(P, lds, row0, col0, ns, acc);
+  if (P.flush && ns > P.flush) e_unflush(acc, P.fbuf + (size_t)blockIdx.x * WT * WT);
+  e_store(P, acc, row0, col0, diag);
+}
+
+// The full-depth wide launches run k_gram3e (measured +3.5-8.5 % over k_gram3p on whole
+// RDMs at N = 10k, profiles/r3_gram_ab.log); VISREPS_GRAM_KERNEL=p selects k_gram3p (A/B).
+static bool gram_phased() {
+  const char* e = getenv("VISREPS_GRAM_KERNEL");
+  return !(e && strcmp(e, "p") == 0);
+}
+
 // VISREPS_GRAM_PIPE=0: the register-staged k_gram3w (A/B timing)
 static bool gram_pipe() {
   const char* e = getenv("VISREPS_GRAM_PIPE");
@@ -1632,12 +1957,14 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   W.splits = 1;
   W.kslice = P.nstage * GK;
   const int gen = num_cus();
-  const bool pipe = gram_pipe();
+  const bool pipe = gram_pipe(), phased = gram_phased();
   W.flush = (size_t)gen * WT * WT <= gram_fbuf_floats() ? flush_stages : 0;
   for (int b0 = 0; b0 < W.tile_count; b0 += gen) {
     W.blk0 = b0;
     KtScope kt(KT_GRAM_WIDE, 2.0 * (double)std::min(gen, W.tile_count - b0) * WT * WT * (double)d, st);
-    if (pipe)
+    if (phased)
+      k_gram3e<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
+    else if (pipe)
       k_gram3p<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
     else
       k_gram3w<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
