@@ -53,8 +53,8 @@ from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_resp
 from visreps_amd.models.custom_model import CustomCNN
 from visreps_amd.models.utils import FeatureExtractor
 from visreps_amd._lib import KTIMER_KERNELS, check, ktimer_enable, ktimer_read, lib, stream_of
-from visreps_amd.pipeline import (KERNELS, ShardedRDMs, StepTimes, all_units_rsa, engine_bytes, engine_call_bytes,
-                                  engine_pair_bytes, make_schedule, phase1_rows, phase1_select)
+from visreps_amd.pipeline import (KERNELS, PlanPrefetch, ShardedRDMs, StepTimes, all_units_rsa, engine_bytes,
+                                  engine_call_bytes, engine_pair_bytes, make_schedule, phase1_rows, phase1_select)
 
 METRIC = "end-to-end RSA eval sec (extract→RDM→1000-bootstrap Spearman), N=10k stimuli"
 LAYERS = ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
@@ -345,6 +345,11 @@ def main():
     sched = make_schedule(N, dims, points, NSD_ROIS_4, world)
 
     split = split_mode(N, dims)
+    # VISREPS_PLAN_PREFETCH=1: rank plans on a second stream under the Grams. Measured neutral
+    # (profiles/r3_bench_ab.log: the Grams' 2 x 245 VGPRs per SIMD leave no room beside them,
+    # so the plan kernels only interleave: units -43 ms, Grams +33 ms); off by default.
+    prefetch = os.environ.get("VISREPS_PLAN_PREFETCH", "0") == "1"
+    plan_stream = torch.cuda.Stream(device=dev) if prefetch else None
     _, _, keep = phase1_rows(N, 1000, 42, rank, world)
 
     def step(times: StepTimes):
@@ -364,12 +369,15 @@ def main():
         sel = phase1_select(feats, projectors, responses, points, N, n_select=1000, seed=42,
                             pg=pg, times=times, selected_rows=sel_rows)
         ev[2].record()
-        rd = ex.finish()  # this rank's RDMs: its pieces' Grams + the exchange of the rest
+        # this rank's RDMs: its pieces' Grams + the exchange of the rest; the rank plans of the
+        # RDMs its units read are built on a second stream as each RDM is ready
+        pf = PlanPrefetch(dev, sched.needs(rank), plan_stream) if prefetch else None
+        rd = ex.finish(on_ready=pf)
         ev[3].record()
         del feats, rows, ex, sel_rows
         neural = {r: rd[("n", r)] for r in regions if ("n", r) in rd}
         res = all_units_rsa(lambda p: rd.pop(("m", p)), points, neural, N, n_boot=args.boot, seed=42, pg=pg,
-                            times=times, regions=regions)
+                            times=times, regions=regions, plans=pf.plans() if pf else None)
         ev[4].record()
         times.phases(["extract", "phase1", "rdms", "units"], ev)
         return res, neural, sel

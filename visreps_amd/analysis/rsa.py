@@ -154,7 +154,8 @@ class RankPlan:
     Built once per RDM and reused by every Spearman against it: the model RDM of a
     layer serves all ROIs, a neural RDM all layers."""
 
-    def __init__(self, rdm: torch.Tensor):
+    def __init__(self, rdm: torch.Tensor, ws_tag: str = "plan_build"):
+        # ws_tag: the scratch of builds on another stream (pipeline.PlanPrefetch) is its own
         if rdm.ndim != 2 or rdm.size(0) != rdm.size(1):
             raise ValueError("RankPlan needs a square 2-D RDM")
         self.device = _device_for(rdm)
@@ -166,7 +167,7 @@ class RankPlan:
                              "compute_rdm_correlation / spearman_full")
         L = lib()
         self.buf = torch.empty(L.vr_rank_plan_bytes(self.n), dtype=torch.uint8, device=self.device)
-        ws = workspace.get(self.device, L.vr_rank_plan_workspace(self.n), "plan_build")
+        ws = workspace.get(self.device, L.vr_rank_plan_workspace(self.n), ws_tag)
         with torch.cuda.device(self.device):
             check(
                 L.vr_rank_plan_build_f32(
