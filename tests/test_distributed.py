@@ -304,3 +304,55 @@ def test_bench_schedule(world):
 def test_row_boundaries_for_split_tests_are_a_partition():
     b = _row_boundaries(300, 40)
     assert b[0] == 0 and b[-1] == int(P.lib().vr_rdm_tile_count(300)) and b == sorted(set(b))
+
+
+def _phase1_worker(rank, world, port, n, n_select, out_dir):
+    """pipeline.phase1_select over gloo: points dealt round-robin, projections reduced to
+    their owner, region scores all-gathered (kernels emulated as above)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    R.RankPlan = _OraclePlan
+    R.bootstrap_spearman_multi = _oracle_multi
+    X, Y, Z = _data(n, 40)
+    rows = shard_rows(n, rank, world)
+    feats = {"x": torch.from_numpy(X[rows.start:rows.stop]), "z": torch.from_numpy(Z[rows.start:rows.stop]),
+             "w": torch.from_numpy((X[rows.start:rows.stop] * Z[rows.start:rows.stop]).copy())}
+    gen = torch.Generator().manual_seed(5)
+    mats = {p: torch.randn(40, 24, generator=gen) for p in feats}
+    projectors = {p: (lambda x, m=mats[p]: x.double() @ m.double()) for p in feats}
+    responses = {"r0": torch.from_numpy(Y[rows.start:rows.stop]), "r1": torch.from_numpy(X[rows.start:rows.stop, :20])}
+    sel = P.phase1_select(feats, projectors, responses, list(feats), n, n_select=n_select, seed=42,
+                          pg=dist.group.WORLD, kernels=CpuKernels())
+    with open(os.path.join(out_dir, f"p1_{world}_{rank}.txt"), "w") as f:
+        for r in sorted(sel):
+            best, lst = sel[r]
+            f.write(r + " " + best + " " + " ".join(f"{e['layer']}:{e['score']:.17g}" for e in lst) + "\n")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_phase1_points_dealt_over_ranks(tmp_path, world):
+    n, n_select = 120, 50
+    for w in (1, world):
+        mp.spawn(_phase1_worker, args=(w, _free_port(), n, n_select, str(tmp_path)), nprocs=w, join=True)
+    ref = (tmp_path / "p1_1_0.txt").read_text()
+    for r in range(world):  # every rank, the same selection and scores as one process
+        assert (tmp_path / f"p1_{world}_{r}.txt").read_text() == ref
+    # and those are the oracle's: SRP of the selection rows, emulated RDMs, midrank Spearman
+    X, Y, Z = _data(n, 40)
+    sel_idx = np.random.RandomState(42).choice(n, n_select, replace=False)
+    gen = torch.Generator().manual_seed(5)
+    full = {"x": X, "z": Z, "w": X * Z}
+    mats = {p: torch.randn(40, 24, generator=gen) for p in full}
+    for line in ref.splitlines():
+        r, best, *pairs = line.split()
+        y = (Y if r == "r0" else X[:, :20])[sel_idx]
+        nr = emulated_rdm(np.ascontiguousarray(y))
+        iu = np.triu_indices(n_select, 1)
+        want = {}
+        for p in full:
+            proj = (torch.from_numpy(full[p][sel_idx]).double() @ mats[p].double()).float().numpy()
+            want[p] = O.midrank_spearman(emulated_rdm(proj)[iu], nr[iu])
+        got = {kv.split(":")[0]: float(kv.split(":")[1]) for kv in pairs}
+        assert all(abs(got[p] - want[p]) < 1e-12 for p in full), (got, want)
+        assert best == max(full, key=lambda p: (want[p], -list(full).index(p)))

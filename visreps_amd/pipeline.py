@@ -695,7 +695,8 @@ def phase1_rows(n: int, n_select: Optional[int], seed: int, rank: int, world: in
 def phase1_select(feats: Dict[str, torch.Tensor], projectors: Dict, responses: Dict[str, torch.Tensor],
                   points: Sequence[str], n: int, *, n_select: int = 1000, seed: int = 42,
                   pg=None, times: Optional[StepTimes] = None,
-                  selected_rows: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, Tuple[str, List[Dict]]]:
+                  selected_rows: Optional[Dict[str, torch.Tensor]] = None,
+                  kernels: Optional[RdmKernels] = None) -> Dict[str, Tuple[str, List[Dict]]]:
     """Phase-1 layer selection of the reference eval (evals.py:249-287) on stimulus-sharded
     features. RandomState(seed).choice(n, n_select) picks the selection stimuli (re-created
     per (region, subject); the regions share one subject's stimuli, so one draw serves them
@@ -703,45 +704,75 @@ def phase1_select(feats: Dict[str, torch.Tensor], projectors: Dict, responses: D
     bulk extraction's torch.sparse.mm, models/utils.py:297-344, here vr_srp_csr_f32). The
     projection is row by row, so projecting the selected rows equals projecting every row
     and selecting after, as the reference does: phase 1 reads no other projected row
-    (evals.py:254-268) and phase 2 re-extracts. Then selection RDMs of the projected points
-    and of each region's responses; Spearman of every point against every region; best =
-    first strict maximum. selected_rows[p] (optional) holds this rank's selected rows of
-    point p in phase1_rows order, kept during extraction instead of all of feats[p].
-    Returns {region: (best point, [{"layer", "score"} per point])} on every rank."""
+    (evals.py:254-268) and phase 2 re-extracts.
+
+    Over ranks the points are dealt round-robin: point i's projected rows are summed (the
+    ranks' rows are disjoint: exact) onto rank i mod world only, which builds its selection
+    RDM and plan and scores it against every region; the regions' selection RDMs (small) are
+    built on every rank; the (point, region) scores are all-gathered. Scores do not depend
+    on the world size (exact sums, exact-integer Spearman). Best = first strict maximum.
+    selected_rows[p] (optional) holds this rank's selected rows of point p in phase1_rows
+    order, kept during extraction instead of all of feats[p]. kernels: the RDM entry points
+    (RdmKernels; a CPU emulation in the gloo tests). Returns {region: (best point,
+    [{"layer", "score"} per point])} on every rank."""
     rank, world = _world(pg)
+    K = kernels or KERNELS
     k, mine, src = phase1_rows(n, n_select, seed, rank, world)
     dev = next(iter(responses.values())).device
     pos_t = torch.as_tensor(mine, dtype=torch.long, device=dev)
     src_t = torch.as_tensor(src, dtype=torch.long, device=dev)
+    owner = {p: i % world for i, p in enumerate(points)}
 
-    def selected(x_mine: torch.Tensor) -> torch.Tensor:  # this rank's selected rows -> (k, d), every rank
+    def selected(x_mine: torch.Tensor, dst: Optional[int]) -> torch.Tensor:
+        """this rank's selected rows -> (k, d) on rank dst (None: on every rank)"""
         out = torch.zeros((k, x_mine.size(1)), dtype=torch.float32, device=dev)
         out[pos_t] = x_mine.float()
         if world > 1:  # disjoint rows: the sum is exact
-            dist.all_reduce(out, op=dist.ReduceOp.SUM, group=pg)
+            if dst is None or (out.is_cuda and dist.get_backend(pg) != "nccl"):
+                # (gloo reduces no device tensors: the one-GPU rehearsal sums on every rank)
+                dist.all_reduce(out, op=dist.ReduceOp.SUM, group=pg)
+            else:
+                g = dst if pg is None or pg == dist.group.WORLD else dist.get_global_rank(pg, dst)
+                dist.reduce(out, dst=g, op=dist.ReduceOp.SUM, group=pg)
         return out
 
     def timed_rdm(x: torch.Tensor) -> torch.Tensor:
         out = torch.empty((x.size(0), x.size(0)), dtype=torch.float32, device=dev)
-        rdm_tiles_into(x, out, 0, int(lib().vr_rdm_tile_count(x.size(0))), times=times)
+        K.tiles_from_rows(x, out, 0, int(lib().vr_rdm_tile_count(x.size(0))), 1e-12, times)
         return out
 
-    mplans = []
+    mplans = {}
     for p in points:
         rows_p = selected_rows[p] if selected_rows is not None else feats[p][src_t]
         proj = projectors[p](rows_p)  # SRP of this rank's selected stimuli
-        mplans.append(R.RankPlan(timed_rdm(selected(proj))))
-        del proj
-    out = {}
+        full = selected(proj, owner[p])
+        if owner[p] == rank:
+            mplans[p] = R.RankPlan(timed_rdm(full))
+        del proj, full
+    mine_pts = [p for p in points if p in mplans]
+    scores: Dict[Tuple[str, str], float] = {}
     for r, y in responses.items():
-        pn = R.RankPlan(timed_rdm(selected(y[src_t])))
-        sc = R.bootstrap_spearman_multi(pn, mplans, None, full_first=True)[:, 0].cpu().numpy()
-        best, best_score, scores = None, -float("inf"), []
-        for p, v in zip(points, sc):
-            scores.append({"layer": p, "score": float(v)})
+        pn = R.RankPlan(timed_rdm(selected(y[src_t], None)))
+        if mine_pts:
+            sc = torch.as_tensor(R.bootstrap_spearman_multi(pn, [mplans[p] for p in mine_pts], None,
+                                                            full_first=True))[:, 0].cpu().numpy()
+            for p, v in zip(mine_pts, sc):
+                scores[(p, r)] = float(v)
+    if world > 1:
+        gathered: List[Dict] = [None] * world
+        dist.all_gather_object(gathered, scores, group=pg)
+        scores = {}
+        for g in gathered:
+            scores.update(g)
+    out = {}
+    for r in responses:
+        best, best_score, lst = None, -float("inf"), []
+        for p in points:
+            v = scores[(p, r)]
+            lst.append({"layer": p, "score": v})
             if v > best_score:  # strict: the first maximal point wins (evals.py:273-275)
-                best, best_score = p, float(v)
-        out[r] = (best, scores)
+                best, best_score = p, v
+        out[r] = (best, lst)
     return out
 
 
