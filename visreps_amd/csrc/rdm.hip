@@ -1496,25 +1496,48 @@ __device__ inline void e_loop(const GramParams& P, char* lds, int64_t row0, int6
   }
 }
 
+// Split-K partial of the wave's block: fp32 [split][super-tile][256 x 256] (k_gram_reduce_w)
+__device__ inline void e_partial(const GramParams& P, f32x4 (&acc)[8][4], int split, int ltile) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3, g = lane >> 4, l16 = lane & 15;
+  float* out = P.partial + ((int64_t)split * P.tile_count + ltile) * (WT * WT);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[(wr * 128 + i * 16 + 4 * g + e) * WT + wc * 64 + j * 16 + l16] = acc[i][j][e];
+}
+
+// Launch position id -> (super-tile, k split) as k_gram3p: split-major; one split = the
+// whole depth (P.kslice = nstage * GK).
 __global__ __launch_bounds__(W_THREADS, 1) void k_gram3e(GramParams P) {
   __shared__ __attribute__((aligned(16))) char lds[2 * E_STAGE];
   const int id = P.blk0 + (int)xcd_remap(blockIdx.x, (uint32_t)gridDim.x);
+  const int split = id / P.tile_count, ltile = id % P.tile_count;
   int bi, bj;
-  band_tile(id, P.tile0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension
+  band_tile(ltile, P.tile0, P.tile_count, P.T, bi, bj);  // P.T = super-tiles per dimension
   const bool diag = (bi == bj);
   const int64_t row0 = (int64_t)bi * WT, col0 = (int64_t)bj * WT;
+  const int64_t sper = P.kslice / GK;  // stages per split
+  const int64_t st0 = (int64_t)split * sper;
+  const int ns = (int)(P.nstage - st0 < sper ? P.nstage - st0 : sper);
+  GramParams S = P;
+  S.planes = P.planes + st0 * 64;  // records of stage st0 onwards (the row stride stays nstage)
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int ns = (int)P.nstage;
   if (diag)
-    e_loop<true>(P, lds, row0, col0, ns, acc);
+    e_loop<true>(S, lds, row0, col0, ns, acc);
   else
-    e_loop<false>(P, lds, row0, col0, ns, acc);
+    e_loop<false>(S, lds, row0, col0, ns, acc);
   if (P.flush && ns > P.flush) e_unflush(acc, P.fbuf + (size_t)blockIdx.x * WT * WT);
-  e_store(P, acc, row0, col0, diag);
+  if (P.splits == 1)
+    e_store(P, acc, row0, col0, diag);
+  else
+    e_partial(P, acc, split, ltile);
 }
 
 // The full-depth wide launches run k_gram3e (measured +3.5-8.5 % over k_gram3p on whole
@@ -1716,12 +1739,12 @@ static RangePlan plan_range(int64_t n, int64_t d, int64_t t0, int64_t t1, bool s
   rp.s0 = tri_start(r0, T2);
   rp.s1 = t1 == total ? tri_start(R, T2) : tri_start(r1, T2);
   rp.rem_count = 0;
-  // VISREPS_GRAM_WIDE_REM=1: the rows below R on the same kernel split over k (one
-  // generation, k_gram_reduce_w) instead of 128-tiles (run_split). Within noise at N = 10k
-  // (profiles/r3_gram_ab.log: +0.7-1.4 % on whole RDMs in alternating rounds, -2 % across
-  // two bench runs): the wide kernel's per-CU rate is spent on +16 % work (the diagonal
-  // super-tiles' lower quadrants), 220 of 256 CUs busy and the partial round trip.
-  static const bool wide_rem = getenv("VISREPS_GRAM_WIDE_REM") && strcmp(getenv("VISREPS_GRAM_WIDE_REM"), "1") == 0;
+  // The rows below R run on the wide kernel split over k (one generation, partials summed
+  // in split order by k_gram_reduce_w); VISREPS_GRAM_WIDE_REM=0 runs them as 128-tiles
+  // (run_split). With k_gram3e: +1.4 % on whole RDMs at D = 290,400, equal at 43,264
+  // (profiles/r3_gram_ab.log) -- the wide kernel's per-CU rate, less +16 % work (the
+  // diagonal super-tiles' lower quadrants), 220 of 256 CUs busy and the partial round trip.
+  static const bool wide_rem = !(getenv("VISREPS_GRAM_WIDE_REM") && strcmp(getenv("VISREPS_GRAM_WIDE_REM"), "0") == 0);
   if (t1 == total && !wide_rem) {
     rp.rem0 = trem;
     rp.rem_count = total - trem;
@@ -1981,7 +2004,10 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
       Rm.blk0 = b0;
       const int nb = std::min(gen, nblk - b0);
       KtScope kt(KT_GRAM_WIDE, 2.0 * (double)nb / Rm.splits * WT * WT * (double)d, st);
-      k_gram3p<<<(unsigned)nb, W_THREADS, 0, st>>>(Rm);
+      if (phased)
+        k_gram3e<<<(unsigned)nb, W_THREADS, 0, st>>>(Rm);
+      else
+        k_gram3p<<<(unsigned)nb, W_THREADS, 0, st>>>(Rm);
       VR_CHECK_LAUNCH();
     }
     if (Rm.splits > 1) {
