@@ -101,15 +101,12 @@ def extract_split(extractor: FeatureExtractor, images: torch.Tensor, batch: int,
             sel = {k: torch.empty((len(keep), v[0].numel()), dtype=torch.float32, device=dev) for k, v in feats.items()}
         b1 = min(n, b0 + batch)
         at = np.flatnonzero((keep >= b0) & (keep < b1))  # host-side: no device sync per batch
-        at_t = torch.as_tensor(at, dtype=torch.long, device=dev)
-        src_t = torch.as_tensor(keep[at] - b0, dtype=torch.long, device=dev)
         xs = {k: v.reshape(v.size(0), -1) for k, v in feats.items()}
         # every point of the batch in one launch (rows x points blocks: a batch's rows alone
         # would leave most CUs idle)
         K.split_rows_multi(list(xs.values()), correction, [out[k] for k in xs], b0)
-        if len(at):
-            for k, x in xs.items():
-                sel[k][at_t] = x[src_t].float()
+        # the batch's phase-1 selection rows of every point, one launch
+        K.gather_rows_multi(list(xs.values()), keep[at] - b0, at, [sel[k] for k in xs])
     return out, sel
 
 

@@ -287,6 +287,13 @@ int vr_rdm_split_rows_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, 
 int vr_rdm_split_rows_multi_f32(int npts, const float* const* X, const int64_t* d, const int64_t* ldx,
                                 int64_t rows, float correction, float* const* mean, float* const* stdv,
                                 uint16_t* const* planes, void* stream);
+/* Rows src[i] (host array, nrows entries) of every point's X[p] (row stride ldx[p], d[p]
+ * floats) to rows dst[i] of out[p] (row stride ldo[p]): one launch per 64 rows for all
+ * npts (<= 32) points. bench.extract_split keeps the phase-1 selection rows of each
+ * extraction batch with it (the rows `RandomState(42).choice` picks, evals.py:259-263). */
+int vr_gather_rows_multi_f32(int npts, const float* const* X, const int64_t* d, const int64_t* ldx,
+                             int nrows, const int32_t* src, const int32_t* dst, float* const* out,
+                             const int64_t* ldo, void* stream);
 size_t vr_rdm_planes_tiles_workspace(int64_t n, int64_t d, int64_t tile_begin, int64_t tile_end);
 int vr_rdm_pearson_tiles_planes(const uint16_t* planes, const float* mean, const float* stdv,
                                 int64_t n, int64_t d, float* rdm, int64_t ldr, float correction,

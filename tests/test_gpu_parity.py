@@ -411,16 +411,21 @@ def test_rdm_generation_tail_split(dev, mode, monkeypatch):
     assert torch.equal(tail, tail.T) and torch.all(torch.diagonal(tail) == 0)
 
 
-@pytest.mark.parametrize("wide", ["1", "0"])
-def test_rdm_wide_supertiles(dev, wide, monkeypatch):
-    # n = 6000: 24 x 25 / 2 = 300 super-tiles of 256; rows [0, 30 * 128) run on the wide
-    # 256 x 256 kernel (255 super-tiles = one generation), 128-tile rows 30..46 below on
-    # k_gram3 (generation + tail split). Both schemes against fp64; exact symmetry.
-    n, d = 6000, 1100
+@pytest.mark.parametrize("wide,kernel,d", [("1", "e", 1100), ("1", "p", 1100), ("0", "e", 1100),
+                                           ("1", "e", 40), ("1", "e", 9000), ("1", "p", 9000)])
+def test_rdm_wide_supertiles(dev, wide, kernel, d, monkeypatch):
+    # n = 6000: 24 x 25 / 2 = 300 super-tiles of 256; super-tile rows [0, 15) run on the wide
+    # kernel (255 super-tiles = one generation; k_gram3e, or k_gram3p with
+    # VISREPS_GRAM_KERNEL=p), the 45 super-tiles below on the wide kernel split over k
+    # (k_gram_reduce_w) -- the 128-tile rows on k_gram3 when the wide kernel is off. Depths:
+    # 35 stages (odd, a ragged last stage), 2 stages, 282 stages (one accumulator flush).
+    # Every scheme against fp64; exact symmetry.
+    n = 6000
     feats = O.synthetic_features(n, [d], seed=13, relu=[True])[0]
     x = torch.from_numpy(feats).to(dev)
     monkeypatch.setenv("VISREPS_GRAM", "split")
     monkeypatch.setenv("VISREPS_GRAM_WIDE", wide)
+    monkeypatch.setenv("VISREPS_GRAM_KERNEL", kernel)
     got = R.compute_rdm(x).double()
     xd = x.double()
     xd = xd - xd.mean(1, keepdim=True)

@@ -151,6 +151,8 @@ _PROTOTYPES = {
         ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, ctypes.c_float, _vp, _vp, _vp, _vp]),
     "vr_rdm_split_rows_multi_f32": (
         ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _c_i64, ctypes.c_float, _vp, _vp, _vp, _vp]),
+    "vr_gather_rows_multi_f32": (
+        ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     "vr_rdm_planes_tiles_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64]),
     "vr_rdm_pearson_tiles_planes": (
         ctypes.c_int,

@@ -2118,6 +2118,62 @@ int vr_rdm_split_rows_multi_f32(int npts, const float* const* X, const int64_t* 
   return VR_OK;
 }
 
+}  // extern "C"
+
+namespace vr {
+// Rows src[i] of every point's batch output X[p] -> rows dst[i] of out[p] (fp32), one
+// block per (row, point): the phase-1 selection rows kept during extraction, one launch per
+// batch instead of an index_put per point.
+constexpr int GATHER_MULTI_ROWS = 64;
+struct GatherMulti {
+  const float* X[SPLIT_MULTI_MAX];
+  float* out[SPLIT_MULTI_MAX];
+  int64_t d[SPLIT_MULTI_MAX];
+  int64_t ldx[SPLIT_MULTI_MAX];
+  int64_t ldo[SPLIT_MULTI_MAX];
+  int32_t src[GATHER_MULTI_ROWS];
+  int32_t dst[GATHER_MULTI_ROWS];
+};
+__global__ __launch_bounds__(256) void k_gather_rows_multi(GatherMulti G) {
+  const int i = blockIdx.x, p = blockIdx.y;
+  const float* x = G.X[p] + (int64_t)G.src[i] * G.ldx[p];
+  float* o = G.out[p] + (int64_t)G.dst[i] * G.ldo[p];
+  for (int64_t k = threadIdx.x; k < G.d[p]; k += blockDim.x) o[k] = x[k];
+}
+}  // namespace vr
+
+extern "C" {
+
+int vr_gather_rows_multi_f32(int npts, const float* const* X, const int64_t* d, const int64_t* ldx, int nrows,
+                             const int32_t* src, const int32_t* dst, float* const* out, const int64_t* ldo,
+                             void* stream) {
+  VR_REQUIRE(npts >= 0 && npts <= SPLIT_MULTI_MAX && nrows >= 0, "vr_gather_rows_multi_f32: npts=%d nrows=%d",
+             npts, nrows);
+  if (npts == 0 || nrows == 0) return VR_OK;
+  VR_REQUIRE(X && d && ldx && src && dst && out && ldo, "vr_gather_rows_multi_f32: null pointer");
+  for (int r0 = 0; r0 < nrows; r0 += GATHER_MULTI_ROWS) {
+    const int m = std::min(GATHER_MULTI_ROWS, nrows - r0);
+    GatherMulti G{};
+    for (int p = 0; p < npts; ++p) {
+      VR_REQUIRE(X[p] && out[p] && d[p] > 0 && ldx[p] >= d[p] && ldo[p] >= d[p],
+                 "vr_gather_rows_multi_f32: point %d: bad pointer or shape", p);
+      G.X[p] = X[p];
+      G.out[p] = out[p];
+      G.d[p] = d[p];
+      G.ldx[p] = ldx[p];
+      G.ldo[p] = ldo[p];
+    }
+    for (int i = 0; i < m; ++i) {
+      VR_REQUIRE(src[r0 + i] >= 0 && dst[r0 + i] >= 0, "vr_gather_rows_multi_f32: negative row");
+      G.src[i] = src[r0 + i];
+      G.dst[i] = dst[r0 + i];
+    }
+    k_gather_rows_multi<<<dim3((unsigned)m, (unsigned)npts), 256, 0, as_stream(stream)>>>(G);
+    VR_CHECK_LAUNCH();
+  }
+  return VR_OK;
+}
+
 int vr_rdm_split_rows_f32(const float* X, int64_t rows, int64_t d, int64_t ldx, float correction,
                           float* mean, float* stdv, uint16_t* planes, void* stream) {
   VR_REQUIRE(rows >= 0 && d > 0 && ldx >= d, "vr_rdm_split_rows_f32: bad shape rows=%lld d=%lld",

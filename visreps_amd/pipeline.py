@@ -220,6 +220,27 @@ class RdmKernels:
             stream_of(xs[0].device)), "vr_rdm_split_rows_multi_f32")
 
     @staticmethod
+    def gather_rows_multi(xs: Sequence[torch.Tensor], src, dst, outs: Sequence[torch.Tensor]) -> None:
+        """outs[p][dst[i]] = xs[p][src[i]] for every point p (host index lists; one launch,
+        vr_gather_rows_multi_f32)."""
+        import ctypes
+
+        k, m = len(xs), len(src)
+        if k == 0 or m == 0:
+            return
+        if any(x.dtype != torch.float32 or x.stride(1) != 1 for x in xs) or any(o.stride(1) != 1 for o in outs):
+            si = torch.as_tensor(np.asarray(src), dtype=torch.long, device=xs[0].device)
+            di = torch.as_tensor(np.asarray(dst), dtype=torch.long, device=xs[0].device)
+            for x, o in zip(xs, outs):
+                o[di] = x[si].float()
+            return
+        P64, I64, I32 = ctypes.c_void_p * k, ctypes.c_int64 * k, ctypes.c_int32 * m
+        check(lib().vr_gather_rows_multi_f32(
+            k, P64(*[x.data_ptr() for x in xs]), I64(*[x.size(1) for x in xs]), I64(*[x.stride(0) for x in xs]),
+            m, I32(*[int(v) for v in src]), I32(*[int(v) for v in dst]), P64(*[o.data_ptr() for o in outs]),
+            I64(*[o.stride(0) for o in outs]), stream_of(xs[0].device)), "vr_gather_rows_multi_f32")
+
+    @staticmethod
     def tiles_from_planes(sr: SplitRows, n: int, out: torch.Tensor, t0: int, t1: int, correction: float,
                           times: Optional[StepTimes] = None) -> None:
         """Gram tiles [t0, t1) from pre-split rows (vr_rdm_pearson_tiles_planes)."""
