@@ -2134,11 +2134,22 @@ struct GatherMulti {
   int32_t src[GATHER_MULTI_ROWS];
   int32_t dst[GATHER_MULTI_ROWS];
 };
+constexpr int GATHER_CHUNK = 8192;  // floats per block
 __global__ __launch_bounds__(256) void k_gather_rows_multi(GatherMulti G) {
-  const int i = blockIdx.x, p = blockIdx.y;
+  const int i = blockIdx.y, p = blockIdx.z;
+  const int64_t k0 = (int64_t)blockIdx.x * GATHER_CHUNK;
+  if (k0 >= G.d[p]) return;
+  const int64_t k1 = std::min<int64_t>(G.d[p], k0 + GATHER_CHUNK);
   const float* x = G.X[p] + (int64_t)G.src[i] * G.ldx[p];
   float* o = G.out[p] + (int64_t)G.dst[i] * G.ldo[p];
-  for (int64_t k = threadIdx.x; k < G.d[p]; k += blockDim.x) o[k] = x[k];
+  const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(o)) & 15) == 0 && (k1 - k0) % 4 == 0 &&
+                   k0 % 4 == 0;
+  if (vec) {
+    for (int64_t k = k0 + 4 * (int64_t)threadIdx.x; k < k1; k += 4 * (int64_t)blockDim.x)
+      *reinterpret_cast<f32x4*>(o + k) = *reinterpret_cast<const f32x4*>(x + k);
+  } else {
+    for (int64_t k = k0 + threadIdx.x; k < k1; k += blockDim.x) o[k] = x[k];
+  }
 }
 }  // namespace vr
 
@@ -2168,7 +2179,10 @@ int vr_gather_rows_multi_f32(int npts, const float* const* X, const int64_t* d, 
       G.src[i] = src[r0 + i];
       G.dst[i] = dst[r0 + i];
     }
-    k_gather_rows_multi<<<dim3((unsigned)m, (unsigned)npts), 256, 0, as_stream(stream)>>>(G);
+    int64_t dmax = 0;
+    for (int p = 0; p < npts; ++p) dmax = std::max<int64_t>(dmax, d[p]);
+    const unsigned chunks = (unsigned)((dmax + GATHER_CHUNK - 1) / GATHER_CHUNK);
+    k_gather_rows_multi<<<dim3(chunks, (unsigned)m, (unsigned)npts), 256, 0, as_stream(stream)>>>(G);
     VR_CHECK_LAUNCH();
   }
   return VR_OK;
