@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import functools
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -228,7 +229,8 @@ class RdmKernels:
         k, m = len(xs), len(src)
         if k == 0 or m == 0:
             return
-        if any(x.dtype != torch.float32 or x.stride(1) != 1 for x in xs) or any(o.stride(1) != 1 for o in outs):
+        if (any(x.dtype != torch.float32 or x.stride(1) != 1 for x in xs) or any(o.stride(1) != 1 for o in outs)
+                or os.environ.get("VISREPS_SEL_GATHER") == "torch"):  # (the latter: A/B timing)
             si = torch.as_tensor(np.asarray(src), dtype=torch.long, device=xs[0].device)
             di = torch.as_tensor(np.asarray(dst), dtype=torch.long, device=xs[0].device)
             for x, o in zip(xs, outs):
