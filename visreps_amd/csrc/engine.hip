@@ -74,6 +74,9 @@ constexpr int EST_STEP_BITS = 12;  // interpolation steps per interval: 2^12
 #ifndef VR_PROBE_WB
 #define VR_PROBE_WB 0
 #endif
+#ifndef VR_PROBE_WBA
+#define VR_PROBE_WBA 0  // the same for k_rankA
+#endif
 #ifndef VR_PROBE_ACC
 #define VR_PROBE_ACC 0
 #endif
@@ -600,7 +603,11 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
     uint32_t cd = (w0 + lane >= P0 && w0 + lane < P1) ? codes[w0 + lane] : 0u;
     uint32_t f0 = sload(gflag + (w0 >> 5)), f1 = sload(gflag + (w0 >> 5) + 1);
     for (; w0 < P1; w0 += 64) {
+#if VR_PROBE_WBA  // timing probe only (wrong scores): k_rankA without mask lookups / transposes
+      const uint64_t x = active ? (0xF7DFBEFDFBF7EFDFull ^ ((uint64_t)(cd & 7u) << 3)) : 0ull;
+#else
       const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+#endif
       uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
       asm volatile("" ::"v"(x) : "memory");
       if constexpr (EST) {
