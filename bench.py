@@ -466,14 +466,15 @@ def main():
             gpeak, gkern = FP32_MFMA_PEAK_TF, "k_gram (exact fp32, v_mfma_f32_32x32x2_f32)"
         else:  # 3 bf16 MFMA products per algorithmic FLOP: ceiling = bf16 dense peak / 3
             gpeak = round(BF16_MFMA_PEAK_TF / 3, 1)
-            gkern = ("k_gram3p / k_gram3 (centred rows split hi+lo bf16 by k_stats_split, 3 x "
-                     "v_mfma_f32_32x32x16_bf16 per k-step, fp32 accumulate; peak = bf16 dense peak / 3)")
+            gkern = ("k_gram3e / k_gram3 (centred rows split hi+lo bf16 by k_stats_split, 3 x "
+                     "bf16 MFMA per k-step -- v_mfma_f32_16x16x32_bf16 in the 256^2 super-tiles, "
+                     "32x32x16 in the 128^2 tiles -- fp32 accumulate; peak = bf16 dense peak / 3)")
         gw = kernels["k_gram_wide"]
         roof_gram = {"bound": "mfma", "achieved": round(gram_tf, 2), "peak": gpeak,
                      "unit": "TFLOP/s", "frac": round(gram_tf / gpeak, 4), "kernel": gkern,
                      "algorithmic_flops": "N(N+1)D per RDM (phase-1 selection RDMs included)",
                      "ms_per_step": round(times.gram_ms / args.steps, 2),
-                     "wide_kernel": {"name": "k_gram3p (256^2 super-tiles)", "ms_per_step": gw["ms_per_step"],
+                     "wide_kernel": {"name": ("k_gram3p" if os.environ.get("VISREPS_GRAM_KERNEL") == "p" else "k_gram3e") + " (256^2 super-tiles)", "ms_per_step": gw["ms_per_step"],
                                      "tflops_tile": gw["tflops"],
                                      "frac_tile": round(gw["tflops"] / gpeak, 4) if gw["tflops"] else None,
                                      "note": "tile FLOPs 2 d x 256^2 per block (diagonal super-tiles counted whole)"}}

@@ -470,3 +470,29 @@ def test_spearman_full_nan_and_constant(dev):
     b = a.clone()
     b[3, 7] = float("nan")
     assert np.isnan(R.spearman_full(a, b))
+
+
+# --------------------------------------------------------------------------- radix sort
+@pytest.mark.parametrize("m", [2, 4095, 4096, 4097, 100003, (1 << 20) + 17])
+@pytest.mark.parametrize("dist", ["uniform", "few", "equal", "top"])
+def test_sort_pairs_stable_vs_numpy(dev, m, dist):
+    """vr_sort_pairs_u32 (sort.hip) against numpy's stable argsort: ragged last tiles,
+    all-equal digits, few distinct keys (long same-digit runs inside one wave) and keys at
+    0xFFFFFFFF (the value the kernel's padding lanes carry). Bit-exact incl. value order."""
+    from visreps_amd.analysis.distributed_spearman import RankKernels
+    rs = np.random.RandomState(m % 1000 + len(dist))
+    if dist == "uniform":
+        k = rs.randint(0, 1 << 32, size=m, dtype=np.uint64).astype(np.uint32)
+    elif dist == "few":
+        k = rs.choice(np.array([0, 7, 0x01000100, 0xFFFFFFFF, 12345678], np.uint32), size=m)
+    elif dist == "equal":
+        k = np.full(m, 0x5A5A5A5A, np.uint32)
+    else:
+        k = (0xFFFFFFFF - rs.randint(0, 3, size=m)).astype(np.uint32)
+    v = np.arange(m, dtype=np.uint32)[::-1].copy()
+    kt = torch.from_numpy(k.view(np.int32)).to(dev)
+    vt = torch.from_numpy(v.view(np.int32)).to(dev)
+    ks, vs = RankKernels.sort(kt, vt)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(ks.cpu().numpy().view(np.uint32), k[order])
+    np.testing.assert_array_equal(vs.cpu().numpy().view(np.uint32), v[order])

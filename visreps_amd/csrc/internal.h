@@ -16,7 +16,10 @@ int scan_exclusive_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* t
 
 // ---- LSD radix sort of (uint32 key, uint32 value) pairs (sort.hip) -----------------
 constexpr int RS_BS = 256;
-constexpr int RS_IPT = 16;
+#ifndef VR_RS_IPT
+#define VR_RS_IPT 16
+#endif
+constexpr int RS_IPT = VR_RS_IPT;
 constexpr int RS_TILE = RS_BS * RS_IPT;
 size_t radix_ws_elems(int64_t n);  // uint32 elements of scratch (histograms + scan)
 // Sorts ascending by key, stable. keys/vals hold the result; *_alt are ping-pong

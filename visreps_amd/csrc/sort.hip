@@ -1,7 +1,10 @@
 // LSD radix sort of (uint32 key, uint32 value) pairs, 8-bit digits, 4 passes.
-// Per pass: tile histograms (digit-major) -> device-wide exclusive scan -> stable
-// scatter, where each 4096-element tile is first ordered by digit in LDS with eight
-// stable 1-bit splits, then written out digit-run by digit-run (coalesced).
+// Per pass: tile histograms (tile-major) -> exclusive scan in (digit, tile) order -> stable
+// scatter, where each 4096-element tile is first ordered by digit in LDS, then written
+// out digit-run by digit-run (coalesced). The in-tile order comes from wave ballots
+// (k_rs_scatter: each wave ranks its 1024 keys in rounds of 64 by the peer masks of
+// eight ballots, then per-wave digit totals place them); VR_RS_SPLIT8 builds the older
+// form, eight stable 1-bit splits over the tile.
 // Used once per RDM to order its strict upper triangle by value (the rank plan).
 #include "internal.h"
 
@@ -14,15 +17,207 @@ __global__ __launch_bounds__(RS_BS) void k_rs_hist(const uint32_t* __restrict__ 
   h[threadIdx.x] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+  if (base + RS_TILE <= n && (reinterpret_cast<uintptr_t>(keys) & 15) == 0) {
+    const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
+    uint4 q[RS_IPT / 4];
 #pragma unroll
-  for (int j = 0; j < RS_IPT; ++j) {
-    int64_t i = base + (int64_t)j * RS_BS + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    for (int j = 0; j < RS_IPT / 4; ++j) q[j] = k4[j * RS_BS + threadIdx.x];
+#pragma unroll
+    for (int j = 0; j < RS_IPT / 4; ++j) {
+      atomicAdd(&h[(q[j].x >> shift) & 255u], 1u);
+      atomicAdd(&h[(q[j].y >> shift) & 255u], 1u);
+      atomicAdd(&h[(q[j].z >> shift) & 255u], 1u);
+      atomicAdd(&h[(q[j].w >> shift) & 255u], 1u);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < RS_IPT; ++j) {
+      int64_t i = base + (int64_t)j * RS_BS + threadIdx.x;
+      if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    }
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+  hist[(int64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];  // tile-major: one 1-KB row
 }
 
+// Exclusive scan of the tile histograms in (digit, tile) order while they stay tile-major
+// ([tile][digit], so the big passes read and write coalesced 1-KB rows): per-chunk column
+// sums (k_rs_colsum), each digit's column of chunk sums scanned by its own block
+// (k_rs_colscan, which leaves the digit total), then every chunk adds the digit bases
+// (a block scan of the 256 totals) and writes its in-chunk column prefixes (k_rs_colapply).
+struct RsChunks {
+  int64_t ch;  // tiles per chunk
+  int64_t c;   // chunks (<= 1024)
+};
+static RsChunks rs_chunks(int64_t nb) {
+  int64_t ch = (nb + 1023) / 1024;
+  if (ch < 16) ch = 16;
+  return RsChunks{ch, (nb + ch - 1) / ch};
+}
+
+__global__ __launch_bounds__(256) void k_rs_colsum(const uint32_t* __restrict__ h, int64_t nb,
+                                                   int64_t ch, uint32_t* __restrict__ cs) {
+  const int d = threadIdx.x;
+  const int64_t t0 = (int64_t)blockIdx.x * ch;
+  const int64_t t1 = t0 + ch < nb ? t0 + ch : nb;
+  uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t t = t0;
+  for (; t + 8 <= t1; t += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += h[(t + u) * 256 + d];
+  }
+  for (; t < t1; ++t) acc[0] += h[t * 256 + d];
+  cs[(int64_t)blockIdx.x * 256 + d] =
+      acc[0] + acc[1] + acc[2] + acc[3] + acc[4] + acc[5] + acc[6] + acc[7];
+}
+
+// grid = 256 digits; block of 256 threads, each owning a run of up to 4 chunks
+__global__ __launch_bounds__(256) void k_rs_colscan(uint32_t* __restrict__ cs, int64_t c,
+                                                    uint32_t* __restrict__ total) {
+  __shared__ uint32_t scan_lds[256 / 64 + 1];
+  const int d = blockIdx.x, i = threadIdx.x;
+  uint32_t x[4], sum = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t q = (int64_t)i * 4 + u;
+    x[u] = q < c ? cs[q * 256 + d] : 0u;
+    sum += x[u];
+  }
+  uint32_t tot;
+  uint32_t acc = block_exclusive_scan<256>(sum, scan_lds, tot);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t q = (int64_t)i * 4 + u;
+    if (q < c) cs[q * 256 + d] = acc;
+    acc += x[u];
+  }
+  if (i == 0) total[d] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_rs_colapply(uint32_t* __restrict__ h, int64_t nb,
+                                                     int64_t ch, const uint32_t* __restrict__ cs,
+                                                     const uint32_t* __restrict__ total) {
+  __shared__ uint32_t scan_lds[256 / 64 + 1];
+  const int d = threadIdx.x;
+  uint32_t tot;
+  const uint32_t base = block_exclusive_scan<256>(total[d], scan_lds, tot);
+  const int64_t t0 = (int64_t)blockIdx.x * ch;
+  const int64_t t1 = t0 + ch < nb ? t0 + ch : nb;
+  uint32_t acc = base + cs[(int64_t)blockIdx.x * 256 + d];
+  int64_t t = t0;
+  for (; t + 8 <= t1; t += 8) {
+    uint32_t x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = h[(t + u) * 256 + d];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      h[(t + u) * 256 + d] = acc;
+      acc += x[u];
+    }
+  }
+  for (; t < t1; ++t) {
+    const uint32_t x = h[t * 256 + d];
+    h[t * 256 + d] = acc;
+    acc += x;
+  }
+}
+
+#ifndef VR_RS_SPLIT8
+#define VR_RS_SPLIT8 0
+#endif
+
+#if !VR_RS_SPLIT8
+// Each wave ranks its own 1024 consecutive keys in 16 rounds of 64 with no block barrier:
+// a key's rank among the same-digit keys of its round from the peer mask of eight
+// ballots, plus the wave's running count of that digit (wave-private LDS counters). The
+// block then needs two barriers: the per-wave digit totals give every key its slot in the
+// digit-ordered tile (digit start + same-digit keys of the waves before + wave rank).
+__global__ __launch_bounds__(RS_BS) void k_rs_scatter(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
+    const uint32_t* __restrict__ offs, int64_t nb) {
+  static_assert(RS_BS == 256, "one thread per digit");
+  constexpr int NW = RS_BS / 64, WT = RS_TILE / NW;  // waves, keys per wave
+  __shared__ uint32_t sk[RS_TILE];
+  __shared__ uint32_t sv[RS_TILE];
+  __shared__ uint32_t wcnt[NW][256];  // wave w's running (then total) count of digit d
+  __shared__ uint32_t start[256];
+  __shared__ uint32_t scan_lds[RS_BS / 64 + 1];
+
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+  const int64_t left = n - base;
+  const int nvalid = left < RS_TILE ? (int)left : RS_TILE;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) wcnt[q][t] = 0;
+  __syncthreads();
+  uint32_t kk[RS_IPT], vv[RS_IPT], rk[RS_IPT];
+#pragma unroll
+  for (int j = 0; j < RS_IPT; ++j) {
+    const int p = w * WT + j * 64 + lane;
+    kk[j] = 0xFFFFFFFFu;
+    vv[j] = 0;
+    if (p < nvalid) {
+      kk[j] = kin[base + p];
+      vv[j] = vin[base + p];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < RS_IPT; ++j) {
+    const bool valid = w * WT + j * 64 + lane < nvalid;
+    const uint32_t d = (kk[j] >> shift) & 255u;
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    // all lanes read before the leaders write (one wave: LDS ops complete in order)
+    const uint32_t before = wcnt[w][d];
+    rk[j] = before + r;
+    if (valid && r == 0) wcnt[w][d] = before + (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  {
+    uint32_t c = 0, tot;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) c += wcnt[q][t];
+    const uint32_t s0 = block_exclusive_scan<RS_BS>(c, scan_lds, tot);  // ends with a barrier
+    start[t] = s0;
+    uint32_t acc = s0;  // wcnt[q][t] becomes the slot of digit t's first key of wave q
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const uint32_t x = wcnt[q][t];
+      wcnt[q][t] = acc;
+      acc += x;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RS_IPT; ++j) {
+    if (w * WT + j * 64 + lane < nvalid) {
+      const uint32_t pos = wcnt[w][(kk[j] >> shift) & 255u] + rk[j];
+      sk[pos] = kk[j];
+      sv[pos] = vv[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RS_IPT; ++j) {
+    const int s = j * RS_BS + t;
+    if (s < nvalid) {
+      const uint32_t k = sk[s];
+      const uint32_t d = (k >> shift) & 255u;
+      const int64_t g = (int64_t)offs[(int64_t)blockIdx.x * 256 + d] + (uint32_t)s - start[d];
+      kout[g] = k;
+      vout[g] = sv[s];
+    }
+  }
+}
+#else
 __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
@@ -93,32 +288,37 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     uint32_t d = (k >> shift) & 255u;
     uint32_t r = (uint32_t)s - start[d];
     if (r < cnt[d]) {
-      int64_t g = (int64_t)offs[(int64_t)d * nb + blockIdx.x] + r;
+      int64_t g = (int64_t)offs[(int64_t)blockIdx.x * 256 + d] + r;
       kout[g] = k;
       vout[g] = sv[lds_pad(s)];
     }
   }
 }
+#endif
 
 size_t radix_ws_elems(int64_t n) {
   const int64_t nb = (n + RS_TILE - 1) / RS_TILE;
-  const int64_t h = 256 * nb;
-  return (size_t)(h + 64) + scan_ws_elems(h);
+  return (size_t)(256 * nb + 64) + (size_t)256 * rs_chunks(nb).c + 256;
 }
 
 int radix_sort_kv(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
                   int64_t n, uint32_t* ws, hipStream_t st) {
   if (n <= 1) return VR_OK;
   const int64_t nb = (n + RS_TILE - 1) / RS_TILE;
-  const int64_t h = 256 * nb;
+  const RsChunks C = rs_chunks(nb);
   uint32_t* hist = ws;
-  uint32_t* scan_ws = ws + h + 64;
+  uint32_t* cs = ws + 256 * nb + 64;
   uint32_t *ki = keys, *vi = vals, *ko = keys_alt, *vo = vals_alt;
   for (int pass = 0; pass < 4; ++pass) {
     const int shift = pass * 8;
     k_rs_hist<<<(unsigned)nb, RS_BS, 0, st>>>(ki, n, shift, hist, nb);
     VR_CHECK_LAUNCH();
-    VR_TRY(scan_exclusive_u32(hist, hist, h, nullptr, scan_ws, st));
+    k_rs_colsum<<<(unsigned)C.c, 256, 0, st>>>(hist, nb, C.ch, cs);
+    VR_CHECK_LAUNCH();
+    k_rs_colscan<<<256, 256, 0, st>>>(cs, C.c, cs + 256 * C.c);
+    VR_CHECK_LAUNCH();
+    k_rs_colapply<<<(unsigned)C.c, 256, 0, st>>>(hist, nb, C.ch, cs, cs + 256 * C.c);
+    VR_CHECK_LAUNCH();
     k_rs_scatter<<<(unsigned)nb, RS_BS, 0, st>>>(ki, vi, ko, vo, n, shift, hist, nb);
     VR_CHECK_LAUNCH();
     uint32_t* tk = ki; ki = ko; ko = tk;
