@@ -10,13 +10,30 @@
 
 namespace vr {
 
+#ifndef VR_RS_XCD
+#define VR_RS_XCD 1
+#endif
+// Tile of this block. With VR_RS_XCD the blocks one XCD receives (blockIdx % 8 equal, as
+// the dispatcher deals them) take consecutive tiles, so the digit runs that neighbouring
+// tiles write side by side meet in the same L2 instead of in eight.
+__device__ inline int64_t rs_tile(int64_t nb) {
+#if VR_RS_XCD
+  const int64_t b = blockIdx.x, x = b & 7, k = b >> 3, per = nb >> 3, rem = nb & 7;
+  return x * per + (x < rem ? x : rem) + k;
+#else
+  (void)nb;
+  return blockIdx.x;
+#endif
+}
+
 __global__ __launch_bounds__(RS_BS) void k_rs_hist(const uint32_t* __restrict__ keys,
                                                    int64_t n, int shift,
                                                    uint32_t* __restrict__ hist, int64_t nb) {
   __shared__ uint32_t h[256];
   h[threadIdx.x] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+  const int64_t tile = rs_tile(nb);
+  const int64_t base = tile * RS_TILE;
   if (base + RS_TILE <= n && (reinterpret_cast<uintptr_t>(keys) & 15) == 0) {
     const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
     uint4 q[RS_IPT / 4];
@@ -37,7 +54,7 @@ __global__ __launch_bounds__(RS_BS) void k_rs_hist(const uint32_t* __restrict__ 
     }
   }
   __syncthreads();
-  hist[(int64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];  // tile-major: one 1-KB row
+  hist[tile * 256 + threadIdx.x] = h[threadIdx.x];  // tile-major: one 1-KB row
 }
 
 // Exclusive scan of the tile histograms in (digit, tile) order while they stay tile-major
@@ -145,7 +162,8 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
   __shared__ uint32_t scan_lds[RS_BS / 64 + 1];
 
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+  const int64_t tile = rs_tile(nb);
+  const int64_t base = tile * RS_TILE;
   const int64_t left = n - base;
   const int nvalid = left < RS_TILE ? (int)left : RS_TILE;
 #pragma unroll
@@ -211,7 +229,7 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     if (s < nvalid) {
       const uint32_t k = sk[s];
       const uint32_t d = (k >> shift) & 255u;
-      const int64_t g = (int64_t)offs[(int64_t)blockIdx.x * 256 + d] + (uint32_t)s - start[d];
+      const int64_t g = (int64_t)offs[tile * 256 + d] + (uint32_t)s - start[d];
       kout[g] = k;
       vout[g] = sv[s];
     }
@@ -230,7 +248,8 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
   __shared__ uint32_t scan_lds[RS_BS / 64 + 1];
 
   const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * RS_TILE;
+  const int64_t tile = rs_tile(nb);
+  const int64_t base = tile * RS_TILE;
   cnt[t] = 0;
   __syncthreads();
 #pragma unroll
@@ -288,7 +307,7 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     uint32_t d = (k >> shift) & 255u;
     uint32_t r = (uint32_t)s - start[d];
     if (r < cnt[d]) {
-      int64_t g = (int64_t)offs[(int64_t)blockIdx.x * 256 + d] + r;
+      int64_t g = (int64_t)offs[tile * 256 + d] + r;
       kout[g] = k;
       vout[g] = sv[lds_pad(s)];
     }
