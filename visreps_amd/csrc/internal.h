@@ -21,6 +21,10 @@ constexpr int RS_BS = 256;
 #endif
 constexpr int RS_IPT = VR_RS_IPT;
 constexpr int RS_TILE = RS_BS * RS_IPT;
+// One LSD pass (8-bit digit at `shift`) of (ki, vi) into (ko, vo): the building block of
+// radix_sort_kv, also the engine's partition of (B position, A position) pairs.
+int radix_pass_kv(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, int64_t n,
+                  int shift, uint32_t* ws, hipStream_t st);
 size_t radix_ws_elems(int64_t n);  // uint32 elements of scratch (histograms + scan)
 // Sorts ascending by key, stable. keys/vals hold the result; *_alt are ping-pong
 // buffers of the same length.
@@ -59,6 +63,14 @@ __device__ inline uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds, uint3
 
 // Padded LDS index for tiles read both striped (lane-contiguous) and blocked (16
 // consecutive per thread): one pad dword per 32 keeps both patterns conflict-free.
+// Block -> work item for a 1-D grid of nb items such that the blocks one XCD receives
+// (blockIdx % 8 equal, as the dispatcher deals them) take consecutive items: neighbouring
+// items' partial-line writes then meet in one L2.
+__device__ inline int64_t xcd_item(int64_t nb) {
+  const int64_t b = blockIdx.x, x = b & 7, k = b >> 3, per = nb >> 3, rem = nb & 7;
+  return x * per + (x < rem ? x : rem) + k;
+}
+
 __device__ inline int lds_pad(int p) { return p + (p >> 5); }
 
 // Sortable transform of an fp32 value: ascending uint32 order == ascending float order,

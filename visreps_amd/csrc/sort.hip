@@ -13,13 +13,12 @@ namespace vr {
 #ifndef VR_RS_XCD
 #define VR_RS_XCD 1
 #endif
-// Tile of this block. With VR_RS_XCD the blocks one XCD receives (blockIdx % 8 equal, as
-// the dispatcher deals them) take consecutive tiles, so the digit runs that neighbouring
-// tiles write side by side meet in the same L2 instead of in eight.
+// Tile of this block. With VR_RS_XCD the blocks one XCD receives take consecutive tiles
+// (xcd_item), so the digit runs that neighbouring tiles write side by side meet in the
+// same L2 instead of in eight.
 __device__ inline int64_t rs_tile(int64_t nb) {
 #if VR_RS_XCD
-  const int64_t b = blockIdx.x, x = b & 7, k = b >> 3, per = nb >> 3, rem = nb & 7;
-  return x * per + (x < rem ? x : rem) + k;
+  return xcd_item(nb);
 #else
   (void)nb;
   return blockIdx.x;
@@ -320,26 +319,32 @@ size_t radix_ws_elems(int64_t n) {
   return (size_t)(256 * nb + 64) + (size_t)256 * rs_chunks(nb).c + 256;
 }
 
-int radix_sort_kv(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
-                  int64_t n, uint32_t* ws, hipStream_t st) {
-  if (n <= 1) return VR_OK;
+int radix_pass_kv(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, int64_t n,
+                  int shift, uint32_t* ws, hipStream_t st) {
+  if (n <= 0) return VR_OK;
   const int64_t nb = (n + RS_TILE - 1) / RS_TILE;
   const RsChunks C = rs_chunks(nb);
   uint32_t* hist = ws;
   uint32_t* cs = ws + 256 * nb + 64;
+  k_rs_hist<<<(unsigned)nb, RS_BS, 0, st>>>(ki, n, shift, hist, nb);
+  VR_CHECK_LAUNCH();
+  k_rs_colsum<<<(unsigned)C.c, 256, 0, st>>>(hist, nb, C.ch, cs);
+  VR_CHECK_LAUNCH();
+  k_rs_colscan<<<256, 256, 0, st>>>(cs, C.c, cs + 256 * C.c);
+  VR_CHECK_LAUNCH();
+  k_rs_colapply<<<(unsigned)C.c, 256, 0, st>>>(hist, nb, C.ch, cs, cs + 256 * C.c);
+  VR_CHECK_LAUNCH();
+  k_rs_scatter<<<(unsigned)nb, RS_BS, 0, st>>>(ki, vi, ko, vo, n, shift, hist, nb);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+int radix_sort_kv(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                  int64_t n, uint32_t* ws, hipStream_t st) {
+  if (n <= 1) return VR_OK;
   uint32_t *ki = keys, *vi = vals, *ko = keys_alt, *vo = vals_alt;
   for (int pass = 0; pass < 4; ++pass) {
-    const int shift = pass * 8;
-    k_rs_hist<<<(unsigned)nb, RS_BS, 0, st>>>(ki, n, shift, hist, nb);
-    VR_CHECK_LAUNCH();
-    k_rs_colsum<<<(unsigned)C.c, 256, 0, st>>>(hist, nb, C.ch, cs);
-    VR_CHECK_LAUNCH();
-    k_rs_colscan<<<256, 256, 0, st>>>(cs, C.c, cs + 256 * C.c);
-    VR_CHECK_LAUNCH();
-    k_rs_colapply<<<(unsigned)C.c, 256, 0, st>>>(hist, nb, C.ch, cs, cs + 256 * C.c);
-    VR_CHECK_LAUNCH();
-    k_rs_scatter<<<(unsigned)nb, RS_BS, 0, st>>>(ki, vi, ko, vo, n, shift, hist, nb);
-    VR_CHECK_LAUNCH();
+    VR_TRY(radix_pass_kv(ki, vi, ko, vo, n, pass * 8, ws, st));
     uint32_t* tk = ki; ki = ko; ko = tk;
     uint32_t* tv = vi; vi = vo; vo = tv;
   }
