@@ -53,6 +53,7 @@ from visreps_amd.dataloaders.synthetic import NSD_ROIS_4, make_images, make_resp
 from visreps_amd.models.custom_model import CustomCNN
 from visreps_amd.models.utils import FeatureExtractor
 from visreps_amd._lib import KTIMER_KERNELS, check, ktimer_enable, ktimer_read, lib, stream_of
+from visreps_amd.analysis._random import draw_bootstrap_indices
 from visreps_amd.pipeline import (KERNELS, PlanPrefetch, ShardedRDMs, StepTimes, all_units_rsa, engine_bytes,
                                   engine_call_bytes, engine_pair_bytes, make_schedule, phase1_rows, phase1_select)
 
@@ -349,9 +350,16 @@ def main():
     plan_stream = torch.cuda.Stream(device=dev) if prefetch else None
     _, _, keep = phase1_rows(N, 1000, 42, rank, world)
 
+    from concurrent.futures import ThreadPoolExecutor
+
+    draw_pool = ThreadPoolExecutor(1)
+
     def step(times: StepTimes):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
         ev[0].record()
+        # this step's bootstrap index sets, drawn on a host thread (the ctypes call releases
+        # the GIL) while the GPU extracts; all_units_rsa takes them when its units start
+        draw = draw_pool.submit(draw_bootstrap_indices, 42, N, int(0.9 * N), args.boot) if args.boot > 0 else None
         if split:  # the Gram prepass fused into extraction (bench.extract_split)
             feats, sel_rows = extract_split(extractor, images, args.batch, keep)
         else:
@@ -374,7 +382,8 @@ def main():
         del feats, rows, ex, sel_rows
         neural = {r: rd[("n", r)] for r in regions if ("n", r) in rd}
         res = all_units_rsa(lambda p: rd.pop(("m", p)), points, neural, N, n_boot=args.boot, seed=42, pg=pg,
-                            times=times, regions=regions, plans=pf.plans() if pf else None)
+                            times=times, regions=regions, plans=pf.plans() if pf else None,
+                            indices=draw.result if draw is not None else None)
         ev[4].record()
         times.phases(["extract", "phase1", "rdms", "units"], ev)
         return res, neural, sel

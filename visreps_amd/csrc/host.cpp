@@ -63,12 +63,19 @@ static void mt_seed(MTState* s, uint32_t seed) {
   s->pos = 624;
 }
 
+static inline uint32_t mt_twist(uint32_t a, uint32_t b, uint32_t c) {
+  const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+  return c ^ (y >> 1) ^ (0u - (y & 1u) & 0x9908b0dfu);
+}
+
+// the same recurrence as mt[i] = twist(mt[i], mt[(i+1) % 624], mt[(i+397) % 624]) in
+// order, split where the indices wrap so the loops carry no modulo
 static void mt_regen(MTState* s) {
   uint32_t* mt = s->mt;
-  for (int i = 0; i < 624; ++i) {
-    uint32_t y = (mt[i] & 0x80000000u) | (mt[(i + 1) % 624] & 0x7fffffffu);
-    mt[i] = mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-  }
+  int i = 0;
+  for (; i < 624 - 397; ++i) mt[i] = mt_twist(mt[i], mt[i + 1], mt[i + 397]);
+  for (; i < 623; ++i) mt[i] = mt_twist(mt[i], mt[i + 1], mt[i + 397 - 624]);
+  mt[623] = mt_twist(mt[623], mt[0], mt[396]);
   s->pos = 0;
 }
 

@@ -819,7 +819,8 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
                   seed: int = 42, pg=None, times: Optional[StepTimes] = None,
                   keep_plans: bool = False, plan_fn=None, unit_fn=None, group_fn=None,
                   regions: Optional[Sequence[str]] = None,
-                  plans: Optional[Dict[Tuple[str, str], R.RankPlan]] = None) -> Dict[Tuple[str, str], Dict]:
+                  plans: Optional[Dict[Tuple[str, str], R.RankPlan]] = None,
+                  indices: Optional[Callable[[], np.ndarray]] = None) -> Dict[Tuple[str, str], Dict]:
     """Point + bootstrap Spearman RSA for every (point, region) unit; returns the
     per-unit results on every rank.
 
@@ -849,8 +850,14 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
     if n_boot > 0 and mine:
         # RandomState(seed) is re-created per (region, subject) (evals.py:356), so every unit
         # draws the same (n_boot, k) index sets: drawn once per call (host MT19937), one upload
+        # indices(): the same draw started earlier by the caller (bench.py draws on a host
+        # thread from the start of the step, so the ~0.2 s of MT19937 overlaps GPU work
+        # even when a rank's queue is short, as at 8 GPUs)
         dev = neural_rdms[mine[0][1]].device
-        idx = torch.from_numpy(draw_bootstrap_indices(seed, n, k, n_boot)).to(dev)
+        drawn = indices() if indices is not None else draw_bootstrap_indices(seed, n, k, n_boot)
+        if drawn.shape != (n_boot, k):
+            raise ValueError(f"indices() gave {drawn.shape}, expected {(n_boot, k)}")
+        idx = torch.from_numpy(drawn).to(dev)
     local: Dict[Tuple[str, str], np.ndarray] = {}
     need = {p for p, _ in mine}
     mplans = {}
