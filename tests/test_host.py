@@ -64,6 +64,16 @@ def test_bootstrap_indices_cache_and_stream():
     assert not b.flags.writeable
 
 
+@pytest.mark.parametrize("n,k,draws", [(1024, 921, 20), (3001, 2700, 37), (10000, 9000, 40), (1500, 1, 9)])
+def test_draw_bootstrap_indices_threaded_path(n, k, draws):
+    """vr_legacy_choice splits many draws over threads (sequential accept/reject replay,
+    then permutations from the recorded generator states): bit-exact vs RandomState."""
+    from visreps_amd.analysis._random import draw_bootstrap_indices
+    rs = np.random.RandomState(42)
+    ref = np.stack([rs.choice(n, k, replace=False) for _ in range(draws)]).astype(np.int32)
+    np.testing.assert_array_equal(draw_bootstrap_indices(42, n, k, draws), ref)
+
+
 def test_choice_errors():
     from visreps_amd.analysis._random import LegacyRandomState
 

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -163,11 +164,61 @@ int vr_legacy_choice(uint32_t seed, int64_t n, int64_t k, int64_t n_draws, int32
   VR_REQUIRE(out != nullptr || n_draws == 0 || k == 0, "vr_legacy_choice: null out");
   MTState s;
   mt_seed(&s, seed);
-  std::vector<int32_t> perm((size_t)n);
-  for (int64_t d = 0; d < n_draws; ++d) {
-    mt_permutation(&s, n, perm.data());
-    if (k > 0) std::memcpy(out + d * k, perm.data(), (size_t)k * sizeof(int32_t));
+  const unsigned hw = std::thread::hardware_concurrency();
+  const int64_t nt = std::min<int64_t>({(int64_t)(hw ? hw : 1), 16, n_draws});
+  if (nt < 2 || n < 1024 || k == 0) {
+    std::vector<int32_t> perm((size_t)n);
+    for (int64_t d = 0; d < n_draws; ++d) {
+      mt_permutation(&s, n, perm.data());
+      if (k > 0) std::memcpy(out + d * k, perm.data(), (size_t)k * sizeof(int32_t));
+    }
+    return VR_OK;
   }
+  // Many draws: the stream is split at draw boundaries. A sequential pass replays only the
+  // bounded draws' accept/reject decisions (no shuffle; the accept test and the mask update
+  // are branch-free), recording the generator state at the start of every draw; threads
+  // then run the permutations from those states. Same outputs as the loop above.
+  std::vector<MTState> snap((size_t)n_draws);
+  for (int64_t d = 0; d < n_draws; ++d) {
+    snap[(size_t)d] = s;
+    uint32_t i = (uint32_t)(n - 1), mask = i;
+    mask |= mask >> 1;
+    mask |= mask >> 2;
+    mask |= mask >> 4;
+    mask |= mask >> 8;
+    mask |= mask >> 16;
+    uint32_t buf[624];
+    while (i >= 1) {
+      if (s.pos >= 624) mt_regen(&s);
+      const int m = 624 - s.pos;
+      for (int j = 0; j < m; ++j) {  // tempered outputs of the rest of this block
+        uint32_t y = s.mt[s.pos + j];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        buf[j] = y ^ (y >> 18);
+      }
+      int j = 0;
+      for (; j < m && i >= 1; ++j) {
+        const uint32_t acc = (buf[j] & mask) <= i;
+        i -= acc;
+        mask = i <= (mask >> 1) ? mask >> 1 : mask;
+      }
+      s.pos += j;
+    }
+  }
+  std::vector<std::thread> pool;
+  for (int64_t t = 0; t < nt; ++t) {
+    pool.emplace_back([&, t]() {
+      std::vector<int32_t> perm((size_t)n);
+      for (int64_t d = t; d < n_draws; d += nt) {
+        MTState local = snap[(size_t)d];
+        mt_permutation(&local, n, perm.data());
+        std::memcpy(out + d * k, perm.data(), (size_t)k * sizeof(int32_t));
+      }
+    });
+  }
+  for (auto& th : pool) th.join();
   return VR_OK;
 }
 
