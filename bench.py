@@ -182,6 +182,7 @@ def structured_est_probe(n: int, plan_b, dev) -> dict:
     idx = bootstrap_indices(42, n, int(0.9 * n), 1000)
     L = lib()
     out = {}
+    all_scores = {}
     for form, env in (("est", None), ("exact", "0")):
         old = os.environ.get("VISREPS_ENGINE_EST")
         if env is None:
@@ -199,13 +200,16 @@ def structured_est_probe(n: int, plan_b, dev) -> dict:
             torch.cuda.synchronize()
             out[form] = {"unit_ms": round(e0.elapsed_time(e1), 2), "reruns": int(L.vr_engine_est_reruns()) - r0,
                          "point": float(sc[0, 0])}
+            all_scores[form] = sc.cpu().numpy()
         finally:
             if old is None:
                 os.environ.pop("VISREPS_ENGINE_EST", None)
             else:
                 os.environ["VISREPS_ENGINE_EST"] = old
     out["passes"] = -(-1001 // 64)
-    out["scores_equal"] = out["est"]["point"] == out["exact"]["point"]
+    # every one of the 1001 scores (point + 1000 bootstraps), bit for bit
+    out["scores_equal"] = bool(np.array_equal(all_scores["est"], all_scores["exact"]))
+    out["scores_compared"] = int(all_scores["est"].size)
     out["note"] = ("neural RDM d_ab = u_a + u_b + 0.05 noise, u ~ Exp(1)^2, vs the V1 neural plan of the bench: "
                    "EST passes the A side flags are re-run exact (est.reruns); exact = VISREPS_ENGINE_EST=0")
     return out
@@ -523,6 +527,10 @@ def main():
                                   "projecting every row and selecting, as the reference does), selection RDMs, "
                                   "14x4 Spearmans"),
                        "index_draws": "RandomState(42) 1000 x choice(N, 0.9N) drawn inside every step",
+                       "inputs": ("ImageNet-normalised 224x224 float32 images already resident in HBM: the "
+                                  "get_transform leg (Resize/CenterCrop/Normalize, vr_transform_u8) and the "
+                                  "DataLoader's per-batch H2D copy (visreps/models/utils.py:338) are outside "
+                                  "the timed step"),
                        "parallelism": (f"stimulus-sharded extraction; RDMs by owner ranks (rows all_to_all to the "
                                        f"owners, packed tiles to the consumers); units/{world} ranks")},
             "roofline": roof,

@@ -35,6 +35,7 @@ extern "C" {
 #define VR_EINVAL (-1)    /* invalid argument (shape, pointer, size) */
 #define VR_EHIP (-2)      /* HIP runtime error */
 #define VR_EWORKSPACE (-3) /* workspace smaller than the *_workspace() query */
+#define VR_EINTERNAL (-4)  /* an exact-arithmetic invariant of the result failed (a bug) */
 
 /* Library version (major*10000 + minor*100 + patch). */
 int vr_version(void);
@@ -183,10 +184,13 @@ int vr_bootstrap_spearman_multi(const void* plan_a, const void* const* planBs, i
                                 size_t ws_bytes, void* stream);
 
 /* Passes of the bootstrap engines run in a one-gather-per-pair form (absolute ranks kept
- * modulo 2^16 and recovered against an interpolated count table). A pass whose ranks the
- * table cannot recover (very large tie groups, adversarial orders) is re-run in the
- * exact chunk-base form; this counter is the number of such re-runs in the process so
- * far (scores never depend on it). VISREPS_ENGINE_EST=0 forces the chunk-base form. */
+ * modulo 2^16 and recovered against a count estimate). A pass whose ranks the estimate
+ * cannot recover (very large tie groups, adversarial orders) -- flagged by the A walk's
+ * window checks, or by the tail's invariants (B-side included pairs == M', sum of the
+ * gathered A ranks == M'(M'+1)) -- is re-run in the exact chunk-base form; this counter is
+ * the number of such re-runs in the process so far (scores never depend on it).
+ * VISREPS_ENGINE_EST=0 forces the chunk-base form; an exact-form pass that breaks the
+ * invariants fails the call with VR_EINTERNAL. */
 int64_t vr_engine_est_reruns(void);
 
 // Kernel-level HIP-event timing of the hot kernels, for pricing the dominant kernel against

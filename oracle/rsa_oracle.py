@@ -146,6 +146,25 @@ def bootstrap_rsa(model_rdm, neural_rdm, n_bootstrap: int = 1000, seed: int = 42
             float(np.percentile(scores, 97.5)))
 
 
+def bootstrap_scores_at(model_rdm, neural_rdm, draws, seed: int = 42, method: str = "Spearman"):
+    """Scores of selected bootstrap draws of evals.py:355-369 (0-based draw numbers): the
+    RandomState(seed) stream is drawn in full up to the last one, as the reference loop
+    does, but only the listed draws' sub-RDMs are scored (a full-size check of late draws
+    without the ~2 h of all 1000 Spearmans). Returns {draw: score}."""
+    model_rdm = np.asarray(model_rdm)
+    neural_rdm = np.asarray(neural_rdm)
+    want = set(int(d) for d in draws)
+    rng = np.random.RandomState(seed)
+    n = neural_rdm.shape[0]
+    k = int(n * 0.9)
+    out = {}
+    for i in range(max(want) + 1):
+        idx = rng.choice(n, size=k, replace=False)
+        if i in want:
+            out[i] = compute_rdm_correlation(model_rdm[idx][:, idx], neural_rdm[idx][:, idx], correlation=method)
+    return out
+
+
 def compute_rsa(cfg: Dict, sel_acts: Dict[str, np.ndarray], sel_neural: np.ndarray,
                 eval_acts: Dict[str, np.ndarray], eval_neural: np.ndarray,
                 n_select: Optional[int] = None, bootstrap: bool = True,

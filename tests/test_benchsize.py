@@ -242,44 +242,109 @@ def test_bench_point_split_gram_parity(dev, bench, idx, point):
 
 
 ORACLE_POINTS = ["conv2_post", "conv5_post", "fc1_post"]
+# 0-based draws scored by the oracle beyond the first 5: bootstraps #64, #65, #500, #1000.
+# With the full set in lane 0 of pass 0, draws 0-62 run in pass 0 (EST 4) and draws 63-999
+# in the EST 3 passes -- the k_rankB form behind 840 of the step's 952 B walks.
+LATE_DRAWS = [63, 64, 499, 999]
 
 
 @pytest.mark.parametrize("point", ORACLE_POINTS)
 def test_bench_point_vs_cpu_oracle(dev, bench, point):
-    """Full-size parity against the CPU oracle itself: the product's default
-    path (split-Gram RDMs on the GPU, rank-plan engine) for the point Spearman and the first
-    5 bootstraps of RandomState(42) vs O.bootstrap_rsa(O.compute_rdm(x), O.compute_rdm(y),
-    5, 42) -- numpy float32 RDMs and scipy.stats.spearmanr, the reference's arithmetic
+    """Full-size parity against the CPU oracle itself: the product's
+    default path (split-Gram RDMs on the GPU, rank-plan engine, 1000 bootstraps in one call
+    as the bench runs them) for the point Spearman, the first 5 bootstraps of
+    RandomState(42) and bootstraps #64/#65/#500/#1000 (EST 3 passes) vs the oracle --
+    numpy float32 RDMs and scipy.stats.spearmanr, the reference's arithmetic
     (rsa.py:59-129, evals.py:341-373) -- on the bench's own N = 10k features."""
+    from visreps_amd._lib import lib
+
     feats = bench[0]
     x = feats[point]
     gm = R.compute_rdm(x)
     gn = R.compute_rdm(bench[4])
-    point_g, scores_g, _, _ = R.bootstrap_rsa(gm, gn, n_bootstrap=5, seed=42)
+    r0 = int(lib().vr_engine_est_reruns())
+    point_g, scores_g, _, _ = R.bootstrap_rsa(gm, gn, n_bootstrap=NB, seed=42)
+    reruns = int(lib().vr_engine_est_reruns()) - r0
     del gm, gn
     torch.cuda.empty_cache()
-    point_o, scores_o = _oracle_results(bench)[point].result()
+    point_o, scores_o, late_o = _oracle_results(bench)[point].result()
     dp = abs(point_g - point_o)
-    db = float(np.max(np.abs(np.asarray(scores_g) - scores_o)))
+    db = float(np.max(np.abs(np.asarray(scores_g[:5]) - scores_o)))
+    dl = max(abs(float(scores_g[i]) - late_o[i]) for i in LATE_DRAWS)
     record_margin("bench_point_vs_cpu_oracle", point=point, d=x.size(1), point_hip=point_g, point_oracle=point_o,
-                  dspearman_point=dp, dspearman_boot5=db)
-    assert dp < SPEARMAN_TOL and db < SPEARMAN_TOL, (point, dp, db)
+                  dspearman_point=dp, dspearman_boot5=db, dspearman_late_draws=dl, late_draws=LATE_DRAWS,
+                  est_reruns=reruns)
+    assert dp < SPEARMAN_TOL and db < SPEARMAN_TOL and dl < SPEARMAN_TOL, (point, dp, db, dl)
+
+
+class _engine_form:
+    def __init__(self, value):
+        self.value = value
+
+    def __enter__(self):
+        self.old = os.environ.get("VISREPS_ENGINE_EST")
+        os.environ["VISREPS_ENGINE_EST"] = self.value
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("VISREPS_ENGINE_EST", None)
+        else:
+            os.environ["VISREPS_ENGINE_EST"] = self.old
+
+
+def structured_rdm(dev, n, seed=7):
+    """A neural RDM with strong per-stimulus effects (d_ab = u_a + u_b + 0.05 noise, u ~
+    Exp(1)^2): bench.structured_est_probe's RDM, where the wave-uniform EST 3 estimate
+    drifts furthest from the subsets' true counts."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    u = torch.empty(n, device=dev).exponential_(1.0, generator=g) ** 2
+    a = u[:, None] + u[None, :] + 0.05 * torch.rand(n, n, device=dev, generator=g)
+    a = torch.triu(a, 1)
+    return a + a.T
+
+
+def test_bench_unit_est_equals_exact_form(dev, bench, idx):
+    """at N = 10k, all 1001 scores of bench units (conv5_post and conv1_post
+    x V1) and of the structured neural RDM against conv5_post are bit-equal between the
+    default EST form (whatever it flags and re-runs) and VISREPS_ENGINE_EST=0 (every pass in
+    the exact chunk-base form)."""
+    from visreps_amd._lib import lib
+
+    feats, neural_split = bench[0], bench[1]
+    pn = R.RankPlan(neural_split)
+    pms = [R.RankPlan(R.compute_rdm(feats[p])) for p in ("conv5_post", "conv1_post")]
+    ps = R.RankPlan(structured_rdm(dev, N))
+    out = {}
+    for form in ("1", "0"):
+        with _engine_form(form):
+            r0 = int(lib().vr_engine_est_reruns())
+            units = R.bootstrap_spearman_multi(pn, pms, idx, full_first=True).cpu().numpy()
+            st = R.bootstrap_spearman(pms[0], ps, idx, full_first=True).cpu().numpy()
+            out[form] = (units, st, int(lib().vr_engine_est_reruns()) - r0)
+    (u_est, s_est, reruns), (u_ex, s_ex, _) = out["1"], out["0"]
+    record_margin("bench_unit_est_vs_exact", n_scores=int(u_est.size + s_est.size), est_reruns=reruns,
+                  units_equal=bool(np.array_equal(u_est, u_ex)), structured_equal=bool(np.array_equal(s_est, s_ex)))
+    assert u_est.shape == (2, NB + 1) and np.all(np.isfinite(u_est)) and np.all(np.isfinite(s_est))
+    assert np.array_equal(u_est, u_ex)
+    assert np.array_equal(s_est, s_ex)
 
 
 _ORACLE_RUNS = {}
 
 
 def _oracle_results(bench):
-    """The three points' oracle runs (numpy RDMs + scipy Spearmans, ~40 s each on the host)
-    started together on threads at first use (numpy's sorts and BLAS release the GIL), so
-    the three tests cost about one oracle run of wall time."""
+    """The three points' oracle runs (numpy RDMs + 10 scipy Spearmans at N = 10k / k = 9000,
+    ~80 s each on the host) started together on threads at first use (numpy's sorts and BLAS
+    release the GIL), so the three tests cost about one oracle run of wall time."""
     if not _ORACLE_RUNS:
         from concurrent.futures import ThreadPoolExecutor
         on = O.compute_rdm(bench[4].cpu().numpy())
         xs = {p: bench[0][p].cpu().numpy() for p in ORACLE_POINTS}
 
         def run(p):
-            return O.bootstrap_rsa(O.compute_rdm(xs[p]), on, n_bootstrap=5, seed=42)[:2]
+            om = O.compute_rdm(xs[p])
+            point, boot5 = O.bootstrap_rsa(om, on, n_bootstrap=5, seed=42)[:2]
+            return point, boot5, O.bootstrap_scores_at(om, on, LATE_DRAWS, seed=42)
 
         pool = ThreadPoolExecutor(len(ORACLE_POINTS))
         _ORACLE_RUNS.update({p: pool.submit(run, p) for p in ORACLE_POINTS})

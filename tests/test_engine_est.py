@@ -137,6 +137,57 @@ def test_est_modes_equal_exact_form(dev, mode, monkeypatch):
     assert np.array_equal(est, ref)
 
 
+def test_half_tied_rdm_exact_join_is_fast(dev):
+    # One tie group over half the 12.5 M pairs (n = 5000): it spans ~1000 of the exact
+    # form's group-aligned chunks, so the join's chunk lookup must be a binary search
+    # (the old one-chunk-per-step walk made this join take seconds). Exact and
+    # EST forms must agree and the call must stay fast.
+    import time
+
+    n = 5000
+    g = torch.Generator(device=dev).manual_seed(51)
+    a = torch.rand(n, n, device=dev, generator=g)
+    a = torch.where(torch.rand(n, n, device=dev, generator=g) < 0.5, torch.full_like(a, 0.5), a)
+    a = torch.triu(a, 1)
+    a = a + a.T
+    b = _rdm(dev, n, 100, 52)
+    idx = bootstrap_indices(42, n, int(0.9 * n), 127)
+    pa, pb = R.RankPlan(a), R.RankPlan(b)
+    with exact_engine():
+        R.bootstrap_spearman(pa, pb, idx[:2], full_first=True)  # warm
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        ref = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+        dt = time.perf_counter() - t
+    est = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    assert np.array_equal(est, ref)
+    assert dt < 2.0, f"exact-form call with a half-triangle tie group took {dt:.2f}s"
+    an = a.cpu().numpy()
+    assert abs(ref[0] - O.compute_rdm_correlation(an, b.cpu().numpy(), "Spearman")) <= 1e-12
+
+
+@pytest.mark.parametrize("inject", [0, 2])
+def test_b_side_error_is_flagged_and_rerun(dev, monkeypatch, inject):
+    # A B-side recovery error is invisible to the A walk's window checks. Inject one (lanes
+    # 1..63 of one TB row off by one after the A walk of EST pass `inject`): the tail's
+    # invariants (sum of the gathered A ranks == M'(M'+1), B-side included pairs == M')
+    # must flag the pass, the exact re-run must restore every score bit for bit. Pass 0
+    # flagged makes the call give up on the estimate (every later pass exact).
+    n, nb = 2000, 250
+    a, b = _rdm(dev, n, 64, 41, relu=True), _rdm(dev, n, 300, 42)
+    idx = bootstrap_indices(42, n, int(0.9 * n), nb)
+    pa, pb = R.RankPlan(a), R.RankPlan(b)
+    clean = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    monkeypatch.setenv("VISREPS_ENGINE_INJECT", str(inject))
+    r0 = int(lib().vr_engine_est_reruns())
+    got = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    reruns = int(lib().vr_engine_est_reruns()) - r0
+    assert reruns >= 1, "the injected B-side error must flag its pass"
+    assert np.array_equal(got, clean)
+    with exact_engine():
+        assert np.array_equal(R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy(), clean)
+
+
 def test_est_strong_stimulus_structure_equals_exact_form(dev):
     # Continuous RDMs with a strong per-stimulus effect (d_ab = u_a + u_b + noise, u heavy-
     # tailed): the included-pair count of a subset drifts far from the uniform estimate along

@@ -174,6 +174,8 @@ def main(argv=None):
     ap.add_argument("--output", default=None)
     ap.add_argument("--n_components", type=int, default=20)
     ap.add_argument("--batch_size", type=int, default=10000)
+    ap.add_argument("--normalize_signs", action="store_true",
+                    help="largest-|.| component positive (reproducible across solvers); default: raw solver signs")
     a = ap.parse_args(argv)
     feats = a.features or f"datasets/obj_cls/imagenet/features_{a.model_name}.npz"
     out = a.output or f"datasets/obj_cls/imagenet/eigenvectors_{a.model_name}.npz"
@@ -182,8 +184,13 @@ def main(argv=None):
     data = np.load(feats)  # allow_pickle stays False: features are a plain float32 array
     features = data[f"{a.model_name}_features"]
     print(f"Features shape: {features.shape}")
-    comps, vals, mean, total = batched_pca(features, a.n_components, a.batch_size)
-    np.savez(out, eigenvectors=comps, eigenvalues=vals, mean=mean, total_variance=total)
+    comps, vals, mean, total = batched_pca(features, a.n_components, a.batch_size, normalize_signs=a.normalize_signs)
+    # the sign convention travels with the vectors: the coarse labels flip with a component's
+    # sign, so a label set is reproducible only together with this field (extra key; the
+    # reference's four keys are unchanged)
+    sign = "largest_abs_positive" if a.normalize_signs else f"raw:rocsolver-syevd torch {torch.__version__}"
+    np.savez(out, eigenvectors=comps, eigenvalues=vals, mean=mean, total_variance=total,
+             sign_convention=np.array(sign))
     print(f"Eigenvectors saved to {out}")
     print(f"Variance explained by top 6: {(vals[:6].sum() / total) * 100:.2f}%")
 

@@ -184,7 +184,8 @@ struct EngineWs {
   uint32_t* c0rel;      // [EST_NC][64]     EST: that count relative to its segment
   uint32_t* c0seg;      // [EST_NC]         EST: the segment holding each boundary
   uint2* ftab;          // [EST_NC][64]     EST: {L_c, D_c} per interval (window low end, step)
-  uint32_t* viol;       // [EST_MAX_PASSES] EST: pass flagged for the exact re-run
+  uint32_t* viol;       // [EST_MAX_PASSES] EST: pass flagged for the exact re-run;
+                        // [EST_MAX_PASSES]: an exact-form pass broke the tail invariants
 };
 
 constexpr int EST_MAX_PASSES = 512;  // passes between two checks of the EST flags
@@ -198,7 +199,7 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
   e.c0rel = c.take<uint32_t>((size_t)EST_NC * LANES);
   e.c0seg = c.take<uint32_t>((size_t)EST_NC);
   e.ftab = c.take<uint2>((size_t)EST_NC * LANES);
-  e.viol = c.take<uint32_t>((size_t)EST_MAX_PASSES);
+  e.viol = c.take<uint32_t>((size_t)EST_MAX_PASSES + 1);  // + the exact form's invariant flag
   e.masks = c.take<uint64_t>((size_t)n);
   e.posA_byB = c.take<uint32_t>((size_t)M);
   e.chunkA_byB = c.take<uint32_t>((size_t)M);
@@ -228,8 +229,9 @@ enum { JOIN_NONE = 0, JOIN_CHUNK = 1, JOIN_LO = 2 };
 // Every join gathers the 4-B A positions (posMapA), a table the MALL can keep across the
 // joins of one A plan. JOIN_CHUNK also needs the A chunk of the position: chunks are
 // group-aligned, chunk c starting at the first group start >= c L, so the chunk of a
-// position is the last c <= pos / L whose start is <= pos -- one step down per chunk a
-// tie group spans (the exact form is the rare path: VISREPS_ENGINE_EST=0, flagged passes).
+// position is the last c <= pos / L whose start is <= pos. Chunk starts are non-decreasing
+// in c, so that is a binary search (log2 of the chunks a tie group spans, not one step per
+// chunk: a tie group over half the pairs spans thousands of chunks).
 __global__ void k_join(const uint32_t* __restrict__ codesB, int64_t M, int64_t n,
                        const uint32_t* __restrict__ gstartA, const uint32_t* __restrict__ chunk_gA,
                        uint32_t L, uint32_t nchA, const uint32_t* __restrict__ posMapA,
@@ -241,8 +243,19 @@ __global__ void k_join(const uint32_t* __restrict__ codesB, int64_t M, int64_t n
   const uint64_t t = tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n);
   const uint32_t pa = posMapA[t];
   if (mode == JOIN_CHUNK) {
-    uint32_t c = min(pa / L, nchA - 1u);
-    while (c > 0 && gstartA[chunk_gA[c]] > pa) --c;
+    uint32_t hi = min(pa / L, nchA - 1u);
+    uint32_t c = hi;
+    if (gstartA[chunk_gA[hi]] > pa) {  // the last c in [0, hi) with start <= pa (chunk 0 starts at 0)
+      uint32_t lo = 0;                 // invariant: start(lo) <= pa < start(hi)
+      while (hi - lo > 1) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (gstartA[chunk_gA[mid]] <= pa)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      c = lo;
+    }
     posA_byB[i] = pa;
     second[i] = c;
     return;
@@ -1261,14 +1274,19 @@ __global__ __launch_bounds__(1024) void k_tail_part(
 //   sum y = M'(M'+1),  mu = M'(M'+1)^2,
 //   sum k y^2 = 4 M'(M'+1)(2M'+1)/6 - sum_g (k^3 - k)/3   (untied squares minus tie spread)
 // nan_units bit u: unit u's B plan has a NaN (so does every unit when a_nan).
+// Invariants (free: both sums are already here): the B walk's included-pair count P equals
+// the A walk's M', and the sum of the yA it gathered equals sum y = M'(M'+1). A B-side
+// recovery error (a wrong 2^16 window, a corrupted TB row) moves S and sets *viol, so the
+// pass is re-run in the exact form (EST) or the call fails (exact form) -- never a silent
+// wrong score.
 __global__ void k_tail_top(const uint64_t* __restrict__ fpart0, uint32_t nblk,
                            const uint32_t* __restrict__ totA, int a_nan, uint64_t nan_units, int nl,
-                           double* __restrict__ scores0, int64_t score_ld) {
+                           double* __restrict__ scores0, int64_t score_ld, uint32_t* __restrict__ viol) {
   const int lane = threadIdx.x;
   const uint32_t u = blockIdx.x;
   const uint64_t* fpart = fpart0 + (size_t)u * nblk * FP_N * LANES;
   u128 tA = 0, tB = 0, ab = 0;
-  uint64_t P = 0;
+  uint64_t P = 0, Ssum = 0;
   // unrolled so the loads of several partial blocks are in flight at once (the loop is
   // otherwise one L2 round trip per block)
 #pragma unroll 8
@@ -1278,7 +1296,12 @@ __global__ void k_tail_top(const uint64_t* __restrict__ fpart0, uint32_t nblk,
     tB += ((u128)f[3 * LANES] << 64) | f[2 * LANES];
     ab += (((u128)f[5 * LANES] << 64) | f[4 * LANES]) + 2 * (u128)P * f[7 * LANES];
     P += f[6 * LANES];
+    Ssum += f[7 * LANES];
   }
+  const bool forced_nan = a_nan || ((nan_units >> u) & 1ull);
+  const bool broken = lane < nl && !forced_nan &&
+                      (P != (uint64_t)totA[lane] || Ssum != (uint64_t)totA[lane] * ((uint64_t)totA[lane] + 1u));
+  if (__ballot(broken) != 0 && lane == 0) *viol = 1u;  // every writer stores 1
   if (lane >= nl) return;
   const u128 Mp = totA[lane];
   const u128 mu = Mp * (Mp + 1) * (Mp + 1);
@@ -1287,7 +1310,7 @@ __global__ void k_tail_top(const uint64_t* __restrict__ fpart0, uint32_t nblk,
   const i128 va = (i128)(sq - tA / 3) - (i128)mu;
   const i128 vb = (i128)(sq - tB / 3) - (i128)mu;
   double r;
-  if (a_nan || ((nan_units >> u) & 1ull) || Mp < 2 || va <= 0 || vb <= 0) {
+  if (forced_nan || Mp < 2 || va <= 0 || vb <= 0) {
     r = __builtin_nan("");
   } else {
     r = i128_to_f64(num) / sqrt(i128_to_f64(va) * i128_to_f64(vb));
@@ -1406,9 +1429,10 @@ static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* c
 }
 
 // Tail of a pass for units [0, nb) (their B walks done): the nl scores of each, unit j's at
-// scores + j * score_ld. nan_b[j]: unit j's B plan holds a NaN.
+// scores + j * score_ld. nan_b[j]: unit j's B plan holds a NaN. *viol <- 1 when a unit's
+// sums break the invariants (k_tail_top).
 static int tail_units(const EngineWs& E, int64_t nb, uint32_t nseg, bool a_nan, const std::vector<char>& nan_b,
-                      int nl, double* scores, int64_t score_ld, hipStream_t st) {
+                      int nl, double* scores, int64_t score_ld, uint32_t* viol, hipStream_t st) {
   const uint32_t nsb = scan_blocks(nseg);
   for (int64_t u0 = 0; u0 < nb; u0 += 64) {  // 64 units per launch (the NaN bitmask)
     const int64_t cnt = std::min<int64_t>(64, nb - u0);
@@ -1420,7 +1444,7 @@ static int tail_units(const EngineWs& E, int64_t nb, uint32_t nseg, bool a_nan, 
                                                             E.segB_tot + us, nseg, E.useg, E.fpart);
     VR_CHECK_LAUNCH();
     k_tail_top<<<(unsigned)cnt, LANES, 0, st>>>(E.fpart, nsb, E.totA, a_nan ? 1 : 0, nan_units, nl,
-                                                scores + u0 * score_ld, score_ld);
+                                                scores + u0 * score_ld, score_ld, viol);
     VR_CHECK_LAUNCH();
   }
   return VR_OK;
@@ -1451,11 +1475,22 @@ static int with_pass_tag(bool lds, bool full, bool narrow, Fn&& fn) {
 // full_first), 64 per pass. joins: nb pairs of M-element (posA_byB, chunkA_byB) arrays.
 // Passes run in the EST form; the few it flags (and every pass, with VISREPS_ENGINE_EST=0)
 // run in the exact chunk-base form, which needs the chunkA joins too.
-static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, int64_t n,
-                            const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
-                            double* scores, int64_t score_ld, uint32_t* const* joins,
-                            const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st) {
+// Test hook (VISREPS_ENGINE_INJECT=p): after the A walk of EST pass p, add 1 to the TB
+// entries of lanes 1..63 of one pair row -- a B-side recovery error the A walk's checks
+// cannot see. The tail's invariants must flag the pass and the exact re-run must restore
+// every score (tests/test_engine_est.py).
+__global__ void k_inject_tb(uint16_t* __restrict__ TB, uint32_t row, int lw) {
+  const int lane = threadIdx.x;
+  if (lane >= 1 && lane < lw) TB[(size_t)row * lw + lane] += 1u;
+}
+
+static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t nb, int64_t n,
+                                 const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
+                                 double* scores, int64_t score_ld, uint32_t* const* joins,
+                                 const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st) {
   const int64_t M = pairs_of(n);
+  uint32_t* const xbad = E.viol + EST_MAX_PASSES;  // exact-form passes' invariant flag
+  const int64_t inject = env_int("VISREPS_ENGINE_INJECT", -1);
   const int64_t total = n_sets + (full_first ? 1 : 0);
   if (total == 0 || nb == 0) return VR_OK;
   if (M == 0) {  // no pairs: every score is NaN (scipy on empty input)
@@ -1517,7 +1552,8 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
                   ? walk_b<Tg::lds, Tg::full, TBT, true, 0>(Bs[j], pj, cj, n, E, lw, j, cfg, st)
                   : walk_b<Tg::lds, Tg::full, TBT, false, 0>(Bs[j], pj, cj, n, E, lw, j, cfg, st)));
     }
-    return tail_units(E, nb, (uint32_t)cfg.nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0, score_ld, st);
+    return tail_units(E, nb, (uint32_t)cfg.nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0, score_ld, xbad,
+                      st);
   };
   if (!est) {
     return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
@@ -1546,6 +1582,10 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
             constexpr int EM = decltype(em)::value;
             VR_TRY((bigA ? pass_a_est<EM, Tg::lds, Tg::full, true>(A, n, E, lw, nl, cfg, e3, viol, st)
                          : pass_a_est<EM, Tg::lds, Tg::full, false>(A, n, E, lw, nl, cfg, e3, viol, st)));
+            if (p == inject) {
+              k_inject_tb<<<1, LANES, 0, st>>>(static_cast<uint16_t*>(E.TB), (uint32_t)(M / 2), lw);
+              VR_CHECK_LAUNCH();
+            }
             for (int64_t j = 0; j < nb; ++j) {
               const uint32_t* pj = joins[2 * j];
               const uint32_t* lj = EM >= 3 && lo_join ? joins[2 * j + 1] : nullptr;  // EST 3/4: streamed low ends
@@ -1554,7 +1594,7 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
                           : walk_b<Tg::lds, Tg::full, uint16_t, false, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)));
             }
             return tail_units(E, nb, (uint32_t)cfg.est_nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0,
-                              score_ld, st);
+                              score_ld, viol, st);
           };
           // EST 3 needs every lane to hold k stimuli: the pass holding the full set runs EST 4
           const bool full0 = full_first && p == 0;
@@ -1582,6 +1622,25 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
         return VR_OK;
       });
     }
+  }
+  return VR_OK;
+}
+
+// run_engine_multi_impl, then the exact-form passes' invariant flag: a set flag means the
+// exact arithmetic itself went wrong, so the call fails instead of returning the scores.
+static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, int64_t n,
+                            const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
+                            double* scores, int64_t score_ld, uint32_t* const* joins,
+                            const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st) {
+  uint32_t* const xbad = E.viol + EST_MAX_PASSES;
+  VR_CHECK_HIP(hipMemsetAsync(xbad, 0, sizeof(uint32_t), st));
+  VR_TRY(run_engine_multi_impl(A, Bs, nb, n, idx, k, n_sets, full_first, scores, score_ld, joins, E, lw, cfg, st));
+  uint32_t bad = 0;
+  VR_CHECK_HIP(hipMemcpyAsync(&bad, xbad, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VR_CHECK_HIP(hipStreamSynchronize(st));
+  if (bad) {
+    set_error("bootstrap engine: an exact-form pass broke the rank-sum invariants (included pairs / sum of ranks)");
+    return VR_EINTERNAL;
   }
   return VR_OK;
 }

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -207,17 +208,26 @@ int vr_legacy_choice(uint32_t seed, int64_t n, int64_t k, int64_t n_draws, int32
       s.pos += j;
     }
   }
+  // Worker t draws d = t, t + nt, ...; its scratch is allocated here, so nothing inside a
+  // thread can throw. If the system refuses a thread (a container's thread limit), the
+  // stride classes not started run on this thread: same outputs, no exception through the
+  // C ABI.
+  std::vector<std::vector<int32_t>> perm((size_t)nt, std::vector<int32_t>((size_t)n));
+  auto work = [&](int64_t t) {
+    for (int64_t d = t; d < n_draws; d += nt) {
+      MTState local = snap[(size_t)d];
+      mt_permutation(&local, n, perm[(size_t)t].data());
+      std::memcpy(out + d * k, perm[(size_t)t].data(), (size_t)k * sizeof(int32_t));
+    }
+  };
   std::vector<std::thread> pool;
-  for (int64_t t = 0; t < nt; ++t) {
-    pool.emplace_back([&, t]() {
-      std::vector<int32_t> perm((size_t)n);
-      for (int64_t d = t; d < n_draws; d += nt) {
-        MTState local = snap[(size_t)d];
-        mt_permutation(&local, n, perm.data());
-        std::memcpy(out + d * k, perm.data(), (size_t)k * sizeof(int32_t));
-      }
-    });
+  pool.reserve((size_t)nt);
+  int64_t started = 0;
+  try {
+    for (; started < nt; ++started) pool.emplace_back(work, started);
+  } catch (const std::system_error&) {
   }
+  for (int64_t t = started; t < nt; ++t) work(t);
   for (auto& th : pool) th.join();
   return VR_OK;
 }

@@ -10,7 +10,8 @@ MI355X differences (not semantics): activations can stay in HBM (keep_on_device=
 so the RDM kernels read them in place; the SRP product runs in the HIP CSR kernel of
 visreps_amd.analysis.sparse_random_projection; checkpoints are read with
 torch.load(weights_only=True) — the reference pickles whole nn.Modules, which this build
-will not unpickle (convert them to state_dicts).
+will not unpickle (convert them to state_dicts once, in the reference's environment:
+INTEGRATION.md, "Checkpoints: converting the reference's pickled models").
 """
 from __future__ import annotations
 

@@ -213,6 +213,9 @@ class RdmKernels:
         k = len(xs)
         if k == 0 or xs[0].size(0) == 0:
             return
+        # the kernel reads fp32 rows with unit inner stride (half/bf16 hook outputs under
+        # autocast, or strided views, are widened / compacted here, as tiles_from_rows does)
+        xs = [x if (x.dtype == torch.float32 and x.stride(1) == 1) else x.float().contiguous() for x in xs]
         P64, I64 = ctypes.c_void_p * k, ctypes.c_int64 * k
         check(lib().vr_rdm_split_rows_multi_f32(
             k, P64(*[x.data_ptr() for x in xs]), I64(*[x.size(1) for x in xs]), I64(*[x.stride(0) for x in xs]),
@@ -405,10 +408,17 @@ def _all_to_all_rows(send_parts: List[Optional[torch.Tensor]], recv_rows: List[i
     world = len(recv_rows)
     empty = torch.empty((0,) + tuple(row_shape), dtype=dtype, device=device)
     parts = [pt if pt is not None else empty for pt in send_parts]
-    inp = torch.cat(parts, 0) if any(pt.size(0) for pt in parts) else empty
     out = torch.empty((sum(recv_rows),) + tuple(row_shape), dtype=dtype, device=device)
+    if out.is_cuda and dist.get_backend(pg) == "nccl":
+        # RCCL: the list form (grouped send/recv) sends each part from where it lies and
+        # receives into views of `out`: when every rank owns an RDM (distributed_rdm, configs[2])
+        # each rank's rows go to all world owners without world concatenated copies of them
+        outs = list(out.split([int(r) for r in recv_rows], 0))
+        work = dist.all_to_all(outs, [pt.contiguous() for pt in parts], group=pg, async_op=async_op)
+        return work, out, parts
+    inp = torch.cat(parts, 0) if any(pt.size(0) for pt in parts) else empty
     in_splits = [int(pt.size(0)) for pt in parts]
-    if inp.is_cuda and dist.get_backend(pg) != "nccl":
+    if inp.is_cuda:
         # gloo has no all-to-all of device tensors: only the one-GPU rehearsal of the multi-rank
         # path takes this (scripts/gpu_rehearse.sh); RCCL moves device memory directly
         host = torch.empty(out.shape, dtype=out.dtype)
@@ -417,7 +427,7 @@ def _all_to_all_rows(send_parts: List[Optional[torch.Tensor]], recv_rows: List[i
         out.copy_(host)
         return _Done(), out, inp
     work = dist.all_to_all_single(out, inp, output_split_sizes=list(recv_rows), input_split_sizes=in_splits,
-                                  group=pg, async_op=async_op)
+                                  group=pg, async_op=async_op)  # gloo, host tensors (CPU tests)
     return work, out, inp
 
 
@@ -545,18 +555,21 @@ class ShardedRDMs:
             cons = self.sched.consumers[k]
             send: List[Optional[torch.Tensor]] = [None] * self.world
             recv = [0] * self.world
+            others = [c for c in cons if c != rank]
             for pc in pcs:
-                if pc.owner == rank:
+                if pc.owner == rank and others:
                     packed = torch.empty((pc.t1 - pc.t0, TILE * TILE), dtype=torch.float32, device=dev)
                     K.pack(bufs[k], n, pc.t0, pc.t1, packed)
-                    for c in cons:
-                        if c != rank:
-                            send[c] = packed if send[c] is None else torch.cat([send[c], packed], 0)
+                    for c in others:
+                        send[c] = packed if send[c] is None else torch.cat([send[c], packed], 0)
                 if rank in cons and pc.owner != rank:
                     recv[pc.owner] += pc.t1 - pc.t0
-            if any(x is not None for x in send) or any(recv):
-                pass  # every rank joins every RDM's exchange (collective order)
-            _, got, _ = _all_to_all_rows(send, recv, (TILE * TILE,), torch.float32, dev, self.pg)
+            # every rank joins every exchanged RDM's collective (same order everywhere); an RDM
+            # whose consumers all own every piece of it moves nothing, and every rank sees that
+            # from the schedule alone, so all of them skip its collective
+            got = None
+            if any(c != pc.owner for pc in pcs for c in cons):
+                _, got, _ = _all_to_all_rows(send, recv, (TILE * TILE,), torch.float32, dev, self.pg)
             if k in mine:
                 o = bufs.pop(k, None)
                 if o is None:
