@@ -215,6 +215,110 @@ def structured_est_probe(n: int, plan_b, dev) -> dict:
     return out
 
 
+FP64_MFMA_PEAK_TF = 78.6  # MI355X spec sheet: FP64 matrix (not in MI355X_MICROARCH.md; confirm on the box)
+
+
+def kendall_leg(plan_m, plan_n, n: int, n_boot: int) -> dict:
+    """compare_method=kendall (rsa.py:22-40, allowed by utils.py:518) on one bench unit
+    (the first point x V1 plans, N = n, the RandomState(42) subsets): point + n_boot
+    bootstrap tau-a in one call, outside the timed steps. Byte model of the dominant kernel
+    k_kwalk (one stream walk of one pass: an inversion level or a tie stream): 4-B pair code
+    + 2 bit planes = 4.25 B per pair; it is bound by the window machinery (mask lookups,
+    64x64 transposes, bit-parallel pair counts), not HBM, so `frac` is low by construction."""
+    from visreps_amd.analysis import rsa as R
+    from visreps_amd.analysis._random import bootstrap_indices
+
+    idx = bootstrap_indices(42, n, int(0.9 * n), n_boot)
+    R.bootstrap_kendall(plan_m, plan_n, idx[:2], full_first=True)  # warm
+    torch.cuda.synchronize()
+    ktimer_enable(True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    sc = R.bootstrap_kendall(plan_m, plan_n, idx, full_first=True)
+    e1.record()
+    torch.cuda.synchronize()
+    ms, launches, pairs = ktimer_read("k_kwalk")
+    ktimer_enable(False)
+    gbs = 4.25 * pairs / (ms / 1e3) / 1e9 if ms else 0.0
+    return {"unit_ms": round(e0.elapsed_time(e1), 2), "subsets": int(sc.numel()), "point": float(sc[0]),
+            "k_kwalk": {"ms": round(ms, 2), "launches": launches, "avg_us": round(1e3 * ms / max(1, launches), 1),
+                        "bytes_model": "4.25 B per pair per walk (pair code 4 + bucket-start and y-bit planes)",
+                        "achieved_gbs": round(gbs, 1), "peak_gbs": HBM_PEAK_GBS,
+                        "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "bound": "VALU (window transposes + pair counts), not HBM"},
+            "note": ("point + bootstrap tau-a of one unit (bench's first point x V1, N=%d, %d subsets of %d), "
+                     "HIP events; outside the timed steps" % (n, n_boot, int(0.9 * n)))}
+
+
+def configs3_leg(dev, dims: dict, n_boot: int) -> dict:
+    """BASELINE configs[3] on device-resident synthetic inputs, outside the timed steps:
+      * THINGS behavioural RSA (evals.py:95-155 -> compute_rsa, rsa.py:132-281): 1,854
+        concepts (20 % selection / 80 % evaluation, RandomState(42).permutation), 14
+        concept-mean points of the CustomCNN widths vs a 66-d embedding, layer selection +
+        point + n_boot bootstraps;
+      * the encoding score's cross-validated ridge (encoding_score.py:47-62, himalaya
+        RidgeCV(alphas=logspace(-10, 10, 20), cv=5)) at n = 26,000 (20,800 fit, 5,200
+        predicted), p = 4,096, 48 voxels, primal form: six fp64 p x p Grams X^T X on the
+        fp64 MFMA (vr_gram64_f32, k_cov), rocSOLVER eigh, fp64 products.
+    roofline_gram64: algorithmic FLOPs n p (p + 1) per Gram / k_cov HIP-event time / FP64
+    matrix peak (78.6 TF spec)."""
+    from visreps_amd.analysis.alignment import AlignmentData
+    from visreps_amd.analysis.encoding_score import ridge_cv_predict_primal
+    from visreps_amd.analysis.rsa import compute_rsa
+
+    nc = 1854
+    g = torch.Generator(device=dev).manual_seed(1854)
+    z = torch.randn(nc, 64, device=dev, generator=g)
+    acts = {p: torch.relu(z @ (torch.randn(64, d, device=dev, generator=g) / 8)
+                          + 2 * torch.randn(nc, d, device=dev, generator=g)) for p, d in dims.items()}
+    emb = z @ torch.randn(64, 66, device=dev, generator=g) + torch.randn(nc, 66, device=dev, generator=g)
+    perm = np.random.RandomState(42).permutation(nc)
+    ns = int(nc * 0.2)
+    sel_t = torch.as_tensor(perm[:ns], device=dev)
+    ev_t = torch.as_tensor(perm[ns:], device=dev)
+    sel = AlignmentData({p: a[sel_t] for p, a in acts.items()}, emb[sel_t])
+    ev = AlignmentData({p: a[ev_t] for p, a in acts.items()}, emb[ev_t])
+    del acts
+    with contextlib.redirect_stdout(sys.stderr):
+        compute_rsa({"compare_method": "spearman"}, sel, ev, n_select=None, bootstrap=True, n_bootstrap=8)  # warm
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        res = compute_rsa({"compare_method": "spearman"}, sel, ev, n_select=None, bootstrap=True,
+                          n_bootstrap=n_boot)[0]
+        torch.cuda.synchronize()
+        t_rsa = time.perf_counter() - t
+    del sel, ev
+    # ridge at configs[3]'s size (tests/test_encoding.py::test_ridge_cv_full_size_matches_closed_form's data)
+    n_fit, n_new, p, v = 20800, 5200, 4096, 48
+    g = torch.Generator(device=dev).manual_seed(26000)
+    Z = torch.randn(n_fit + n_new, 256, device=dev, generator=g)
+    X = Z @ torch.randn(256, p, device=dev, generator=g) + 0.5 * torch.randn(n_fit + n_new, p, device=dev, generator=g)
+    X = (X - X.mean(0)) / X.std(0)
+    Y = (X @ (torch.randn(p, v, device=dev, generator=g) / 64.0)) * torch.logspace(1, -2, v, device=dev) \
+        + torch.randn(n_fit + n_new, v, device=dev, generator=g)
+    ridge_cv_predict_primal(X[:2000], Y[:2000], X[n_fit:n_fit + 10])  # warm (solver handles, kernels)
+    torch.cuda.synchronize()
+    ktimer_enable(True)
+    t = time.perf_counter()
+    pred, alphas = ridge_cv_predict_primal(X[:n_fit], Y[:n_fit], X[n_fit:])
+    torch.cuda.synchronize()
+    t_ridge = time.perf_counter() - t
+    ms, launches, flops = ktimer_read("k_cov")
+    ktimer_enable(False)
+    tf = flops / (ms / 1e3) / 1e12 if ms else 0.0
+    return {"things_rsa": {"s": round(t_rsa, 3), "concepts": nc, "selection": ns, "evaluation": nc - ns,
+                           "points": len(dims), "n_bootstrap": n_boot, "best_layer": res["layer"],
+                           "score": res["score"]},
+            "ridge": {"s": round(t_ridge, 3), "n_fit": n_fit, "n_new": n_new, "p": p, "voxels": v,
+                      "distinct_alphas": int(len(set(np.asarray(alphas).tolist()))), "form": "primal (p < n)"},
+            "roofline_gram64": {"bound": "mfma", "kernel": "k_cov (v_mfma_f64_16x16x4_f64, fp64 X^T X tiles)",
+                                "achieved": round(tf, 2), "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                                "frac": round(tf / FP64_MFMA_PEAK_TF, 4), "launches": launches,
+                                "ms": round(ms, 2), "algorithmic_flops": "n p (p + 1) per Gram (unique i <= j)",
+                                "peak_source": "MI355X spec sheet FP64 matrix (not listed in MI355X_MICROARCH.md)"},
+            "note": "device-resident synthetic inputs, wall time incl. eigh and host orchestration; outside the timed steps"}
+
+
 def _time(fn):
     t = time.perf_counter()
     out = fn()
@@ -293,6 +397,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-est-probe", action="store_true")
+    ap.add_argument("--no-extra-legs", action="store_true", help="skip the Kendall and configs[3] legs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -403,7 +508,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     times = StepTimes()
-    reruns0 = int(L.vr_engine_est_reruns())
+    reruns0, tails0 = int(L.vr_engine_est_reruns()), int(L.vr_engine_est_tail_flags())
     ktimer_enable(True)  # per-launch HIP events on the launch stream of the hot kernels
     check(L.vr_trace_mark(1, 0, ctypes.c_void_p(stream_of(dev))), "vr_trace_mark")
     t0 = time.perf_counter()
@@ -418,6 +523,7 @@ def main():
     kt = {k: ktimer_read(k) for k in KTIMER_KERNELS}
     ktimer_enable(False)
     est_reruns = int(L.vr_engine_est_reruns()) - reruns0
+    est_tail_flags = int(L.vr_engine_est_tail_flags()) - tails0
     stats = torch.tensor([elapsed, times.engine_ms, times.engine_bytes, times.gram_ms,
                           times.gram_flops], dtype=torch.float64, device=dev)
     if pg is not None:
@@ -498,6 +604,17 @@ def main():
             t = time.perf_counter()
             est_structured = structured_est_probe(N, RankPlan(neural["V1"]), dev)
             log(f"structured-RDM EST probe took {time.perf_counter() - t:.1f}s: {est_structured}")
+        kendall = configs3 = None
+        if world == 1 and N <= 65535 and not args.no_extra_legs:
+            from visreps_amd.analysis.rsa import RankPlan
+
+            t = time.perf_counter()
+            kendall = kendall_leg(RankPlan(neural["V2"]), RankPlan(neural["V1"]), N, args.boot)
+            kendall["note"] = kendall["note"].replace("bench's first point x V1", "the V2 x V1 neural RDMs")
+            log(f"kendall leg took {time.perf_counter() - t:.1f}s: {kendall}")
+            t = time.perf_counter()
+            configs3 = configs3_leg(dev, dims, args.boot)
+            log(f"configs[3] leg took {time.perf_counter() - t:.1f}s: {configs3}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             t = time.perf_counter()
@@ -538,7 +655,10 @@ def main():
             "roofline_gram": roof_gram,
             "kernels_per_step": {k: v for k, v in kernels.items() if v["launches_per_step"]},
             "est_reruns": est_reruns,
+            "est_tail_flags": est_tail_flags,
             "est_structured": est_structured,
+            "kendall_unit": kendall,
+            "configs3": configs3,
             "timed_region": ("bracketed by k_trace_mark_begin / k_trace_mark_end dispatches (vr_trace_mark): "
                              "scripts/check_timed_kernels.py lists the kernels between them in a rocprofv3 "
                              "trace (profiles/r3_timed_kernels.json)"),

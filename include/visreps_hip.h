@@ -192,12 +192,16 @@ int vr_bootstrap_spearman_multi(const void* plan_a, const void* const* planBs, i
  * VISREPS_ENGINE_EST=0 forces the chunk-base form; an exact-form pass that breaks the
  * invariants fails the call with VR_EINTERNAL. */
 int64_t vr_engine_est_reruns(void);
+/* Of those re-runs, the passes the tail invariants flagged (B-side errors; 0 unless a bug
+ * or a fault injection). */
+int64_t vr_engine_est_tail_flags(void);
 
 // Kernel-level HIP-event timing of the hot kernels, for pricing the dominant kernel against
 // its roofline on the stream it runs on (bench.py). Off by default; enabling clears the
 // totals. kernel: 0 k_rankB EST forms over bootstrap subsets, 1 k_rankB exact form, 2 k_rankA,
 // 3 k_join/k_join_lo, 4 k_gram3p/k_gram3w (256^2 super-tiles), 5 k_gram3/k_gram (128^2 tiles),
-// 6 k_countA, 7 k_rankB EST 4 (the full-set pass: point estimates, phase-1 selections).
+// 6 k_countA, 7 k_rankB EST 4 (the full-set pass: point estimates, phase-1 selections), 8 k_kwalk
+// (one Kendall stream walk of one pass), 9 k_cov (fp64 MFMA covariance / ridge Gram tiles).
 // units: pairs walked (engine kernels) or tile FLOPs 2 d x tile elements (Gram kernels).
 // No reference counterpart (the reference has no native kernels).
 int vr_ktimer_enable(int on);
@@ -348,6 +352,17 @@ size_t vr_pca_cov_workspace(int64_t n, int64_t p);
 int vr_pca_cov_f64(const float* X, int64_t n, int64_t p, int64_t ldx, const float* mean,
                    double denom, double* cov, int64_t ldc, void* ws, size_t ws_bytes,
                    void* stream);
+
+/* Uncentred fp64 Grams of fp32 features on the same fp64 MFMA tiles (the encoding score's
+ * ridge): replaces the fp64 X^T X / X X^T that himalaya 0.4.9's
+ * RidgeCV(solver="svd") needs, called from visreps/analysis/encoding_score.py:47-62.
+ * X [dev] fp32 row-major (n, p), leading dimension ldx >= p. rows = 0: G = X^T X (p x p,
+ * the primal form, p < n); rows = 1: G = X X^T (n x n, the kernel form, p >= n). Products
+ * of two fp32 values are exact in fp64, sums fp64. G [dev] fp64, leading dimension ldg,
+ * exactly symmetric. Workspace: vr_gram64_workspace(n, p, rows). */
+size_t vr_gram64_workspace(int64_t n, int64_t p, int rows);
+int vr_gram64_f32(const float* X, int64_t n, int64_t p, int64_t ldx, int rows, double* G, int64_t ldg,
+                  void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------
  * Host: legacy numpy RandomState (MT19937) index streams, bit-exact.

@@ -11,7 +11,7 @@ if [ $# -gt 0 ]; then
       > $out/pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|Error" $out/pytest.log | head; tail -30 $out/pytest.log; exit 1; }
   tail -1 $out/pytest.log
 fi
-timeout -k 10 400 python bench.py --no-cpu-baseline --no-est-probe > $out/bench.json 2> $out/bench.err \
+timeout -k 10 400 python bench.py --no-cpu-baseline --no-est-probe --no-extra-legs > $out/bench.json 2> $out/bench.err \
     || { echo "bench failed"; tail -20 $out/bench.err; exit 1; }
 python3 - $out/bench.json <<'PY'
 import json, sys

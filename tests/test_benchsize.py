@@ -262,9 +262,10 @@ def test_bench_point_vs_cpu_oracle(dev, bench, point):
     x = feats[point]
     gm = R.compute_rdm(x)
     gn = R.compute_rdm(bench[4])
-    r0 = int(lib().vr_engine_est_reruns())
+    r0, t0 = int(lib().vr_engine_est_reruns()), int(lib().vr_engine_est_tail_flags())
     point_g, scores_g, _, _ = R.bootstrap_rsa(gm, gn, n_bootstrap=NB, seed=42)
     reruns = int(lib().vr_engine_est_reruns()) - r0
+    tail = int(lib().vr_engine_est_tail_flags()) - t0
     del gm, gn
     torch.cuda.empty_cache()
     point_o, scores_o, late_o = _oracle_results(bench)[point].result()
@@ -273,7 +274,8 @@ def test_bench_point_vs_cpu_oracle(dev, bench, point):
     dl = max(abs(float(scores_g[i]) - late_o[i]) for i in LATE_DRAWS)
     record_margin("bench_point_vs_cpu_oracle", point=point, d=x.size(1), point_hip=point_g, point_oracle=point_o,
                   dspearman_point=dp, dspearman_boot5=db, dspearman_late_draws=dl, late_draws=LATE_DRAWS,
-                  est_reruns=reruns)
+                  est_reruns=reruns, est_tail_flags=tail)
+    assert tail == 0, "B-side invariant broken on the bench's own RDMs"
     assert dp < SPEARMAN_TOL and db < SPEARMAN_TOL and dl < SPEARMAN_TOL, (point, dp, db, dl)
 
 

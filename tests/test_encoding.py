@@ -84,6 +84,26 @@ def test_gram_kernel_matches_fp64(dev, n, d):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,p,ld", [(300, 70, 70), (1000, 4096, 4096), (2100, 33, 40), (77, 1000, 1003), (5, 3, 3)])
+def test_gram64_kernels_match_fp64(dev, n, p, ld):
+    # vr_gram64_f32 (fp64 MFMA tiles): X X^T (kernel form) and X^T X (primal form) of fp32 X
+    # vs numpy fp64 products -- exact products, fp64 sums: relative 1e-13; exactly symmetric.
+    # Ragged shapes, a row pitch ld > p (unaligned rows) and tiny n.
+    import torch
+    from visreps_amd.analysis.encoding_score import gram64, gram64_cols
+
+    buf = np.random.RandomState(n + p).randn(n, ld).astype(np.float32)
+    x = buf[:, :p]
+    xt = torch.from_numpy(buf).to(dev)[:, :p]  # a strided view: row pitch ld
+    x64 = x.astype(np.float64)
+    for got, ref in ((gram64(xt), x64 @ x64.T), (gram64_cols(xt), x64.T @ x64)):
+        g = got.cpu().numpy()
+        assert g.dtype == np.float64 and g.shape == ref.shape
+        assert np.max(np.abs(g - ref)) <= 1e-13 * max(1.0, np.abs(ref).max())
+        assert np.array_equal(g, g.T)
+
+
+@pytest.mark.gpu
 def test_corr_score_point_and_voxels_match_scipy(dev):
     import torch
     from visreps_amd.analysis.encoding_score import corr_score

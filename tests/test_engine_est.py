@@ -179,10 +179,11 @@ def test_b_side_error_is_flagged_and_rerun(dev, monkeypatch, inject):
     pa, pb = R.RankPlan(a), R.RankPlan(b)
     clean = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
     monkeypatch.setenv("VISREPS_ENGINE_INJECT", str(inject))
-    r0 = int(lib().vr_engine_est_reruns())
+    r0, t0 = int(lib().vr_engine_est_reruns()), int(lib().vr_engine_est_tail_flags())
     got = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
     reruns = int(lib().vr_engine_est_reruns()) - r0
     assert reruns >= 1, "the injected B-side error must flag its pass"
+    assert int(lib().vr_engine_est_tail_flags()) - t0 == 1, "flagged by the tail invariants (the A walk cannot see it)"
     assert np.array_equal(got, clean)
     with exact_engine():
         assert np.array_equal(R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy(), clean)

@@ -104,6 +104,7 @@ _PROTOTYPES = {
         [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _c_sz, _vp],
     ),
     "vr_engine_est_reruns": (_c_i64, []),
+    "vr_engine_est_tail_flags": (_c_i64, []),
     "vr_ktimer_enable": (ctypes.c_int, [ctypes.c_int]),
     "vr_trace_mark": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp]),
     "vr_ktimer_read": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
@@ -136,6 +137,8 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _c_i64, _c_i64, _c_i64, _vp, ctypes.c_double, _vp, _c_i64, _vp, _c_sz, _vp],
     ),
+    "vr_gram64_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
+    "vr_gram64_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _c_sz, _vp]),
     "vr_spearman_full_workspace": (_c_sz, [_c_i64]),
     "vr_spearman_full_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
     "vr_f32_sort_keys": (ctypes.c_int, [_vp, _c_i64, _vp, _vp]),
@@ -245,7 +248,8 @@ workspace = _WorkspacePool()
 
 
 KTIMER_KERNELS = {"k_rankB_est": 0, "k_rankB_exact": 1, "k_rankA": 2, "k_join": 3,
-                  "k_gram_wide": 4, "k_gram_tile": 5, "k_countA": 6, "k_rankB_full": 7}
+                  "k_gram_wide": 4, "k_gram_tile": 5, "k_countA": 6, "k_rankB_full": 7,
+                  "k_kwalk": 8, "k_cov": 9}
 
 
 def ktimer_enable(on: bool = True) -> None:

@@ -25,8 +25,9 @@ primal SVD solution X_V V diag(s / (s^2 + alpha)) U^T Y with lam = s^2. Every co
 with lam above the fp64 rounding floor of the decomposition (n * eps_64 * lam_max) is kept,
 as himalaya's SVD solver keeps every singular value. Narrow layers (p < n) run the primal
 form on the p x p Grams X_T^T X_T of each fold (``ridge_cv_predict_primal``). The ridge
-Grams are fp64 (``gram64``, rocBLAS DGEMM: the solves are conditioning-sensitive, ADVICE
-r1); the eigendecompositions and the small dense products run in fp64 through torch
+Grams are fp64 (the solves are conditioning-sensitive) on the fp64 MFMA tiles of
+``vr_gram64_f32`` (``gram64`` = X X^T, ``gram64_cols`` = X^T X: upper triangle only, fp32
+products exact in fp64); the eigendecompositions and the small dense products run in fp64 through torch
 (rocSOLVER / rocBLAS); the statistic and its bootstrap run in ``vr_corr_score_f32``. The
 MFMA Gram kernel (``vr_gram_f32``, ``gram``) stays available for fp32 callers.
 
@@ -49,7 +50,7 @@ from ..utils import rprint
 from ._random import LegacyRandomState
 from .rsa import percentile
 
-__all__ = ["compute_encoding_score", "gram", "corr_score", "ridge_cv_predict",
+__all__ = ["compute_encoding_score", "gram", "gram64", "gram64_cols", "corr_score", "ridge_cv_predict",
            "ridge_cv_predict_primal", "kfold_splits", "ALPHAS"]
 
 ALPHAS = np.logspace(-10, 10, 20)
@@ -145,11 +146,36 @@ def _eig(K: torch.Tensor):
     return lam, Q, keep
 
 
+def _gram64(x: torch.Tensor, rows: bool) -> torch.Tensor:
+    dev = _device(x)
+    x = x.to(dev, torch.float32)
+    if x.ndim != 2 or x.stride(1) != 1:
+        x = x.contiguous()
+    n, p = x.shape
+    m = n if rows else p
+    out = torch.empty((m, m), dtype=torch.float64, device=dev)
+    if m == 0:
+        return out
+    if (p if rows else n) == 0:
+        return out.zero_()
+    L = lib()
+    ws = workspace.get(dev, L.vr_gram64_workspace(n, p, int(rows)), "gram64")
+    with torch.cuda.device(dev):
+        check(L.vr_gram64_f32(_ptr(x), n, p, x.stride(0), int(rows), _ptr(out), m, _ptr(ws), ws.numel(),
+                              stream_of(dev)), "vr_gram64_f32")
+    return out
+
+
 def gram64(x: torch.Tensor) -> torch.Tensor:
-    """x x^T in fp64 (the ridge solves are conditioning-sensitive; the RSA Grams use
-    vr_gram_f32)."""
-    xd = x.double()
-    return xd @ xd.T
+    """x x^T in fp64 for fp32 x (the kernel form's K; the ridge solves are
+    conditioning-sensitive): the fp64 MFMA tiles of vr_gram64_f32, upper triangle only,
+    mirrored (the RSA Grams use vr_gram_f32)."""
+    return _gram64(x, rows=True)
+
+
+def gram64_cols(x: torch.Tensor) -> torch.Tensor:
+    """x^T x in fp64 for fp32 x (the primal form's p x p Gram), vr_gram64_f32."""
+    return _gram64(x, rows=False)
 
 
 def _dual_predict(K_new: torch.Tensor, lam, Q, keep, Y: torch.Tensor, alphas: torch.Tensor):
@@ -204,7 +230,7 @@ def ridge_cv_predict_primal(X_fit: torch.Tensor, Y_fit: torch.Tensor, X_new: tor
 
     def solve(rows):
         Xt = Xd[rows]
-        lam, V, keep = _eig(gram64(Xt.T))
+        lam, V, keep = _eig(gram64_cols(Xt))
         VtXtY = V.T @ (Xt.double().T @ Yd[rows])
         return lam, V, keep, VtXtY
 

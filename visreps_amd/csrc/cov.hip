@@ -18,7 +18,7 @@
 //             divides by the denominator and writes each entry and its mirror (the result
 //             is exactly symmetric, like the reference's batch.T @ batch).
 // Roofline: fp64 MFMA, algorithmic FLOPs = n p (p + 1) (the unique entries i <= j).
-#include "common.h"
+#include "internal.h"
 
 namespace vr {
 
@@ -83,7 +83,7 @@ constexpr int C_STAGE = CK * CLD;  // doubles per panel per stage
 struct CovParams {
   const float* X;
   int64_t n, p, ldx;
-  const float* mean;
+  const float* mean;  // null: uncentred (the ridge Grams)
   double* partial;  // [S][ntile][CT * CT]
   int T;            // tile rows
   int ntile;        // T (T + 1) / 2
@@ -91,6 +91,30 @@ struct CovParams {
   int64_t kslice;   // rows per slice (multiple of CK)
   bool vec;         // 16-B aligned rows: float4 panel loads
 };
+
+// TRANS (the kernel-form ridge Gram X X^T of a row-major (p, n) X): the contraction runs
+// along X's rows, so panel entry (k, c) is X[c * ldx + k]. Each thread loads 4 consecutive
+// k of one column c (one float4 when aligned) and scatters them down the LDS column.
+__device__ inline cf32x4 cov_load_t(const CovParams& P, int64_t col0, int64_t k, int64_t k1) {
+  const int c = threadIdx.x >> 2, kq = (threadIdx.x & 3) * 4;
+  cf32x4 v = {0.f, 0.f, 0.f, 0.f};
+  const int64_t col = col0 + c, r = k + kq;
+  if (col >= P.p || r >= k1) return v;
+  const float* src = P.X + col * P.ldx + r;
+  if (P.vec && r + 4 <= k1) {
+    v = *reinterpret_cast<const cf32x4*>(src);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (r + e < k1) ? src[e] : 0.f;
+  }
+  return v;
+}
+
+__device__ inline void cov_store_t(double* lds, const cf32x4 v) {
+  const int c = threadIdx.x >> 2, kq = (threadIdx.x & 3) * 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) lds[(kq + e) * CLD + c] = (double)v[e];  // out-of-range entries are 0
+}
 
 // tile t of the upper triangle (row-major: (0,0), (0,1), .., (0,T-1), (1,1), ..)
 __device__ inline void cov_tile(int t, int T, int& bi, int& bj) {
@@ -127,6 +151,7 @@ __device__ inline void cov_store(double* lds, const cf32x4 v, const double m[4],
   for (int e = 0; e < 4; ++e) dst[e] = in ? (double)v[e] - m[e] : 0.0;  // padded rows add exact zeros
 }
 
+template <bool TRANS>
 __global__ __launch_bounds__(C_THREADS, 2) void k_cov(CovParams P) {
   __shared__ __attribute__((aligned(16))) double lds[2][2][C_STAGE];  // [buf][A/B]
   const int id = (int)xcd_remap(blockIdx.x, gridDim.x);
@@ -146,8 +171,8 @@ __global__ __launch_bounds__(C_THREADS, 2) void k_cov(CovParams P) {
     const int c = (threadIdx.x & 15) * 4;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      mA[e] = (ci + c + e < P.p) ? (double)P.mean[ci + c + e] : 0.0;
-      mB[e] = (cj + c + e < P.p) ? (double)P.mean[cj + c + e] : 0.0;
+      mA[e] = (P.mean && ci + c + e < P.p) ? (double)P.mean[ci + c + e] : 0.0;
+      mB[e] = (P.mean && cj + c + e < P.p) ? (double)P.mean[cj + c + e] : 0.0;
     }
   }
   f64x4 acc[2][2];
@@ -156,12 +181,19 @@ __global__ __launch_bounds__(C_THREADS, 2) void k_cov(CovParams P) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
 
+  auto load = [&](int64_t col0, int64_t k) { return TRANS ? cov_load_t(P, col0, k, k1) : cov_load(P, col0, k, k1); };
+  auto store = [&](double* dst, const cf32x4 v, const double* m, int64_t k) {
+    if constexpr (TRANS)
+      cov_store_t(dst, v);
+    else
+      cov_store(dst, v, m, k, k1);
+  };
   cf32x4 ga = {0.f, 0.f, 0.f, 0.f}, gb = ga;
   if (nk > 0) {
-    ga = cov_load(P, ci, k0, k1);
-    if (!diag) gb = cov_load(P, cj, k0, k1);
-    cov_store(lds[0][0], ga, mA, k0, k1);
-    if (!diag) cov_store(lds[0][1], gb, mB, k0, k1);
+    ga = load(ci, k0);
+    if (!diag) gb = load(cj, k0);
+    store(lds[0][0], ga, mA, k0);
+    if (!diag) store(lds[0][1], gb, mB, k0);
   }
   __syncthreads();
   // fragment of the 16x16x4 f64 MFMA: lane l supplies A[m = l & 15][k = l >> 4] and
@@ -174,8 +206,8 @@ __global__ __launch_bounds__(C_THREADS, 2) void k_cov(CovParams P) {
     const bool more = kt + 1 < nk;
     const int64_t kn = k0 + (int64_t)(kt + 1) * CK;
     if (more) {
-      ga = cov_load(P, ci, kn, k1);
-      if (!diag) gb = cov_load(P, cj, kn, k1);
+      ga = load(ci, kn);
+      if (!diag) gb = load(cj, kn);
     }
 #pragma unroll
     for (int ks = 0; ks < CK / 4; ++ks) {
@@ -193,8 +225,8 @@ __global__ __launch_bounds__(C_THREADS, 2) void k_cov(CovParams P) {
           acc[m][nn] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[nn], acc[m][nn], 0, 0, 0);
     }
     if (more) {
-      cov_store(lds[cur ^ 1][0], ga, mA, kn, k1);
-      if (!diag) cov_store(lds[cur ^ 1][1], gb, mB, kn, k1);
+      store(lds[cur ^ 1][0], ga, mA, kn);
+      if (!diag) store(lds[cur ^ 1][1], gb, mB, kn);
     }
     __syncthreads();
   }
@@ -290,14 +322,9 @@ size_t vr_pca_cov_workspace(int64_t n, int64_t p) {
   return c.bytes();
 }
 
-int vr_pca_cov_f64(const float* X, int64_t n, int64_t p, int64_t ldx, const float* mean, double denom,
-                   double* cov, int64_t ldc, void* ws, size_t ws_bytes, void* stream) {
-  clear_error();
-  VR_REQUIRE(n >= 0 && p >= 1 && ldx >= p && ldc >= p, "vr_pca_cov_f64: bad shape n=%lld p=%lld",
-             (long long)n, (long long)p);
-  VR_REQUIRE(mean != nullptr && cov != nullptr && (n == 0 || X != nullptr), "vr_pca_cov_f64: null pointer");
-  VR_REQUIRE(ws_bytes >= vr_pca_cov_workspace(n, p), "vr_pca_cov_f64: workspace too small");
-  hipStream_t st = as_stream(stream);
+// (n = contraction length, p = output order) -> k_cov + k_cov_reduce
+static int cov_launch(bool trans, const float* X, int64_t n, int64_t p, int64_t ldx, const float* mean,
+                      double denom, double* cov, int64_t ldc, void* ws, hipStream_t st) {
   CovParams P;
   P.X = X;
   P.n = n;
@@ -308,11 +335,47 @@ int vr_pca_cov_f64(const float* X, int64_t n, int64_t p, int64_t ldx, const floa
   Carver c(ws);
   P.partial = c.take<double>((size_t)P.S * P.ntile * CT * CT);
   P.vec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
-  k_cov<<<(unsigned)(P.ntile * P.S), C_THREADS, 0, st>>>(P);
-  VR_CHECK_LAUNCH();
+  {
+    KtScope kt(KT_COV, (double)n * (double)p * (double)(p + 1), st);  // algorithmic FLOPs
+    if (trans)
+      k_cov<true><<<(unsigned)(P.ntile * P.S), C_THREADS, 0, st>>>(P);
+    else
+      k_cov<false><<<(unsigned)(P.ntile * P.S), C_THREADS, 0, st>>>(P);
+    VR_CHECK_LAUNCH();
+  }
   k_cov_reduce<<<(unsigned)P.ntile, 256, 0, st>>>(P.partial, P.S, P.ntile, P.T, p, denom, cov, ldc);
   VR_CHECK_LAUNCH();
   return VR_OK;
+}
+
+int vr_pca_cov_f64(const float* X, int64_t n, int64_t p, int64_t ldx, const float* mean, double denom,
+                   double* cov, int64_t ldc, void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  VR_REQUIRE(n >= 0 && p >= 1 && ldx >= p && ldc >= p, "vr_pca_cov_f64: bad shape n=%lld p=%lld",
+             (long long)n, (long long)p);
+  VR_REQUIRE(mean != nullptr && cov != nullptr && (n == 0 || X != nullptr), "vr_pca_cov_f64: null pointer");
+  VR_REQUIRE(ws_bytes >= vr_pca_cov_workspace(n, p), "vr_pca_cov_f64: workspace too small");
+  return cov_launch(false, X, n, p, ldx, mean, denom, cov, ldc, ws, as_stream(stream));
+}
+
+size_t vr_gram64_workspace(int64_t n, int64_t p, int rows) {
+  return rows ? vr_pca_cov_workspace(p, n) : vr_pca_cov_workspace(n, p);
+}
+
+int vr_gram64_f32(const float* X, int64_t n, int64_t p, int64_t ldx, int rows, double* G, int64_t ldg,
+                  void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  VR_REQUIRE(n >= 1 && p >= 0 && ldx >= p, "vr_gram64_f32: bad shape n=%lld p=%lld ldx=%lld", (long long)n,
+             (long long)p, (long long)ldx);
+  VR_REQUIRE(ldg >= (rows ? n : p), "vr_gram64_f32: ldg %lld too small", (long long)ldg);
+  VR_REQUIRE(G != nullptr && (p == 0 || X != nullptr), "vr_gram64_f32: null pointer");
+  VR_REQUIRE(ws_bytes >= vr_gram64_workspace(n, p, rows), "vr_gram64_f32: workspace too small");
+  if (rows) {  // X X^T (n x n): contraction over the p columns, X read transposed
+    VR_REQUIRE(p >= 1, "vr_gram64_f32: rows Gram of zero-width X");
+    return cov_launch(true, X, p, n, ldx, nullptr, 1.0, G, ldg, ws, as_stream(stream));
+  }
+  VR_REQUIRE(p >= 1, "vr_gram64_f32: columns Gram of zero-width X");
+  return cov_launch(false, X, n, p, ldx, nullptr, 1.0, G, ldg, ws, as_stream(stream));
 }
 
 }  // extern "C"

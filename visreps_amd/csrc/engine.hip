@@ -80,7 +80,8 @@ constexpr int EST_STEP_BITS = 12;  // interpolation steps per interval: 2^12
 #ifndef VR_PROBE_ACC
 #define VR_PROBE_ACC 0
 #endif
-static std::atomic<int64_t> g_est_reruns{0};  // passes re-run in the exact form (vr_engine_est_reruns)  // coarse intervals at most: table <= 128 x 256 B = 32 KB
+static std::atomic<int64_t> g_est_reruns{0};      // passes re-run in the exact form (vr_engine_est_reruns)
+static std::atomic<int64_t> g_est_tail_flags{0};  // of those, flagged by the tail invariants (vr_engine_est_tail_flags)
 
 // log2 of the coarse interval: the smallest b >= 12 (windows of 64 never straddle a
 // boundary; the 4096 steps are whole positions) with ceil(M / 2^b) <= 96, or, for larger
@@ -1301,7 +1302,8 @@ __global__ void k_tail_top(const uint64_t* __restrict__ fpart0, uint32_t nblk,
   const bool forced_nan = a_nan || ((nan_units >> u) & 1ull);
   const bool broken = lane < nl && !forced_nan &&
                       (P != (uint64_t)totA[lane] || Ssum != (uint64_t)totA[lane] * ((uint64_t)totA[lane] + 1u));
-  if (__ballot(broken) != 0 && lane == 0) *viol = 1u;  // every writer stores 1
+  // bit 1 (the A walk's window checks set bit 0); benign race: every writer stores old | 2
+  if (__ballot(broken) != 0 && lane == 0) *viol |= 2u;
   if (lane >= nl) return;
   const u128 Mp = totA[lane];
   const u128 mu = Mp * (Mp + 1) * (Mp + 1);
@@ -1611,6 +1613,7 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
     VR_CHECK_HIP(hipStreamSynchronize(st));
     for (int64_t p = p0; p < p1; ++p) {
       if (!flags[(size_t)(p - p0)]) continue;
+      if (flags[(size_t)(p - p0)] & 2u) g_est_tail_flags.fetch_add(1);
       if (second != JOIN_CHUNK) VR_TRY(join(JOIN_CHUNK));
       g_est_reruns.fetch_add(1);
       VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) { return exact_pass(tag, p * lw); }));
@@ -1704,6 +1707,7 @@ using namespace vr;
 extern "C" {
 
 int64_t vr_engine_est_reruns(void) { return g_est_reruns.load(); }
+int64_t vr_engine_est_tail_flags(void) { return g_est_tail_flags.load(); }
 
 size_t vr_bootstrap_workspace(int64_t n) {
   size_t b = 0;

@@ -96,7 +96,9 @@ enum KtKernel : int {
   KT_GRAM_TILE = 5,   // k_gram3 / k_gram (128^2 tiles)
   KT_COUNTA = 6,      // k_countA
   KT_RANKB_FULL = 7,  // k_rankB, EST 4: the pass holding the full stimulus set (point estimates)
-  KT_N = 8
+  KT_KWALK = 8,       // k_kwalk: one Kendall stream walk (inversion level or tie stream) of one pass
+  KT_COV = 9,         // k_cov: fp64 MFMA covariance / Gram tiles (PCA covariance, ridge kernel matrix)
+  KT_N = 10
 };
 bool ktimer_on();
 struct KtScope {

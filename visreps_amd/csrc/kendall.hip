@@ -35,6 +35,8 @@ namespace vr {
 constexpr int KW_THREADS = 1024;
 constexpr int KW_WAVES = KW_THREADS / 64;
 constexpr int KFIX_GROUPS = KW_THREADS / 64;
+// k_kwalk's static LDS: the per-wave partials it composes into its block summary
+constexpr size_t KW_STATIC_LDS = (size_t)KW_WAVES * 64 * (8 + 8 + 4 + 4 + 4);
 
 enum KField { KF_DIS = 0, KF_XTIE, KF_NTIE, KF_YTIE, KF_INCL, KF_N };
 
@@ -48,9 +50,10 @@ struct KCfg {
 static KCfg kendall_cfg(int64_t n) {
   KCfg c;
   const size_t need = (size_t)n * sizeof(uint64_t);
-  const size_t cap = 160 * 1024 - 1024;
+  const size_t cap = 160 * 1024 - 1024 - KW_STATIC_LDS;
   c.use_lds = need <= cap;
-  const int per_cu = c.use_lds ? std::max<int>(1, std::min<int>(2, (int)(cap / std::max<size_t>(need, 1)))) : 2;
+  const size_t per_block = (c.use_lds ? need : 0) + KW_STATIC_LDS;
+  const int per_cu = std::max<int>(1, std::min<int>(2, (int)((160 * 1024 - 1024) / per_block)));
   c.grid = num_cus() * per_cu;
   c.nwaves = c.grid * KW_WAVES;
   c.lds = c.use_lds ? need : 0;
@@ -84,10 +87,10 @@ struct KendallWs {
   uint32_t* xj_mem;
   uint32_t* yb_start;  // B order: starts / members of multi-element B groups
   uint32_t* yb_mem;
-  uint64_t* w_acc;     // [nwaves][64] per-wave partials
-  uint32_t* w_zlead;
-  uint32_t* w_c;
-  uint32_t* w_seen;
+  uint64_t* w_acc;     // [grid][64] per-block summaries (KSum s, g, a, b) and included counts
+  uint64_t* w_g;
+  uint64_t* w_a;
+  uint32_t* w_b;
   uint32_t* w_incl;
   uint64_t* tot;       // [KF_N][cap]
 };
@@ -117,10 +120,10 @@ static KendallWs kendall_layout(void* base, int64_t n, int64_t cap_sets, int nwa
   uint32_t** fl[] = {&w.lv_start, &w.lv_bits, &w.xa_start, &w.xa_mem, &w.xj_start, &w.xj_mem,
                      &w.yb_start, &w.yb_mem};
   for (uint32_t** f : fl) *f = c.take<uint32_t>((size_t)FW);
-  w.w_acc = c.take<uint64_t>((size_t)nwaves * LANES);
-  w.w_zlead = c.take<uint32_t>((size_t)nwaves * LANES);
-  w.w_c = c.take<uint32_t>((size_t)nwaves * LANES);
-  w.w_seen = c.take<uint32_t>((size_t)nwaves * LANES);
+  w.w_acc = c.take<uint64_t>((size_t)nwaves * LANES);  // sized per wave; grid entries used
+  w.w_g = c.take<uint64_t>((size_t)nwaves * LANES);
+  w.w_a = c.take<uint64_t>((size_t)nwaves * LANES);
+  w.w_b = c.take<uint32_t>((size_t)nwaves * LANES);
   w.w_incl = c.take<uint32_t>((size_t)nwaves * LANES);
   w.tot = c.take<uint64_t>((size_t)KF_N * (size_t)std::max<int64_t>(cap_sets, 1));
   if (bytes) *bytes = c.bytes();
@@ -265,12 +268,28 @@ __global__ void k_level_split(const uint32_t* __restrict__ ecode, const uint32_t
 // TIE: o = z = included members (aux plane) of multi-element groups, S = their starts;
 // else (inversions): o / z = included positions with bit b of y set / clear (aux plane),
 // S = bucket starts.
+// A range summary as an affine map of the carry C into it (the ones of the segment open at
+// its start): contribution s + g C, carry out a + b C (b in {0, 1}). A wave range is
+// (acc, zlead, c, !seen); ranges compose left to right.
+struct KSum {
+  uint64_t s, g, a;
+  uint32_t b;
+};
+__device__ inline KSum ksum_identity() { return {0ull, 0ull, 0ull, 1u}; }
+// S then R: R's carry in is S's carry out a_S + b_S C
+__device__ inline void ksum_push(KSum& S, uint64_t s, uint64_t g, uint64_t a, uint32_t b) {
+  S.s += s + g * S.a;
+  S.g += S.b ? g : 0ull;
+  S.a = a + (b ? S.a : 0ull);
+  S.b = S.b & b;
+}
+
 template <bool LDS, bool TIE>
 __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ sflag,
     const uint32_t* __restrict__ aux, int64_t M, const uint64_t* __restrict__ gmask, int64_t n,
-    int nl, uint32_t nwaves, uint64_t* __restrict__ w_acc, uint32_t* __restrict__ w_zlead,
-    uint32_t* __restrict__ w_c, uint32_t* __restrict__ w_seen, uint32_t* __restrict__ w_incl) {
+    int nl, uint32_t nwaves, uint64_t* __restrict__ w_acc, uint64_t* __restrict__ w_g,
+    uint64_t* __restrict__ w_a, uint32_t* __restrict__ w_b, uint32_t* __restrict__ w_incl) {
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
   const int lane = threadIdx.x & 63;
@@ -306,50 +325,69 @@ __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
       kseg_window<false>(x & X, x & ~X, S, a, seen);
     }
   }
-  const size_t o = (size_t)wave * LANES + lane;
-  w_acc[o] = a.acc;
-  w_zlead[o] = a.zlead;
-  w_c[o] = a.c;
-  w_seen[o] = seen ? 1u : 0u;
-  w_incl[o] = incl;
+  // The block's 16 wave ranges are consecutive: compose them here (affine carry maps, see
+  // k_kfix) and write one summary per block, so the fix-up reads grid x 64 entries instead
+  // of nwaves x 64 (16x less: the single-block fix-up was bound by reading them).
+  __shared__ uint64_t s_acc[KW_WAVES][LANES], s_zl[KW_WAVES][LANES];
+  __shared__ uint32_t s_c[KW_WAVES][LANES], s_inc[KW_WAVES][LANES], s_seen[KW_WAVES][LANES];
+  const int wv = threadIdx.x >> 6;
+  s_acc[wv][lane] = a.acc;
+  s_zl[wv][lane] = a.zlead;
+  s_c[wv][lane] = a.c;
+  s_seen[wv][lane] = seen ? 1u : 0u;
+  s_inc[wv][lane] = incl;
+  __syncthreads();
+  if (wv != 0) return;
+  KSum S = ksum_identity();
+  uint32_t inc = 0;
+  for (int w = 0; w < KW_WAVES; ++w) {
+    ksum_push(S, s_acc[w][lane], s_zl[w][lane], s_c[w][lane], s_seen[w][lane] == 0u);
+    inc += s_inc[w][lane];
+  }
+  const size_t o = (size_t)blockIdx.x * LANES + lane;
+  w_acc[o] = S.s;
+  w_g[o] = S.g;
+  w_a[o] = S.a;
+  w_b[o] = S.b;
+  w_incl[o] = inc;
 }
 
-// Stream total per lane: sum of wave partials + cross-wave fix-up (kcount.h), added into
-// tot[field][set0 + lane]; optionally the included-pair count into tot[KF_INCL].
+// Stream total per lane: the block summaries (k_kwalk) composed in block order with carry 0
+// into the first, added into tot[field][set0 + lane]; optionally the included-pair count into
+// tot[KF_INCL]. 16 groups compose contiguous block ranges, group 0 composes the groups.
 __global__ __launch_bounds__(KW_THREADS) void k_kfix(
-    const uint64_t* __restrict__ w_acc, const uint32_t* __restrict__ w_zlead,
-    const uint32_t* __restrict__ w_c, const uint32_t* __restrict__ w_seen,
-    const uint32_t* __restrict__ w_incl, uint32_t nwaves, int nl, int field, int add_incl,
+    const uint64_t* __restrict__ w_acc, const uint64_t* __restrict__ w_g,
+    const uint64_t* __restrict__ w_a, const uint32_t* __restrict__ w_b,
+    const uint32_t* __restrict__ w_incl, uint32_t nblk, int nl, int field, int add_incl,
     uint64_t* __restrict__ tot, int64_t cap, int64_t set0) {
-  __shared__ uint64_t s_sum[KFIX_GROUPS][LANES], s_g[KFIX_GROUPS][LANES], s_a[KFIX_GROUPS][LANES],
+  __shared__ uint64_t s_s[KFIX_GROUPS][LANES], s_g[KFIX_GROUPS][LANES], s_a[KFIX_GROUPS][LANES],
       s_inc[KFIX_GROUPS][LANES];
   __shared__ uint32_t s_b[KFIX_GROUPS][LANES];
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const uint32_t per = (nwaves + KFIX_GROUPS - 1) / KFIX_GROUPS;
-  const uint32_t w0 = grp * per, w1 = min(nwaves, w0 + per);
-  KFix F = kfix_identity();
-  uint64_t sum = 0, inc = 0;
-  for (uint32_t w = w0; w < w1; ++w) {
-    const size_t o = (size_t)w * LANES + lane;
-    sum += w_acc[o];
+  const uint32_t per = (nblk + KFIX_GROUPS - 1) / KFIX_GROUPS;
+  const uint32_t b0 = grp * per, b1 = min(nblk, b0 + per);
+  KSum S = ksum_identity();
+  uint64_t inc = 0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const size_t o = (size_t)b * LANES + lane;
+    ksum_push(S, w_acc[o], w_g[o], w_a[o], w_b[o]);
     inc += w_incl[o];
-    kfix_push(F, w_zlead[o], w_c[o], w_seen[o] != 0u);
   }
-  s_sum[grp][lane] = sum + F.f0;
-  s_g[grp][lane] = F.g;
-  s_a[grp][lane] = F.a;
-  s_b[grp][lane] = F.b;
+  s_s[grp][lane] = S.s;
+  s_g[grp][lane] = S.g;
+  s_a[grp][lane] = S.a;
+  s_b[grp][lane] = S.b;
   s_inc[grp][lane] = inc;
   __syncthreads();
   if (grp != 0) return;
-  uint64_t C = 0, total = 0, incl = 0;
+  KSum T = ksum_identity();
+  uint64_t incl = 0;
   for (int g = 0; g < KFIX_GROUPS; ++g) {
-    total += s_sum[g][lane] + s_g[g][lane] * C;
-    C = s_a[g][lane] + (s_b[g][lane] ? C : 0ull);
+    ksum_push(T, s_s[g][lane], s_g[g][lane], s_a[g][lane], s_b[g][lane]);
     incl += s_inc[g][lane];
   }
   if (lane < nl) {
-    tot[(size_t)field * cap + set0 + lane] += total;
+    tot[(size_t)field * cap + set0 + lane] += T.s;  // carry 0 into the stream
     if (add_incl) tot[(size_t)KF_INCL * cap + set0 + lane] = incl;
   }
 }
@@ -392,7 +430,7 @@ template <bool LDS>
 static int set_kwalk_attr() {
   static bool done = false;
   if (LDS && !done) {
-    const int mx = 160 * 1024;
+    const int mx = 160 * 1024 - (int)KW_STATIC_LDS;
     VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk<LDS, false>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, mx));
     VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk<LDS, true>,
@@ -406,28 +444,23 @@ static int set_kwalk_attr() {
 static int walk_stream(bool tie, const uint32_t* codes, const uint32_t* sflag, const uint32_t* aux,
                        int64_t M, const KendallWs& W, int64_t n, int64_t total, int field,
                        bool add_incl, int64_t cap, const KCfg& cfg, hipStream_t st) {
+  if (cfg.use_lds) VR_TRY(set_kwalk_attr<true>());
+  auto walk = [&](const uint64_t* mk, int nl) {
+    const size_t lds = cfg.use_lds ? cfg.lds : 0;
+    auto* k = cfg.use_lds ? (tie ? k_kwalk<true, true> : k_kwalk<true, false>)
+                          : (tie ? k_kwalk<false, true> : k_kwalk<false, false>);
+    k<<<cfg.grid, KW_THREADS, lds, st>>>(codes, sflag, aux, M, mk, n, nl, (uint32_t)cfg.nwaves, W.w_acc, W.w_g,
+                                         W.w_a, W.w_b, W.w_incl);
+  };
   for (int64_t set0 = 0, p = 0; set0 < total; set0 += LANES, ++p) {
     const int nl = (int)std::min<int64_t>(LANES, total - set0);
-    const uint64_t* mk = W.masks + (size_t)p * (size_t)n;
-    if (cfg.use_lds) {
-      VR_TRY(set_kwalk_attr<true>());
-      if (tie)
-        k_kwalk<true, true><<<cfg.grid, KW_THREADS, cfg.lds, st>>>(codes, sflag, aux, M, mk, n, nl, cfg.nwaves,
-                                                                  W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl);
-      else
-        k_kwalk<true, false><<<cfg.grid, KW_THREADS, cfg.lds, st>>>(codes, sflag, aux, M, mk, n, nl, cfg.nwaves,
-                                                                   W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl);
-    } else {
-      if (tie)
-        k_kwalk<false, true><<<cfg.grid, KW_THREADS, 0, st>>>(codes, sflag, aux, M, mk, n, nl, cfg.nwaves,
-                                                             W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl);
-      else
-        k_kwalk<false, false><<<cfg.grid, KW_THREADS, 0, st>>>(codes, sflag, aux, M, mk, n, nl, cfg.nwaves,
-                                                              W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl);
+    {
+      KtScope kt(KT_KWALK, (double)M, st);  // the walk only, not its fix-up
+      walk(W.masks + (size_t)p * (size_t)n, nl);
+      VR_CHECK_LAUNCH();
     }
-    VR_CHECK_LAUNCH();
-    k_kfix<<<1, KW_THREADS, 0, st>>>(W.w_acc, W.w_zlead, W.w_c, W.w_seen, W.w_incl, (uint32_t)cfg.nwaves,
-                                     nl, field, add_incl ? 1 : 0, W.tot, cap, set0);
+    k_kfix<<<1, KW_THREADS, 0, st>>>(W.w_acc, W.w_g, W.w_a, W.w_b, W.w_incl, (uint32_t)cfg.grid, nl, field,
+                                     add_incl ? 1 : 0, W.tot, cap, set0);
     VR_CHECK_LAUNCH();
   }
   return VR_OK;
