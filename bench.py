@@ -55,7 +55,8 @@ from visreps_amd.models.utils import FeatureExtractor
 from visreps_amd._lib import KTIMER_KERNELS, check, ktimer_enable, ktimer_read, lib, stream_of
 from visreps_amd.analysis._random import draw_bootstrap_indices
 from visreps_amd.pipeline import (KERNELS, PlanPrefetch, ShardedRDMs, StepTimes, all_units_rsa, engine_bytes,
-                                  engine_call_bytes, engine_pair_bytes, make_schedule, phase1_rows, phase1_select)
+                                  engine_call_bytes, engine_pair_bytes, engine_tri, make_schedule, phase1_rows,
+                                  phase1_select)
 
 METRIC = "end-to-end RSA eval sec (extract→RDM→1000-bootstrap Spearman), N=10k stimuli"
 LAYERS = ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
@@ -143,11 +144,11 @@ def pmc_traffic(n: int, est: bool):
     return d
 
 
-def kernel_table(kt: dict, steps: int, est: bool) -> dict:
+def kernel_table(kt: dict, steps: int, est: bool, tri: bool = False) -> dict:
     """Per hot kernel over the timed steps (vr_ktimer): ms and launches per step, average
     launch time, and for the engine kernels the algorithmic bytes per launch and GB/s."""
-    a_b, b_b, j_b = engine_pair_bytes(est)
-    bpp = {"k_rankB_est": engine_pair_bytes(True)[1], "k_rankB_full": engine_pair_bytes(True)[1],
+    a_b, b_b, j_b = engine_pair_bytes(est, tri)
+    bpp = {"k_rankB_est": engine_pair_bytes(True, tri)[1], "k_rankB_full": engine_pair_bytes(True, tri)[1],
            "k_rankB_exact": engine_pair_bytes(False)[1],
            "k_rankA": 4 + 128, "k_countA": 4, "k_join": j_b}  # k_rankA: codes 4 + TB row write 128
     out = {}
@@ -540,8 +541,9 @@ def main():
         gram_tf = times.gram_flops / (times.gram_ms / 1e3) / 1e12 if times.gram_ms else 0.0
         est = os.environ.get("VISREPS_ENGINE_EST") != "0"
         pmc = pmc_traffic(N, est)
-        a_b, b_b, j_b = engine_pair_bytes(est)
-        kernels = kernel_table(kt, args.steps, est)
+        tri = engine_tri(N, est)
+        a_b, b_b, j_b = engine_pair_bytes(est, tri)
+        kernels = kernel_table(kt, args.steps, est, tri)
         # `roofline`: the dominant kernel, k_rankB (the B-side rank walk), priced per launch:
         # its algorithmic bytes (pairs walked x B/pair) / its HIP-event launch time
         rb = kernels["k_rankB_est" if est else "k_rankB_exact"]
@@ -549,11 +551,14 @@ def main():
         roof = {"bound": "hbm", "achieved": rb["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(rb["gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": round(rb_pmc["bytes_per_launch"]) if rb_pmc else None,
-                "kernel": ("k_rankB, " + ("EST 3 form" if est else "exact chunk-base form")
-                           + ": B-side rank walk of one unit over one pass of 64 bootstrap subsets "
-                           "(the full-set pass 0 and phase-1 launches are k_rankB_full in kernels_per_step)"),
+                "kernel": ("k_rankB, " + ("EST 5 form (triangle-order TB)" if tri else "EST 3 form" if est
+                                          else "exact chunk-base form")
+                           + ": B-side rank walk of one unit over one pass of %d bootstrap subsets " % (63 if tri else 64)
+                           + "(the full-set pass 0 and phase-1 launches are k_rankB_full in kernels_per_step)"),
                 "algorithmic_bytes_per_launch": round(rb["bytes_per_launch"]),
-                "algorithmic_bytes_model": (f"{b_b} B per pair: codes 4 + A position 4 (streams"
+                "algorithmic_bytes_model": (f"{b_b} B per pair: codes 4 (stream; the row is the pair's triangle "
+                                            "index) + 128 B TB row gather (lane 63: the coarse A position)" if tri else
+                                            f"{b_b} B per pair: codes 4 + A position 4 (streams"
                                             + (" + window low end 4" if b_b > 136 else "; the window low end is "
                                                "computed from the A position") + ") + 128 B TB row gather" if est else
                                             f"{b_b} B per pair: codes, A position, A chunk 4 each + 128 B TB "

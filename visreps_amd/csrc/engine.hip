@@ -406,12 +406,48 @@ struct EstLo {
   int bits;
   float L, R;
   uint32_t Lu, Ru;
+  uint32_t sh;  // EST 6: the coarse A position is pos >> sh
+  uint32_t g;   // EST 5: lane 63 holds the EST 3 low end + 2^15, >> g
 };
+
+// 32-bit triangle index of pair code (a << 16) | b (M < 2^32: a n < 2^32, a (a + 1) < 2^32)
+__device__ inline uint32_t tri32(uint32_t code, uint32_t n) {
+  const uint32_t a = code >> 16, b = code & 0xffffu;
+  return a * n - ((a * (a + 1u)) >> 1) + b - a - 1u;
+}
+
+// EST 5 / 6 (the triangle-order TB, VISREPS_ENGINE_TRI): the TB row of a pair sits at its
+// triangle index and lane 63 holds a 16-bit tag of its A position pos from which both walks
+// evaluate the same window low end (monotone non-decreasing in pos, like EST 3):
+//  EST 5  tag = (EST 3 low end + 2^15) >> g, low end = (tag << g) - 2^15: the EST 3 window
+//         rounded down to a multiple of 2^g (g = 11 at N = 10k: <= 2047 of the 2^15 slack),
+//         one shift and one subtract on the B side;
+//  EST 6  (the pass holding the full set in lane 0) tag = pos >> sh, the EST 4 low ends at the
+//         middle of the coarse interval.
+__device__ inline uint32_t est5_u(const EstLo& e, uint32_t pos) { return 1u + __umulhi(pos << 1, e.Ru); }
+__device__ inline uint32_t est5_lo_tag(const EstLo& e, uint32_t tag) { return (tag << e.g) - 32768u; }
+template <int EST>
+__device__ inline uint32_t tri_tag(const EstLo& e, uint32_t pos) {
+  return EST == 5 ? est5_u(e, pos) >> e.g : pos >> e.sh;
+}
+__device__ inline uint32_t est_lo_pc(const EstLo& e, uint32_t pc, int lane, bool full_lane0) {
+  const uint32_t mid = (pc << e.sh) + ((1u << e.sh) >> 1);
+  const uint32_t lo = e.Lu + __umulhi(mid << 1, e.Ru);  // wave-uniform (scalar) arithmetic
+  if (!full_lane0) return lo;
+  // lane 0 (the full set): + the uniform difference of its low end, masked to lane 0 --
+  // two VALU ops on scalar operands, no per-lane branch
+  const uint32_t d0 = 2u * mid + (1u - 32768u) - lo;
+  return lo + (d0 & (0u - (uint32_t)(lane == 0)));
+}
 // EST 4: EST 3 with lane 0 holding the full set (pass 0 of a full_first call): its count
 // before A position pos is pos itself, so its low end is 2 pos + 1 - 2^15.
 template <int EST>
 __device__ inline uint32_t est_lo_t(const EstLo& e, uint32_t pos, int lane) {
-  if constexpr (EST == 4)
+  if constexpr (EST == 5)
+    return est5_lo_tag(e, est5_u(e, pos) >> e.g);
+  else if constexpr (EST == 6)
+    return est_lo_pc(e, pos >> e.sh, lane, true);
+  else if constexpr (EST == 4)
     return lane == 0 ? 2u * pos + (1u - 32768u) : e.Lu + __umulhi(pos << 1, e.Ru);
   else if constexpr (EST == 3)
     return e.Lu + __umulhi(pos << 1, e.Ru);
@@ -422,10 +458,14 @@ __device__ inline uint32_t est_lo_t(const EstLo& e, uint32_t pos, int lane) {
 }
 template <int EST>
 __device__ inline EstLo est_setup(const uint2* __restrict__ gtab, uint32_t rows, int bits, uint2* smem) {
-  EstLo e{nullptr, bits, 0.f, 0.f, 0u, 0u};
+  EstLo e{nullptr, bits, 0.f, 0.f, 0u, 0u, 0u, 0u};
   if constexpr (EST >= 3) {
     e.Lu = wave_uniform(sload(&gtab->x));
     e.Ru = wave_uniform(sload(&gtab->y));
+    if constexpr (EST >= 5) {
+      e.sh = wave_uniform(sload(&gtab[1].x));
+      e.g = wave_uniform(sload(&gtab[1].y));
+    }
   } else if constexpr (EST == 2) {
     const uint2 v = gtab[threadIdx.x & 63];
     e.L = __uint_as_float(v.x);
@@ -500,8 +540,12 @@ __global__ void k_c0(const uint32_t* __restrict__ c0rel, const uint32_t* __restr
   ftab[(size_t)c * LANES + lane] = make_uint2(2u * a + 1u - 32768u, (uint32_t)((2 * d) >> EST_STEP_BITS));
 }
 
-// EST 3: the wave-uniform estimate {L, R} (est3_params) into ftab row 0 for the A side
-__global__ void k_c0_u(uint32_t Lu, uint32_t Ru, uint2* __restrict__ ftab) { ftab[0] = make_uint2(Lu, Ru); }
+// EST 3 / 5: the wave-uniform estimate {L, R} (est3_params) into ftab row 0, EST 5's coarse
+// position shift into row 1
+__global__ void k_c0_u(uint32_t Lu, uint32_t Ru, uint32_t sh, uint32_t g, uint2* __restrict__ ftab) {
+  ftab[0] = make_uint2(Lu, Ru);
+  ftab[1] = make_uint2(sh, g);
+}
 
 // EST 3 estimate of a call whose subsets all hold k stimuli: M' = k (k - 1) / 2 included
 // pairs per lane, R = floor(2^32 M'/M) (host and device use these same two words; a lane
@@ -553,6 +597,21 @@ __device__ inline void store_rows_est(uint16_t* __restrict__ TB, uint32_t stride
   for (; i < cnt; ++i, row += stride) tb_store((uint16_t)y, row);
 }
 
+// EST 5 / 6: the same rows at their triangle indices (row_t(r) for A position r), lane 63 of
+// each row holding the row's coarse A position r >> sh instead of a rank
+template <int EST, typename RowT>
+__device__ inline void store_rows_tri(uint16_t* __restrict__ TB, uint32_t r0, uint32_t cnt, int lane,
+                                      uint32_t y, const EstLo& el, bool& bad, RowT&& row_t) {
+  if (cnt == 0) return;
+  if (VR_EST_CHECK && (r0 >> 6) != ((r0 + cnt - 1u) >> 6))
+    bad |= est_bad(y, est_lo_t<EST>(el, r0, lane)) || est_bad(y, est_lo_t<EST>(el, r0 + cnt - 1u, lane));
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const uint32_t r = r0 + i;
+    const uint16_t v = lane == LANES - 1 ? (uint16_t)tri_tag<EST>(el, r) : (uint16_t)y;
+    tb_store(v, TB + (size_t)row_t(r) * LANES + lane);
+  }
+}
+
 // A side. Exact form (EST false): chunk-relative doubled ranks y - 2 lp (u16 or u32) and
 // the chunk-start counts lpA for baseA. EST form: absolute doubled ranks modulo 2^16,
 // each checked against the count estimate the B side will use.
@@ -564,11 +623,21 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
     uint32_t* __restrict__ lpA, uint32_t* __restrict__ seg_tot, uint64_t* __restrict__ seg_part,
     uint32_t nseg, EstA est) {
   static_assert(!EST || sizeof(TBT) == 2, "EST ranks are u16");
+  constexpr bool TRI = EST >= 5;  // triangle-order TB rows (EST 5 / 6)
+  static_assert(!TRI || FULL, "triangle-order passes use whole 64-lane rows");
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
-  EstLo el{nullptr, 0, 0.f, 0.f, 0u, 0u};
+  EstLo el{nullptr, 0, 0.f, 0.f, 0u, 0u, 0u, 0u};
   if constexpr (EST != 0)
     el = est_setup<EST>(est.ftab, est.tabrows, est.bits, reinterpret_cast<uint2*>(smask + (LDS ? n : 0)));
+  // TRI: triangle index and lane-63 tag of each position of window wt (lane j: position
+  // wt + j), computed once per window in the vector unit; rows of a tie group that began in
+  // an earlier window get theirs from their code (scalar loads)
+  uint32_t tl = 0, tg = 0, wt = 0;
+  auto row_t = [&](uint32_t r) -> uint32_t {
+    return r - wt < 64u ? readlane_u32(tl, r - wt) : tri32(sload(codes + r), (uint32_t)n);
+  };
+  (void)row_t;
   const int lane = threadIdx.x & 63;
   const bool active = FULL || lane < lw;
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
@@ -597,7 +666,10 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
     auto close = [&](uint32_t xe, uint32_t ce) {
       tie_add<BIGT>(tie, tie_big, ce - cgs);
       if (active) {
-        if constexpr (EST)
+        if constexpr (TRI)
+          store_rows_tri<EST>(reinterpret_cast<uint16_t*>(TB), gs, xe - gs, lane, y0 + cgs + ce + 1u, el, bad,
+                              row_t);
+        else if constexpr (EST)
           store_rows_est<EST>(reinterpret_cast<uint16_t*>(TB), stride, gs, xe - gs, lane, y0 + cgs + ce + 1u,
                               el, bad);
         else
@@ -617,6 +689,11 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
     uint32_t cd = (w0 + lane >= P0 && w0 + lane < P1) ? codes[w0 + lane] : 0u;
     uint32_t f0 = sload(gflag + (w0 >> 5)), f1 = sload(gflag + (w0 >> 5) + 1);
     for (; w0 < P1; w0 += 64) {
+      if constexpr (TRI) {
+        tl = (w0 + lane >= P0 && w0 + lane < P1) ? tri32(cd, (uint32_t)n) : 0u;
+        tg = tri_tag<EST>(el, w0 + (uint32_t)lane);
+        wt = w0;
+      }
 #if VR_PROBE_WBA  // timing probe only (wrong scores): k_rankA without mask lookups / transposes
       const uint64_t x = active ? (0xF7DFBEFDFBF7EFDFull ^ ((uint64_t)(cd & 7u) << 3)) : 0ull;
 #else
@@ -645,6 +722,16 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
         if (cn >= sg.c1 || pn > w0 + 63u) {
           uint32_t t = EST ? y0 + 2u * cw + 1u : 2u * (cw - lp) + 1u;
           TBT* row = TB + (size_t)w0 * stride + lane;
+          if constexpr (TRI) {
+#pragma unroll
+            for (int j = 0; j < 63; ++j) {
+              const uint32_t bit = (uint32_t)(x >> j) & 1u;
+              const uint32_t v = t + bit;
+              const uint32_t pc = readlane_u32(tg, j);
+              tb_store((TBT)(lane == LANES - 1 ? pc : v), TB + (size_t)readlane_u32(tl, j) * LANES + lane);
+              t = v + bit;
+            }
+          } else {
 #if VR_PROBE_STW  // timing probe only (wrong TB layout): one 4-byte store per two rows
           uint32_t* row2 = reinterpret_cast<uint32_t*>(TB + (size_t)w0 * stride) + lane;
 #pragma unroll
@@ -664,6 +751,7 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
             t = v + bit;
           }
 #endif
+          }
           gs = w0 + 63u;
           cgs = cw + popc64(x & lowmask(63));
           F = 0;
@@ -942,8 +1030,12 @@ constexpr int EPS = VR_EST_PIPE;
 // B side: the window low end of pair j of the window (lane j of pa / la holds pair j). EST 3
 // and 4 read the join's precomputed value (EST 4's lane 0: 2 posA + 1 - 2^15).
 template <int EST>
-__device__ inline uint32_t est_lo_b(const EstLo& el, uint32_t pa, uint32_t la, int j, int lane) {
-  if constexpr (EST == 4) {
+__device__ inline uint32_t est_lo_b(const EstLo& el, uint32_t pa, uint32_t la, int j, int lane, uint32_t tv) {
+  if constexpr (EST == 5) {  // the tag in lane 63 of the gathered row (tv: this pair's loaded entry)
+    return est5_lo_tag(el, readlane_u32(tv, LANES - 1));
+  } else if constexpr (EST == 6) {
+    return est_lo_pc(el, readlane_u32(tv, LANES - 1), lane, true);
+  } else if constexpr (EST == 4) {
     const uint32_t l = readlane_u32(la, j);
     const uint32_t l0 = 2u * readlane_u32(pa, j) + (1u - 32768u);
     return lane == 0 ? l0 : l;
@@ -981,7 +1073,7 @@ __device__ inline void pipe_batch(const uint16_t* __restrict__ TB, uint32_t stri
   uint32_t y[EBB];
 #pragma unroll
   for (int q = 0; q < EBB; ++q)
-    y[q] = est_recover(t[H % EPS][q], est_lo_b<EST>(el, pa, la, H * EBB + q, lane));
+    y[q] = est_recover(t[H % EPS][q], est_lo_b<EST>(el, pa, la, H * EBB + q, lane, t[H % EPS][q]));
   fn(H, y);
   if constexpr (H + 1 < NBT) pipe_batch<EST, H + 1>(TB, stride, el, pa, la, lane_bt, lane, t, fn);
 }
@@ -1021,7 +1113,7 @@ __device__ inline void gather_window_est(const uint16_t* __restrict__ TB, uint32
     }
 #pragma unroll
     for (int q = 0; q < EBB; ++q)  // EST 3: the join's precomputed low end (lane j = pair j)
-      t[q] = est_recover(t[q], est_lo_b<EST>(el, pa, la, h * EBB + q, lane));
+      t[q] = est_recover(t[q], est_lo_b<EST>(el, pa, la, h * EBB + q, lane, t[q]));
     fn(h, t);
   }
 }
@@ -1076,7 +1168,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
   constexpr int NB = EST ? EBB : BB;  // pairs per gather batch
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
-  EstLo el{nullptr, 0, 0.f, 0.f, 0u, 0u};
+  EstLo el{nullptr, 0, 0.f, 0.f, 0u, 0u, 0u, 0u};
   if constexpr (EST != 0) el = est_setup<EST>(ftab, tabrows, bits, reinterpret_cast<uint2*>(smask + (LDS ? n : 0)));
   const int lane = threadIdx.x & 63;
   const bool active = FULL || lane < lw;
@@ -1106,6 +1198,14 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
                      uint32_t& f1) {
       const uint32_t pos = w + (uint32_t)lane;
       const bool valid = pos >= P0 && pos < P1;
+      if constexpr (EST >= 5) {  // triangle-order TB: the row is the pair's triangle index
+        cd = valid ? codes[pos] : 0u;
+        pa = valid ? tri32(cd, (uint32_t)n) : 0u;
+        ca = 0u;
+        f0 = sload(gflag + (w >> 5));
+        f1 = sload(gflag + (w >> 5) + 1);
+        return;
+      }
       pa = valid ? posA_byB[pos] : 0u;
       // EST 3/4: the window low end of the pair's A position, L + (2 posA R >> 32), computed
       // here per lane for the window's 64 pairs (three VALU ops per window lane, no stream),
@@ -1368,7 +1468,7 @@ static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const
 // pre-pass reads the masks from LDS when they fit (CL), the rank walk from L2.
 template <int EM, bool CL, bool FULL, bool BTA>
 static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, int nl, const EngineCfg& cfg,
-                      uint2 e3, uint32_t* viol, hipStream_t st) {
+                      uint2 e3, uint2 tri, uint32_t* viol, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     VR_TRY(allow_big_lds(k_countA<CL, FULL>));
@@ -1388,7 +1488,7 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
   }
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
   if constexpr (EM >= 3)
-    k_c0_u<<<1, 1, 0, st>>>(e3.x, e3.y, E.ftab);
+    k_c0_u<<<1, 1, 0, st>>>(e3.x, e3.y, tri.x, tri.y, E.ftab);
   else if constexpr (EM == 2)
     k_c0_lin<<<1, LANES, 0, st>>>(E.totA, M, E.ftab);
   else
@@ -1420,7 +1520,7 @@ static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* c
   const uint32_t nseg = (uint32_t)(EST ? cfg.est_nwaves : cfg.nwaves);
   const size_t us = (size_t)E.useg * (size_t)u;
   {
-    KtScope kt(EST == 4 ? KT_RANKB_FULL : EST ? KT_RANKB_EST : KT_RANKB_EXACT, (double)M, st);
+    KtScope kt(EST == 4 || EST == 6 ? KT_RANKB_FULL : EST ? KT_RANKB_EST : KT_RANKB_EXACT, (double)M, st);
     k_rankB<LDS, FULL, TBT, BTB, EST><<<EST ? cfg.est_grid : cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
         B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
         posA_byB, chunkA_byB, E.baseA, E.segB_tot + us, E.segB_part + us * PB_N, nseg, E.ftab,
@@ -1481,9 +1581,9 @@ static int with_pass_tag(bool lds, bool full, bool narrow, Fn&& fn) {
 // entries of lanes 1..63 of one pair row -- a B-side recovery error the A walk's checks
 // cannot see. The tail's invariants must flag the pass and the exact re-run must restore
 // every score (tests/test_engine_est.py).
-__global__ void k_inject_tb(uint16_t* __restrict__ TB, uint32_t row, int lw) {
+__global__ void k_inject_tb(uint16_t* __restrict__ TB, uint32_t row, int stride, int lanes) {
   const int lane = threadIdx.x;
-  if (lane >= 1 && lane < lw) TB[(size_t)row * lw + lane] += 1u;
+  if (lane >= 1 && lane < lanes) TB[(size_t)row * stride + lane] += 1u;
 }
 
 static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t nb, int64_t n,
@@ -1533,17 +1633,32 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
     second = mode;
     return VR_OK;
   };
+  // EST 5 / 6 (the default EST 3 / 4 passes while M <= 2^28; VISREPS_ENGINE_TRI=0 keeps the
+  // A-order TB): the A walk writes each pair's 128-B row at its triangle index, lane 63
+  // holding the coarse A position, so the B walk finds the row from its own pair codes --
+  // no per-unit join, no A-position / low-end streams (132 instead of 140 B per pair) -- at
+  // the price of scattered (instead of sequential) row writes in the A walk and 63 subsets
+  // per pass. Flagged passes re-run in the exact form, which joins on demand.
+  const bool tri = est && cfg.est_mode == 3 && lw == LANES && M <= ((int64_t)1 << 28) &&
+                   env_int("VISREPS_ENGINE_TRI", 1) != 0;
+  // EST 6 coarse position pos >> sh and EST 5 tag (low end + 2^15) >> g: both 16 bits
+  uint32_t sh = 0, g = 0;
+  while (((uint64_t)(M - 1) >> sh) >= 65536u) ++sh;
+  {
+    const uint64_t umax = 1u + (uint32_t)(((uint64_t)(2u * (uint32_t)(M - 1)) * e3.y) >> 32);
+    while ((umax >> g) >= 65536u) ++g;
+  }
+  const uint2 trip = make_uint2(sh, g);
   // EST 3: the join precomputes the window low ends (JOIN_LO), the B walk streams them;
   // VISREPS_ENGINE_LO_JOIN=0 has the walk compute them from the A positions instead (4 B
   // fewer per pair and pass, but measured no faster: 1367 vs 1359 us per k_rankB launch,
   // profiles/r3_engine_lo_ab.log)
-  const bool lo_join = cfg.est_mode == 3 && env_int("VISREPS_ENGINE_LO_JOIN", 1) != 0;
-  VR_TRY(join(!est ? JOIN_CHUNK : (lo_join ? JOIN_LO : JOIN_NONE)));
-  // the exact chunk-base form of the pass starting at subset set0
-  auto exact_pass = [&](auto tag, int64_t set0) -> int {
+  const bool lo_join = !tri && cfg.est_mode == 3 && env_int("VISREPS_ENGINE_LO_JOIN", 1) != 0;
+  if (!tri) VR_TRY(join(!est ? JOIN_CHUNK : (lo_join ? JOIN_LO : JOIN_NONE)));
+  // the exact chunk-base form of subsets [set0, set0 + nl), nl <= lw
+  auto exact_pass = [&](auto tag, int64_t set0, int nl) -> int {
     using Tg = decltype(tag);
     using TBT = typename Tg::tbt;
-    const int nl = (int)std::min<int64_t>(lw, total - set0);
     VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
     VR_TRY((bigA ? pass_a<Tg::lds, Tg::full, TBT, true>(A, n, E, lw, cfg, st)
                  : pass_a<Tg::lds, Tg::full, TBT, false>(A, n, E, lw, cfg, st)));
@@ -1557,13 +1672,18 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
     return tail_units(E, nb, (uint32_t)cfg.nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0, score_ld, xbad,
                       st);
   };
-  if (!est) {
+  // subsets [s0, total) in exact passes of lw
+  auto exact_from = [&](int64_t s0) -> int {
+    if (second != JOIN_CHUNK) VR_TRY(join(JOIN_CHUNK));
     return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
-      for (int64_t set0 = 0; set0 < total; set0 += lw) VR_TRY(exact_pass(tag, set0));
+      for (int64_t set0 = s0; set0 < total; set0 += lw)
+        VR_TRY(exact_pass(tag, set0, (int)std::min<int64_t>(lw, total - set0)));
       return VR_OK;
     });
-  }
-  const int64_t npass = (total + lw - 1) / lw;
+  };
+  if (!est) return exact_from(0);
+  const int64_t sub = tri ? LANES - 1 : lw;  // subsets per EST pass
+  const int64_t npass = (total + sub - 1) / sub;
   const int64_t pfirst = 0;
   // The first EST pass runs alone: when the estimate cannot hold these A ranks (strongly
   // structured RDMs, giant tie groups) every pass is run in the exact form from there on.
@@ -1576,34 +1696,43 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
       using Tg = decltype(tag);
       if constexpr (sizeof(typename Tg::tbt) == 2) {
         for (int64_t p = p0; p < p1; ++p) {
-          const int64_t set0 = p * lw;
-          const int nl = (int)std::min<int64_t>(lw, total - set0);
+          const int64_t set0 = p * sub;
+          const int nl = (int)std::min<int64_t>(sub, total - set0);
           VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
           uint32_t* viol = E.viol + (p - p0);
           auto run_pass = [&](auto em) -> int {
             constexpr int EM = decltype(em)::value;
-            VR_TRY((bigA ? pass_a_est<EM, Tg::lds, Tg::full, true>(A, n, E, lw, nl, cfg, e3, viol, st)
-                         : pass_a_est<EM, Tg::lds, Tg::full, false>(A, n, E, lw, nl, cfg, e3, viol, st)));
-            if (p == inject) {
-              k_inject_tb<<<1, LANES, 0, st>>>(static_cast<uint16_t*>(E.TB), (uint32_t)(M / 2), lw);
-              VR_CHECK_LAUNCH();
+            if constexpr (EM >= 5 && !Tg::full) {
+              return VR_OK;  // (never taken: triangle-order passes are whole 64-lane rows)
+            } else {
+              VR_TRY((bigA ? pass_a_est<EM, Tg::lds, Tg::full, true>(A, n, E, lw, nl, cfg, e3, trip, viol, st)
+                           : pass_a_est<EM, Tg::lds, Tg::full, false>(A, n, E, lw, nl, cfg, e3, trip, viol, st)));
+              if (p == inject) {
+                k_inject_tb<<<1, LANES, 0, st>>>(static_cast<uint16_t*>(E.TB), (uint32_t)(M / 2), lw,
+                                                 (int)std::min<int64_t>(lw, sub));
+                VR_CHECK_LAUNCH();
+              }
+              for (int64_t j = 0; j < nb; ++j) {
+                // EST 3/4: A positions and streamed low ends; EST 5/6: neither
+                const uint32_t* pj = EM >= 5 ? nullptr : joins[2 * j];
+                const uint32_t* lj = EM >= 3 && EM <= 4 && lo_join ? joins[2 * j + 1] : nullptr;
+                VR_TRY((h[(size_t)j + 1].max_group >= 65536u
+                            ? walk_b<Tg::lds, Tg::full, uint16_t, true, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)
+                            : walk_b<Tg::lds, Tg::full, uint16_t, false, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)));
+              }
+              return tail_units(E, nb, (uint32_t)cfg.est_nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0,
+                                score_ld, viol, st);
             }
-            for (int64_t j = 0; j < nb; ++j) {
-              const uint32_t* pj = joins[2 * j];
-              const uint32_t* lj = EM >= 3 && lo_join ? joins[2 * j + 1] : nullptr;  // EST 3/4: streamed low ends
-              VR_TRY((h[(size_t)j + 1].max_group >= 65536u
-                          ? walk_b<Tg::lds, Tg::full, uint16_t, true, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)
-                          : walk_b<Tg::lds, Tg::full, uint16_t, false, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)));
-            }
-            return tail_units(E, nb, (uint32_t)cfg.est_nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0,
-                              score_ld, viol, st);
           };
           // EST 3 needs every lane to hold k stimuli: the pass holding the full set runs EST 4
           const bool full0 = full_first && p == 0;
-          VR_TRY(cfg.est_mode == 3   ? (full0 ? run_pass(std::integral_constant<int, 4>{})
-                                              : run_pass(std::integral_constant<int, 3>{}))
-                 : cfg.est_mode == 2 ? run_pass(std::integral_constant<int, 2>{})
-                                     : run_pass(std::integral_constant<int, 1>{}));
+          if (tri)
+            VR_TRY(full0 ? run_pass(std::integral_constant<int, 6>{}) : run_pass(std::integral_constant<int, 5>{}));
+          else
+            VR_TRY(cfg.est_mode == 3   ? (full0 ? run_pass(std::integral_constant<int, 4>{})
+                                                : run_pass(std::integral_constant<int, 3>{}))
+                   : cfg.est_mode == 2 ? run_pass(std::integral_constant<int, 2>{})
+                                       : run_pass(std::integral_constant<int, 1>{}));
         }
       }
       return VR_OK;
@@ -1616,15 +1745,11 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
       if (flags[(size_t)(p - p0)] & 2u) g_est_tail_flags.fetch_add(1);
       if (second != JOIN_CHUNK) VR_TRY(join(JOIN_CHUNK));
       g_est_reruns.fetch_add(1);
-      VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) { return exact_pass(tag, p * lw); }));
+      const int64_t set0 = p * sub;
+      const int nl = (int)std::min<int64_t>(sub, total - set0);
+      VR_TRY(with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) { return exact_pass(tag, set0, nl); }));
     }
-    if (p0 == pfirst && flags[0] && p1 < npass) {  // give up on the estimate for this call
-      if (second != JOIN_CHUNK) VR_TRY(join(JOIN_CHUNK));
-      return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
-        for (int64_t p = p1; p < npass; ++p) VR_TRY(exact_pass(tag, p * lw));
-        return VR_OK;
-      });
-    }
+    if (p0 == pfirst && flags[0] && p1 < npass) return exact_from(p1 * sub);  // give up on the estimate
   }
   return VR_OK;
 }

@@ -657,12 +657,27 @@ def engine_bytes(n: int, n_boot: int) -> float:
 # and the A positions and the window low ends the join precomputed (VISREPS_ENGINE_LO_JOIN=0:
 # computes them from the A positions instead); k_join reads the B codes, gathers the 4-B A
 # position map and writes the A positions and low ends, per unit.
-def engine_pair_bytes(est: Optional[bool] = None) -> Tuple[int, int, int]:
+def engine_tri(n: int, est: Optional[bool] = None) -> bool:
+    """Whether the bootstrap calls at n stimuli run the triangle-order EST passes (EST 5/6:
+    M <= 2^28, EST 3 estimate, VISREPS_ENGINE_TRI not 0; engine.hip run_engine_multi_impl)."""
+    import os
+
+    if est is None:
+        est = os.environ.get("VISREPS_ENGINE_EST") != "0"
+    return (est and os.environ.get("VISREPS_ENGINE_TRI", "1") != "0"
+            and os.environ.get("VISREPS_ENGINE_EST_MODE", "3") == "3" and n * (n - 1) // 2 <= (1 << 28))
+
+
+def engine_pair_bytes(est: Optional[bool] = None, tri: bool = False) -> Tuple[int, int, int]:
     """(A walk per pass, B walk per pass and unit, join per unit) bytes per pair."""
     import os
 
     if est is None:
         est = os.environ.get("VISREPS_ENGINE_EST") != "0"
+    if est and tri:
+        # triangle-order TB: A: codes 4 (count pre-pass) + codes 4 + TB row write 128 (at the
+        # pair's triangle index); B: codes 4 + TB row gather 128; no join
+        return 4 + 4 + 128, 4 + 128, 0
     if not est:
         # A: codes 4 + TB row write 128; B: codes, posA, chunkA 4 each + TB row 128;
         # join: B codes 4 + 8-B pair-map record + posA and chunkA writes 4 each
@@ -676,10 +691,11 @@ def engine_pair_bytes(est: Optional[bool] = None) -> Tuple[int, int, int]:
 
 def engine_call_bytes(n: int, subsets: int, units: int) -> float:
     """Algorithmic HBM bytes of one engine call: `units` B plans against one A plan over
-    `subsets` subsets (64 per pass)."""
-    a, b, j = engine_pair_bytes()
+    `subsets` subsets (64 per pass; 63 in the triangle-order form)."""
+    tri = engine_tri(n)
+    a, b, j = engine_pair_bytes(tri=tri)
     M = n * (n - 1) // 2
-    passes = -(-subsets // 64)
+    passes = -(-subsets // (63 if tri else 64))
     return float(M) * (passes * (a + units * b) + units * j)
 
 
