@@ -312,6 +312,26 @@ int vr_rdm_tiles_pack(const float* rdm, int64_t ldr, int64_t n, int64_t tile_beg
 int vr_rdm_tiles_unpack(const float* packed, int64_t n, int64_t tile_begin, int64_t tile_end,
                         float* rdm, int64_t ldr, void* stream);
 
+/* One RDM over stimulus-sharded rows behind the C ABI (SURVEY §8(b),(e)): rank `rank` of an
+ * RCCL communicator `comm` (ncclComm_t) holds rows_local <= ceil(n / world) consecutive
+ * stimulus rows X_local [dev] fp32 (row stride ldx), the ranks' blocks in rank order make
+ * the n rows. Block sizes, the split bf16 hi/lo plane records (+ row statistics) and the
+ * packed tile ranges are all-gathered over RCCL; each rank computes one tile range cut at
+ * the wide kernel's aligned boundaries (vr_rdm_sharded_range: bit-identical tiles to the
+ * one-GPU split-Gram launch), and every rank ends with the full RDM in rdm [dev] (ldr >= n).
+ * Collective: every rank calls it with the same n, d, world. RCCL is bound at run time
+ * (librccl.so.1, the copy torch loaded if any); vr_rccl_* create a communicator from it for
+ * callers without their own RCCL binding. No reference counterpart (single-GPU reference). */
+int vr_rccl_available(void);
+int vr_rccl_unique_id(void* out /* 128 bytes (ncclUniqueId) */);
+int vr_rccl_comm_init(void** comm, int world, const void* unique_id, int rank);
+int vr_rccl_comm_destroy(void* comm);
+int vr_rdm_sharded_range(int64_t n, int64_t d, int world, int rank, int64_t* tile_begin, int64_t* tile_end);
+size_t vr_rdm_sharded_workspace(int64_t n, int64_t d, int world);
+int vr_rdm_pearson_sharded(const float* X_local, int64_t rows_local, int64_t n, int64_t d, int64_t ldx, float* rdm,
+                           int64_t ldr, float correction, void* comm, int rank, int world, void* ws, size_t ws_bytes,
+                           void* stream);
+
 /* ------------------------------------------------------------------------------
  * Image preprocessing: the eval loaders' get_transform (visreps/dataloaders/obj_cls.py:
  * 27-45) = torchvision Resize(resize, BILINEAR) on a PIL image (Pillow's ImagingResample:

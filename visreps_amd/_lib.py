@@ -161,6 +161,18 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _vp, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _c_i64, _c_i64, _vp, _c_sz, _vp],
     ),
+    "vr_rccl_available": (ctypes.c_int, []),
+    "vr_rccl_unique_id": (ctypes.c_int, [_vp]),
+    "vr_rccl_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, _vp, ctypes.c_int]),
+    "vr_rccl_comm_destroy": (ctypes.c_int, [_vp]),
+    "vr_rdm_sharded_range": (ctypes.c_int, [_c_i64, _c_i64, ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "vr_rdm_sharded_workspace": (_c_sz, [_c_i64, _c_i64, ctypes.c_int]),
+    "vr_rdm_pearson_sharded": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _vp, ctypes.c_int, ctypes.c_int, _vp,
+         _c_sz, _vp],
+    ),
     "vr_rdm_tiles_pack": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _vp]),
     "vr_rdm_tiles_unpack": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp]),
     "vr_transform_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_int]),
