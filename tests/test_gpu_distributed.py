@@ -150,3 +150,49 @@ def test_bench_extract_split_equals_fp32_path(dev, monkeypatch):
         got = torch.empty((n, n), device=dev)
         P.KERNELS.tiles_from_planes(split[p], n, got, 0, total, 1e-12)
         assert torch.equal(got, one), p
+
+
+def _gloo_rdm_worker(rank, world, port, n, d, out_dir):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(30000)
+    x = torch.relu(torch.randn(n, d, device=dev, generator=g))  # the same rows on every rank
+    rows = shard_rows(n, rank, world)
+    x_local = x[rows.start:rows.stop].clone()
+    if rank != 0:
+        del x
+    torch.cuda.empty_cache()
+    got = P.distributed_rdm(x_local, n, dist.group.WORLD)
+    del x_local
+    if rank == 0:
+        one = torch.empty((n, n), dtype=torch.float32, device=dev)
+        P.KERNELS.tiles_from_rows(x, one, 0, int(lib().vr_rdm_tile_count(n)), 1e-12)
+        equal = bool(torch.equal(got, one))
+        with open(os.path.join(out_dir, "equal.txt"), "w") as f:
+            f.write(f"{int(equal)} {n} {d}\n")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_distributed_rdm_30k_on_one_gpu(dev, tmp_path):
+    """distributed_rdm (pipeline.ShardedRDMs: row exchange to the owners, aligned
+    pieces, packed piece exchange) at world 2 -- both ranks on this GPU over gloo, the
+    orchestration RCCL runs on the 8-GPU node -- at 30,000 x 43,264 (5.2 GB of rows, 3.6 GB
+    RDM): torch.equal with the one-launch RDM."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    n, d = 30000, 43264
+    mp.spawn(_gloo_rdm_worker, args=(2, port, n, d, str(tmp_path)), nprocs=2, join=True)
+    flag, n_, d_ = open(tmp_path / "equal.txt").read().split()
+    assert flag == "1" and int(n_) == n and int(d_) == d
