@@ -193,14 +193,14 @@ def structured_est_probe(n: int, plan_b, dev) -> dict:
         try:
             R.bootstrap_spearman_multi(plan_a, [plan_b], idx, full_first=True)  # warm
             torch.cuda.synchronize()
-            r0 = int(L.vr_engine_est_reruns())
+            r0, q0 = int(L.vr_engine_est_reruns()), int(L.vr_engine_est_predicted())
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             sc = R.bootstrap_spearman_multi(plan_a, [plan_b], idx, full_first=True)
             e1.record()
             torch.cuda.synchronize()
             out[form] = {"unit_ms": round(e0.elapsed_time(e1), 2), "reruns": int(L.vr_engine_est_reruns()) - r0,
-                         "point": float(sc[0, 0])}
+                         "predicted_exact": int(L.vr_engine_est_predicted()) - q0, "point": float(sc[0, 0])}
             all_scores[form] = sc.cpu().numpy()
         finally:
             if old is None:
@@ -212,7 +212,9 @@ def structured_est_probe(n: int, plan_b, dev) -> dict:
     out["scores_equal"] = bool(np.array_equal(all_scores["est"], all_scores["exact"]))
     out["scores_compared"] = int(all_scores["est"].size)
     out["note"] = ("neural RDM d_ab = u_a + u_b + 0.05 noise, u ~ Exp(1)^2, vs the V1 neural plan of the bench: "
-                   "EST passes the A side flags are re-run exact (est.reruns); exact = VISREPS_ENGINE_EST=0")
+                   "EST passes the A side flags are re-run exact (est.reruns); a call whose first-pass A counts "
+                   "already break the EST 3 window runs exact from the start (est.predicted_exact, no EST pass "
+                   "spent); exact = VISREPS_ENGINE_EST=0")
     return out
 
 
@@ -510,6 +512,7 @@ def main():
     torch.cuda.synchronize()
     times = StepTimes()
     reruns0, tails0 = int(L.vr_engine_est_reruns()), int(L.vr_engine_est_tail_flags())
+    pred0 = int(L.vr_engine_est_predicted())
     ktimer_enable(True)  # per-launch HIP events on the launch stream of the hot kernels
     check(L.vr_trace_mark(1, 0, ctypes.c_void_p(stream_of(dev))), "vr_trace_mark")
     t0 = time.perf_counter()
@@ -524,6 +527,7 @@ def main():
     kt = {k: ktimer_read(k) for k in KTIMER_KERNELS}
     ktimer_enable(False)
     est_reruns = int(L.vr_engine_est_reruns()) - reruns0
+    est_predicted = int(L.vr_engine_est_predicted()) - pred0
     est_tail_flags = int(L.vr_engine_est_tail_flags()) - tails0
     stats = torch.tensor([elapsed, times.engine_ms, times.engine_bytes, times.gram_ms,
                           times.gram_flops], dtype=torch.float64, device=dev)
@@ -660,6 +664,7 @@ def main():
             "roofline_gram": roof_gram,
             "kernels_per_step": {k: v for k, v in kernels.items() if v["launches_per_step"]},
             "est_reruns": est_reruns,
+            "est_predicted_exact": est_predicted,
             "est_tail_flags": est_tail_flags,
             "est_structured": est_structured,
             "kendall_unit": kendall,

@@ -192,9 +192,13 @@ int vr_bootstrap_spearman_multi(const void* plan_a, const void* const* planBs, i
  * VISREPS_ENGINE_EST=0 forces the chunk-base form; an exact-form pass that breaks the
  * invariants fails the call with VR_EINTERNAL. */
 int64_t vr_engine_est_reruns(void);
-/* Of those re-runs, the passes the tail invariants flagged (B-side errors; 0 unless a bug
- * or a fault injection). */
+/* Of those re-runs, the passes only the tail invariants flagged: the A walk's window checks
+ * passed, so the B side recovered a wrong rank (0 unless a bug or a fault injection). */
 int64_t vr_engine_est_tail_flags(void);
+/* Engine calls whose first pass's A counts (a count pre-pass before any EST pass) already
+ * put some subset's ranks outside the EST 3 window, so the whole call ran in the exact form
+ * without spending a flagged EST pass (VISREPS_ENGINE_EST_PREDICT=0 disables the check). */
+int64_t vr_engine_est_predicted(void);
 
 // Kernel-level HIP-event timing of the hot kernels, for pricing the dominant kernel against
 // its roofline on the stream it runs on (bench.py). Off by default; enabling clears the

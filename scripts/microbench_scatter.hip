@@ -62,6 +62,32 @@ __global__ __launch_bounds__(1024) void gather(const uint16_t* __restrict__ tb, 
   out[wave * 64 + lane] = acc;
 }
 
+// the same gather with narrower rows: T per lane (u8: 64-B rows, u16x2 per lane pair: 32-B
+// rows read by 16 lanes as u16) -- what a u8-residue TB would cost
+template <int NB, typename T, int ROWB>
+__global__ __launch_bounds__(1024) void gather_n(const uint8_t* __restrict__ tb, const uint32_t* __restrict__ perm,
+                                                 uint32_t rows, uint32_t per_wave, uint32_t* out) {
+  const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t r0 = wave * per_wave;
+  constexpr uint32_t LPR = ROWB / sizeof(T);  // lanes per row
+  uint32_t acc = 0;
+  for (uint32_t r = r0; r < r0 + per_wave && r < rows; r += 64) {
+    const uint32_t pr = (r + lane < rows) ? perm[r + lane] : 0u;
+#pragma unroll
+    for (int h = 0; h < 64; h += NB) {
+      uint32_t v[NB];
+#pragma unroll
+      for (int t = 0; t < NB; ++t) {
+        const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)pr, h + t);
+        v[t] = __builtin_nontemporal_load((const T*)(tb + (size_t)row * ROWB) + (lane % LPR));
+      }
+#pragma unroll
+      for (int t = 0; t < NB; ++t) acc += v[t];
+    }
+  }
+  out[wave * 64 + lane] = acc;
+}
+
 int main() {
   const uint32_t rows = 49995000u;  // M at N = 10k
   std::vector<uint32_t> h(rows);
@@ -107,5 +133,10 @@ int main() {
   if (run("write random (default)", [&] { scatter<true, false><<<grid, 1024>>>(tb, perm, rows, per_wave); })) return 1;
   if (run("gather random NB8", [&] { gather<8><<<grid, 1024>>>(tb, perm, rows, per_wave, out); })) return 1;
   if (run("gather random NB16", [&] { gather<16><<<grid, 1024>>>(tb, perm, rows, per_wave, out); })) return 1;
+  auto gb = [&](auto k) { k<<<grid, 1024>>>((const uint8_t*)tb, perm, rows, per_wave, out); };
+  if (run("gather random 64B u8 NB16", [&] { gb(gather_n<16, uint8_t, 64>); })) return 1;
+  if (run("gather random 64B u16 NB16", [&] { gb(gather_n<16, uint16_t, 64>); })) return 1;
+  if (run("gather random 32B u8 NB16", [&] { gb(gather_n<16, uint8_t, 32>); })) return 1;
+  if (run("gather random 128B u16 NB16", [&] { gb(gather_n<16, uint16_t, 128>); })) return 1;
   return 0;
 }

@@ -137,6 +137,52 @@ def test_est_modes_equal_exact_form(dev, mode, monkeypatch):
     assert np.array_equal(est, ref)
 
 
+@pytest.mark.parametrize("n,nb", [(2500, 200), (700, 64)])
+def test_triangle_order_form_equals_exact_form(dev, n, nb, monkeypatch):
+    # EST 5 / 6 (opt-in VISREPS_ENGINE_TRI=1): TB rows at triangle indices, 63 subsets per
+    # pass, lane 63 the tag; 201 / 65 draws leave partial last passes
+    monkeypatch.setenv("VISREPS_ENGINE_TRI", "1")
+    neural = R.RankPlan(_rdm(dev, n, 120, 31))
+    models = [R.RankPlan(_rdm(dev, n, 90, 32, relu=True)), R.RankPlan(_rdm(dev, n, 300, 33))]
+    idx = bootstrap_indices(42, n, int(0.9 * n), nb)
+    r0, t0 = int(lib().vr_engine_est_reruns()), int(lib().vr_engine_est_tail_flags())
+    est = R.bootstrap_spearman_multi(neural, models, idx, full_first=True).cpu().numpy()
+    assert int(lib().vr_engine_est_reruns()) == r0, "continuous RDMs must not need the exact re-run"
+    assert int(lib().vr_engine_est_tail_flags()) == t0
+    with exact_engine():
+        ref = R.bootstrap_spearman_multi(neural, models, idx, full_first=True).cpu().numpy()
+    assert np.array_equal(est, ref)
+
+
+def test_structured_rdm_goes_exact_up_front(dev, monkeypatch):
+    # n = 5000 with the heavy per-stimulus effects: the first pass's A counts (k_countA at
+    # <= 256 boundaries) are already far outside the EST 3 window, so the call runs exact
+    # from the start -- no EST pass is spent and flagged (vr_engine_est_predicted counts
+    # the call, vr_engine_est_reruns stays) -- and the scores equal the exact form; with the
+    # check off, the first EST pass is flagged and the call gives up there, same scores.
+    n = 5000
+    g = torch.Generator(device=dev).manual_seed(7)
+    u = torch.empty(n, device=dev).exponential_(1.0, generator=g) ** 2
+    a = u[:, None] + u[None, :] + 0.05 * torch.rand(n, n, device=dev, generator=g)
+    a = torch.triu(a, 1)
+    a = a + a.T
+    pa, pb = R.RankPlan(a), R.RankPlan(_rdm(dev, n, 90, 41))
+    del a
+    idx = bootstrap_indices(42, n, int(0.9 * n), 140)
+    L = lib()
+    p0, r0 = int(L.vr_engine_est_predicted()), int(L.vr_engine_est_reruns())
+    est = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    assert int(L.vr_engine_est_predicted()) - p0 == 1
+    assert int(L.vr_engine_est_reruns()) == r0
+    with exact_engine():
+        ref = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    assert np.array_equal(est, ref)
+    monkeypatch.setenv("VISREPS_ENGINE_EST_PREDICT", "0")
+    late = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    assert int(L.vr_engine_est_reruns()) - r0 >= 1, "without the check the first EST pass is flagged"
+    assert np.array_equal(late, ref)
+
+
 def test_half_tied_rdm_exact_join_is_fast(dev):
     # One tie group over half the 12.5 M pairs (n = 5000): it spans ~1000 of the exact
     # form's group-aligned chunks, so the join's chunk lookup must be a binary search

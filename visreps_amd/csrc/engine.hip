@@ -81,7 +81,8 @@ constexpr int EST_STEP_BITS = 12;  // interpolation steps per interval: 2^12
 #define VR_PROBE_ACC 0
 #endif
 static std::atomic<int64_t> g_est_reruns{0};      // passes re-run in the exact form (vr_engine_est_reruns)
-static std::atomic<int64_t> g_est_tail_flags{0};  // of those, flagged by the tail invariants (vr_engine_est_tail_flags)
+static std::atomic<int64_t> g_est_predicted{0};   // calls sent to the exact form before any EST pass (vr_engine_est_predicted)
+static std::atomic<int64_t> g_est_tail_flags{0};  // of those, flagged by the tail invariants alone (vr_engine_est_tail_flags)
 
 // log2 of the coarse interval: the smallest b >= 12 (windows of 64 never straddle a
 // boundary; the 4096 steps are whole positions) with ceil(M / 2^b) <= 96, or, for larger
@@ -562,6 +563,26 @@ __global__ void k_c0_lin(const uint32_t* __restrict__ total, int64_t M, uint2* _
   const int lane = threadIdx.x;
   const float R = (float)(2.0 * (double)total[lane] / (double)M);
   ftab[lane] = make_uint2(__float_as_uint(1.0f - 32768.0f), __float_as_uint(R));
+}
+
+// EST 3 up-front check (est_predict): lane `lane`'s included count a at coarse boundary
+// q = c 2^bits against the wave-uniform estimate. The first included pair at or after q has
+// doubled rank >= 2a + 1 while the window it must fall in is centred on
+// 1 + (2 q R >> 32); a boundary already 2^15 + 2^13 off (the 2^13: slack for the next
+// included pair's distance and tie groups) means a stored rank of that lane falls outside
+// its window there, so the pass would be flagged. Lanes >= nl hold no subset; lane 0 of a
+// full-first pass (the full set, EST 4) is exact by construction.
+__global__ void k_est_predict(const uint32_t* __restrict__ c0rel, const uint32_t* __restrict__ c0seg,
+                              const uint32_t* __restrict__ segpre, int bits, uint32_t Ru, int nl, int skip0,
+                              uint32_t* __restrict__ flag) {
+  const uint32_t c = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (lane >= nl || (skip0 && lane == 0)) return;
+  const uint64_t q = (uint64_t)c << bits;
+  const int64_t a = (int64_t)c0_at(c, lane, c0rel, c0seg, segpre);
+  const int64_t dv = 2 * a - (int64_t)((2 * q * (uint64_t)Ru) >> 32);
+  const int64_t lim = (1 << 15) + (1 << 13);
+  if (dv > lim || dv < -lim) *flag = 1u;  // benign race: every writer stores 1
 }
 
 // ---------------------------------------------------------------------------------
@@ -1505,6 +1526,43 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
   return VR_OK;
 }
 
+// EST 3 up-front check of a call's first pass (masks already built): the count pre-pass at
+// boundaries every 2^b positions (<= EST_NC of them), its scan, k_est_predict. bad <- the
+// wave-uniform estimate cannot hold these A ranks (strongly structured RDMs: per-stimulus
+// effects move a subset's count hundreds of thousands of pairs off the line), so the call
+// goes to the exact form before spending an EST pass and its joins on a flag.
+template <bool CL, bool FULL>
+static int est_predict(const PlanView& A, int64_t n, const EngineWs& E, int lw, int nl, bool full0,
+                       const EngineCfg& cfg, uint2 e3, hipStream_t st, bool& bad) {
+  static bool attr = false;
+  if (!attr) {
+    VR_TRY(allow_big_lds(k_countA<CL, FULL>));
+    attr = true;
+  }
+  const int64_t M = pairs_of(n);
+  const uint32_t nch = plan_nchunks(M);
+  const uint32_t nseg = (uint32_t)cfg.est_nwaves;
+  int b = 12;
+  while (((M + ((int64_t)1 << b) - 1) >> b) > (int64_t)EST_NC) ++b;
+  const uint32_t nc = est_intervals(M, b);
+  {
+    KtScope kt(KT_COUNTA, (double)M, st);
+    k_countA<CL, FULL><<<cfg.est_grid, ENG_THREADS, CL ? (size_t)n * sizeof(uint64_t) : 0, st>>>(
+        A.codes, A.gstart, A.chunk_g, nch, E.masks, n, lw, b, E.c0rel, E.c0seg, E.segA_tot, nseg);
+    VR_CHECK_LAUNCH();
+  }
+  VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
+  uint32_t* flag = E.viol;  // pass flags are cleared before the EST passes
+  VR_CHECK_HIP(hipMemsetAsync(flag, 0, sizeof(uint32_t), st));
+  k_est_predict<<<nc, LANES, 0, st>>>(E.c0rel, E.c0seg, E.segA_pre, b, e3.y, nl, full0 ? 1 : 0, flag);
+  VR_CHECK_LAUNCH();
+  uint32_t h = 0;
+  VR_CHECK_HIP(hipMemcpyAsync(&h, flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VR_CHECK_HIP(hipStreamSynchronize(st));
+  bad = h != 0;
+  return VR_OK;
+}
+
 // B walk of a pass for one B plan (unit slot u of the segment partials), joined to A by
 // posA_byB (and chunkA_byB: the A chunks in the exact form, EST 3's window low ends)
 template <bool LDS, bool FULL, typename TBT, bool BTB, int EST>
@@ -1633,14 +1691,16 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
     second = mode;
     return VR_OK;
   };
-  // EST 5 / 6 (the default EST 3 / 4 passes while M <= 2^28; VISREPS_ENGINE_TRI=0 keeps the
-  // A-order TB): the A walk writes each pair's 128-B row at its triangle index, lane 63
+  // EST 5 / 6 (opt-in, VISREPS_ENGINE_TRI=1, in place of the EST 3 / 4 passes while
+  // M <= 2^28): the A walk writes each pair's 128-B row at its triangle index, lane 63
   // holding the coarse A position, so the B walk finds the row from its own pair codes --
   // no per-unit join, no A-position / low-end streams (132 instead of 140 B per pair) -- at
   // the price of scattered (instead of sequential) row writes in the A walk and 63 subsets
-  // per pass. Flagged passes re-run in the exact form, which joins on demand.
+  // per pass. Flagged passes re-run in the exact form, which joins on demand. Measured on
+  // MI355X at configs[1] the scattered writes cost the A walk more (+0.70 ms
+  // per pass) than the joins save, so the A-order TB stays the default.
   const bool tri = est && cfg.est_mode == 3 && lw == LANES && M <= ((int64_t)1 << 28) &&
-                   env_int("VISREPS_ENGINE_TRI", 1) != 0;
+                   env_int("VISREPS_ENGINE_TRI", 0) != 0;
   // EST 6 coarse position pos >> sh and EST 5 tag (low end + 2^15) >> g: both 16 bits
   uint32_t sh = 0, g = 0;
   while (((uint64_t)(M - 1) >> sh) >= 65536u) ++sh;
@@ -1654,7 +1714,20 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
   // fewer per pair and pass, but measured no faster: 1367 vs 1359 us per k_rankB launch,
   // profiles/r3_engine_lo_ab.log)
   const bool lo_join = !tri && cfg.est_mode == 3 && env_int("VISREPS_ENGINE_LO_JOIN", 1) != 0;
-  if (!tri) VR_TRY(join(!est ? JOIN_CHUNK : (lo_join ? JOIN_LO : JOIN_NONE)));
+  // the EST 3 estimate checked against the first pass's A counts before any join or pass
+  // (VISREPS_ENGINE_EST_PREDICT=0: skip the check; a failing estimate is then caught by the
+  // first pass's flags, at the cost of that pass)
+  bool predicted_bad = false;
+  if (est && cfg.est_mode == 3 && env_int("VISREPS_ENGINE_EST_PREDICT", 1) != 0) {
+    const int64_t sub0 = tri ? LANES - 1 : lw;
+    const int nl0 = (int)std::min<int64_t>(sub0, total);
+    VR_TRY(build_pass_masks(idx, k, 0, nl0, full_first, E.masks, n, st));
+    VR_TRY(with_pass_tag(cfg.est_lds, lw == LANES, true, [&](auto tag) -> int {
+      using Tg = decltype(tag);
+      return est_predict<Tg::lds, Tg::full>(A, n, E, lw, nl0, full_first != 0, cfg, e3, st, predicted_bad);
+    }));
+  }
+  if (!tri && !predicted_bad) VR_TRY(join(!est ? JOIN_CHUNK : (lo_join ? JOIN_LO : JOIN_NONE)));
   // the exact chunk-base form of subsets [set0, set0 + nl), nl <= lw
   auto exact_pass = [&](auto tag, int64_t set0, int nl) -> int {
     using Tg = decltype(tag);
@@ -1682,6 +1755,10 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
     });
   };
   if (!est) return exact_from(0);
+  if (predicted_bad) {
+    g_est_predicted.fetch_add(1);
+    return exact_from(0);
+  }
   const int64_t sub = tri ? LANES - 1 : lw;  // subsets per EST pass
   const int64_t npass = (total + sub - 1) / sub;
   const int64_t pfirst = 0;
@@ -1742,7 +1819,9 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
     VR_CHECK_HIP(hipStreamSynchronize(st));
     for (int64_t p = p0; p < p1; ++p) {
       if (!flags[(size_t)(p - p0)]) continue;
-      if (flags[(size_t)(p - p0)] & 2u) g_est_tail_flags.fetch_add(1);
+      // only the tail invariants flagged it: the A walk's window checks passed, so the B side
+      // recovered a wrong rank (an A-flagged pass breaks the invariants too, as expected)
+      if ((flags[(size_t)(p - p0)] & 3u) == 2u) g_est_tail_flags.fetch_add(1);
       if (second != JOIN_CHUNK) VR_TRY(join(JOIN_CHUNK));
       g_est_reruns.fetch_add(1);
       const int64_t set0 = p * sub;
@@ -1833,6 +1912,7 @@ extern "C" {
 
 int64_t vr_engine_est_reruns(void) { return g_est_reruns.load(); }
 int64_t vr_engine_est_tail_flags(void) { return g_est_tail_flags.load(); }
+int64_t vr_engine_est_predicted(void) { return g_est_predicted.load(); }
 
 size_t vr_bootstrap_workspace(int64_t n) {
   size_t b = 0;

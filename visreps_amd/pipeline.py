@@ -659,12 +659,12 @@ def engine_bytes(n: int, n_boot: int) -> float:
 # position map and writes the A positions and low ends, per unit.
 def engine_tri(n: int, est: Optional[bool] = None) -> bool:
     """Whether the bootstrap calls at n stimuli run the triangle-order EST passes (EST 5/6:
-    M <= 2^28, EST 3 estimate, VISREPS_ENGINE_TRI not 0; engine.hip run_engine_multi_impl)."""
+    M <= 2^28, EST 3 estimate, opt-in VISREPS_ENGINE_TRI=1; engine.hip run_engine_multi_impl)."""
     import os
 
     if est is None:
         est = os.environ.get("VISREPS_ENGINE_EST") != "0"
-    return (est and os.environ.get("VISREPS_ENGINE_TRI", "1") != "0"
+    return (est and os.environ.get("VISREPS_ENGINE_TRI", "0") != "0"
             and os.environ.get("VISREPS_ENGINE_EST_MODE", "3") == "3" and n * (n - 1) // 2 <= (1 << 28))
 
 
