@@ -1174,6 +1174,34 @@ __device__ inline void gather_window(const TBT* __restrict__ TB, const uint32_t*
   }
 }
 
+#ifndef VR_XWIN
+#define VR_XWIN 1  // EST 3 / 4 B walk: next window's streams and masks fetched inside the window (0: off)
+#endif
+
+// EST 3 / 4 B walk, prefetching form (VR_XWIN; the window low ends computed from the A
+// positions in scalar registers, not streamed): every vector-memory load of the walk is
+// issued from asm and retired by a counted asm `s_waitcnt vmcnt(N)`, so the compiler places
+// no vmcnt wait of its own: the next window's streams S (codes, A positions: 2 loads) and
+// its two L2 mask gathers M (when the masks are not in LDS) are issued between the window's
+// TB row batches G[0..7] (8 loads each) and retired with them, and the next window's 64 x 64
+// transpose runs while G[3] is in flight. A window boundary then costs only the drain of
+// G[7] and the refill from G[0] -- no dependent mask round trip and no transpose with the
+// gathers idle. Issue order:
+//   S(w+1) G[0] G[1] G[2] M(w+1) G[3] ... G[7] | S(w+2) G'[0] ...
+// (batch h is waited for once batch h+1 is issued: vmcnt(8); S is retired with G[0], M with
+// G[2], the last batch with vmcnt(0)).
+// Nothing is in flight across the loop's back edge (G[7] is retired with vmcnt(0)), so no
+// register holding an asm load result is live there. tests/test_isa_guard.py checks the
+// generated code for every register these asm loads define.
+__device__ inline void xw_ld2(const uint32_t* a, const uint32_t* b, uint32_t voff, uint32_t& x, uint32_t& y) {
+  asm volatile("global_load_dword %0, %1, %2" : "=v"(x) : "v"(voff), "s"(a) : "memory");
+  asm volatile("global_load_dword %0, %1, %2" : "=v"(y) : "v"(voff), "s"(b) : "memory");
+}
+__device__ inline void xw_ldm(const uint64_t* m, uint32_t code, uint64_t& a, uint64_t& b) {
+  asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(a) : "v"((code >> 16) * 8u), "s"(m) : "memory");
+  asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(b) : "v"((code & 0xffffu) * 8u), "s"(m) : "memory");
+}
+
 // B side. Exact form: yA = 2 baseA[chunkA] + TB[posA] (two gathers per pair). EST form:
 // yA recovered from TB[posA] (absolute, modulo 2^16) and the LDS count table (one gather).
 template <bool LDS, bool FULL, typename TBT, bool BIGT, int EST>
@@ -1214,6 +1242,131 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       S = 0;
       cgs = ce;
     };
+    // EST 3 / 4 (small tie groups): the prefetching walk, which computes the window low
+    // ends from the A positions (a join's streamed low ends, VISREPS_ENGINE_LO_JOIN=1, hold
+    // the same values and are not read)
+    constexpr bool XW = VR_XWIN && (EST == 3 || EST == 4) && !BIGT;
+    constexpr bool walked = XW;
+    if constexpr (XW) {
+      static_assert(EBB == 8, "prefetching batches are 8 pairs");
+      {
+        const uint16_t* TB16 = reinterpret_cast<const uint16_t*>(TB);
+        uint32_t lane_bt;
+        asm("" : "=v"(lane_bt) : "0"((uint32_t)lane * 2u));
+        // stream offset of window wv: lanes past the segment end re-read its last position
+        auto voff_of = [&](uint32_t wv) -> uint32_t {
+          const uint32_t lim = wave_uniform(min(63u, P1 - 1u - wv));
+          return min((uint32_t)lane, lim) * 4u;
+        };
+        // inclusion bits of window wv from its two mask words per lane
+        auto bits_of = [&](uint32_t wv, uint64_t ma, uint64_t mb) -> uint64_t {
+          const uint32_t pos = wv + (uint32_t)lane;
+          const uint64_t v = transpose64((pos >= P0 && pos < P1) ? (ma & mb) : 0ull, lane);
+          return active ? v : 0ull;
+        };
+        uint32_t w = P0 & ~63u;
+        uint32_t cd, pa;
+        xw_ld2(codes + w, posA_byB + w, voff_of(w), cd, pa);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(cd), "+v"(pa) : : "memory");
+        uint64_t x;
+        if constexpr (!LDS) {
+          uint64_t ma, mb;
+          xw_ldm(m, cd, ma, mb);
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(ma), "+v"(mb) : : "memory");
+          x = bits_of(w, ma, mb);
+        } else {
+          x = window_bits(m, cd, w, P0, P1, lane, active);
+        }
+        for (;;) {
+          const bool more = w + 64 < P1;
+          const uint32_t wn = more ? w + 64 : w;
+          uint32_t cdn, pan;
+          const uint64_t F = restrict_flags(((uint64_t)sload(gflag + (w >> 5) + 1) << 32) | sload(gflag + (w >> 5)), w,
+                                            P0, P1);
+          uint64_t xn = 0;
+          // the window's batch pipeline; proc(h, ya) consumes batch h's recovered A ranks
+          // (issued inside each of its two instances: a load in flight across the branch into
+          // them would be copied between registers before its wait)
+          auto pipeline = [&](auto&& proc) {
+            uint64_t ma = 0, mb = 0;
+            uint32_t t[2][EBB];
+            xw_ld2(codes + wn, posA_byB + wn, voff_of(wn), cdn, pan);  // S(w+1)
+            gather_issue_t(TB16, stride, pa, 0, lane_bt, t[0]);
+#pragma unroll
+            for (int h = 0; h < 64 / EBB; ++h) {
+              uint32_t(&cur)[EBB] = t[h & 1];
+              if (h + 1 < 64 / EBB) {
+                gather_issue_t(TB16, stride, pa, (h + 1) * EBB, lane_bt, t[(h + 1) & 1]);
+                gather_wait_n<EBB>(cur);
+                if (h == 0) asm volatile("" : "+v"(cdn), "+v"(pan));  // S(w+1): older than G[0]
+                if constexpr (!LDS) {
+                  if (h == 1) xw_ldm(m, cdn, ma, mb);  // M(w+1), behind G[2]
+                }
+                if (h == 2) {  // only G[3] may be in flight: M(w+1) is retired
+                  if constexpr (!LDS) {
+                    asm volatile("" : "+v"(ma), "+v"(mb));
+                    xn = bits_of(wn, ma, mb);
+                  } else {
+                    xn = window_bits(m, cdn, wn, P0, P1, lane, active);
+                  }
+                }
+              } else {
+                gather_wait_n<0>(cur);
+              }
+              proc(h, cur);
+            }
+          };
+          // the window low ends of the window's A positions, lane j = pair j (3 VALU ops)
+          const uint32_t la = el.Lu + __umulhi(pa << 1, el.Ru);
+          auto recover = [&](uint32_t v, uint32_t j) -> uint32_t {
+            return est_recover(v, est_lo_b<EST>(el, pa, la, j, lane, v));
+          };
+          auto fast_proc = [&](uint64_t& a64, uint32_t& c1) {
+            return [&](int h, uint32_t* cur) {
+#pragma unroll
+              for (int q = 0; q < EBB; ++q) {
+                const uint32_t j = h * EBB + q;
+                const uint32_t y = recover(cur[q], j);
+                const uint32_t mk = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
+                const uint32_t yb = y & mk;
+                if (j < 63) {
+                  a64 += (uint64_t)yb * c1;
+                  St += yb;
+                  c1 -= mk;
+                } else {
+                  S = yb;
+                  cgs = c1 - 1u;
+                }
+              }
+            };
+          };
+          auto slow_proc = [&](int h, uint32_t* cur) {
+#pragma unroll
+            for (int q = 0; q < EBB; ++q) {
+              const uint32_t j = h * EBB + q;
+              const uint32_t y = recover(cur[q], j);
+              if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
+              S += ((x >> j) & 1ull) ? (uint64_t)y : 0ull;
+            }
+          };
+          if (F == ~0ull) {  // every position starts a group (the per-window form below explains)
+            close(cw);
+            uint64_t a64 = 0;
+            uint32_t c1 = cw + 1u;
+            pipeline(fast_proc(a64, c1));
+            acc += (u128)a64 * 2u;
+          } else {
+            pipeline(slow_proc);
+          }
+          cw += popc64(x);
+          if (!more) break;
+          w = wn;
+          cd = cdn;
+          pa = pan;
+          x = xn;
+        }
+      }
+    }
     uint32_t w0 = P0 & ~63u;
     auto fetch = [&](uint32_t w, uint32_t& pa, uint32_t& ca, uint32_t& cd, uint32_t& f0,
                      uint32_t& f1) {
@@ -1239,9 +1392,9 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       f0 = sload(gflag + (w >> 5));
       f1 = sload(gflag + (w >> 5) + 1);
     };
-    uint32_t pa, ca, cd, f0, f1;
-    fetch(w0, pa, ca, cd, f0, f1);
-    for (; w0 < P1; w0 += 64) {
+    uint32_t pa = 0, ca = 0, cd = 0, f0 = 0, f1 = 0;
+    if constexpr (!walked) fetch(w0, pa, ca, cd, f0, f1);
+    for (; !walked && w0 < P1; w0 += 64) {
       const uint32_t pa_c = pa, ca_c = ca;
       uint32_t lane_b4, lane_bt;  // opaque per window, so the base + lane sum is not hoisted
       asm("" : "=v"(lane_b4) : "0"((uint32_t)lane * 4u));
@@ -1713,7 +1866,7 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
   // VISREPS_ENGINE_LO_JOIN=0 has the walk compute them from the A positions instead (4 B
   // fewer per pair and pass, but measured no faster: 1367 vs 1359 us per k_rankB launch,
   // profiles/r3_engine_lo_ab.log)
-  const bool lo_join = !tri && cfg.est_mode == 3 && env_int("VISREPS_ENGINE_LO_JOIN", 1) != 0;
+  const bool lo_join = !tri && cfg.est_mode == 3 && env_int("VISREPS_ENGINE_LO_JOIN", 0) != 0;
   // the EST 3 estimate checked against the first pass's A counts before any join or pass
   // (VISREPS_ENGINE_EST_PREDICT=0: skip the check; a failing estimate is then caught by the
   // first pass's flags, at the cost of that pass)

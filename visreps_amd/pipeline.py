@@ -654,9 +654,10 @@ def engine_bytes(n: int, n_boot: int) -> float:
 # codes and the two join arrays (posA, chunkA) and gathers one TB row per pair (its 256-byte
 # chunk-base rows come from a 2 MB L2-resident table, not HBM). EST form (the default): the
 # A side streams its codes twice (count pre-pass + rank walk); the B walk streams its codes
-# and the A positions and the window low ends the join precomputed (VISREPS_ENGINE_LO_JOIN=0:
-# computes them from the A positions instead); k_join reads the B codes, gathers the 4-B A
-# position map and writes the A positions and low ends, per unit.
+# and the A positions and computes the window low ends from them (VISREPS_ENGINE_LO_JOIN=1:
+# the join also writes the low ends -- 4 B more per pair there -- which the prefetching EST 3/4
+# walk does not read); k_join reads the B codes, gathers the 4-B A position map and writes
+# the A positions, per unit.
 def engine_tri(n: int, est: Optional[bool] = None) -> bool:
     """Whether the bootstrap calls at n stimuli run the triangle-order EST passes (EST 5/6:
     M <= 2^28, EST 3 estimate, opt-in VISREPS_ENGINE_TRI=1; engine.hip run_engine_multi_impl)."""
@@ -682,7 +683,7 @@ def engine_pair_bytes(est: Optional[bool] = None, tri: bool = False) -> Tuple[in
         # A: codes 4 + TB row write 128; B: codes, posA, chunkA 4 each + TB row 128;
         # join: B codes 4 + 8-B pair-map record + posA and chunkA writes 4 each
         return 4 + 128, 4 + 4 + 4 + 128, 4 + 8 + 4 + 4
-    lo = 0 if os.environ.get("VISREPS_ENGINE_LO_JOIN", "1") == "0" else 4
+    lo = 4 if os.environ.get("VISREPS_ENGINE_LO_JOIN", "0") != "0" else 0
     # A: codes 4 (count pre-pass) + codes 4 + TB row write 128; B: codes 4 + posA 4
     # (+ low end) + TB row gather 128; join: B codes 4 + position-map gather 4 + posA write 4
     # (+ low-end write)
