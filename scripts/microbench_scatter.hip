@@ -75,17 +75,42 @@ __global__ __launch_bounds__(1024) void gather_n(const uint8_t* __restrict__ tb,
     const uint32_t pr = (r + lane < rows) ? perm[r + lane] : 0u;
 #pragma unroll
     for (int h = 0; h < 64; h += NB) {
-      uint32_t v[NB];
+      T v[NB];
 #pragma unroll
       for (int t = 0; t < NB; ++t) {
         const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)pr, h + t);
         v[t] = __builtin_nontemporal_load((const T*)(tb + (size_t)row * ROWB) + (lane % LPR));
       }
 #pragma unroll
-      for (int t = 0; t < NB; ++t) acc += v[t];
+      for (int t = 0; t < NB; ++t) {
+        if constexpr (sizeof(T) == 8)
+          acc += (uint32_t)v[t] ^ (uint32_t)(v[t] >> 32);
+        else
+          acc += v[t];
+      }
     }
   }
   out[wave * 64 + lane] = acc;
+}
+
+// sequential TB writes with 16-B stores per lane: one instruction writes 8 rows (1 KB)
+template <bool NT>
+__global__ __launch_bounds__(1024) void write_x4(uint16_t* __restrict__ tb, uint32_t rows, uint32_t per_wave) {
+  const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t r0 = wave * per_wave;
+  for (uint32_t r = r0; r < r0 + per_wave && r < rows; r += 64) {
+#pragma unroll
+    for (int j = 0; j < 64; j += 8) {
+      if (r + j + 8 > rows) break;
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      u32x4* p = reinterpret_cast<u32x4*>(tb + (size_t)(r + j) * 64) + lane;
+      const u32x4 v = {r + lane, r + j, lane, (uint32_t)j};
+      if (NT)
+        __builtin_nontemporal_store(v, p);
+      else
+        *p = v;
+    }
+  }
 }
 
 int main() {
@@ -102,7 +127,7 @@ int main() {
   }
   uint16_t* tb;
   uint32_t *perm, *out;
-  CK(hipMalloc(&tb, (size_t)rows * 128));
+  CK(hipMalloc(&tb, (size_t)rows * 512));  // room for the 512-B row gathers
   CK(hipMalloc(&perm, (size_t)rows * 4));
   CK(hipMalloc(&out, (size_t)1 << 24));
   CK(hipMemcpy(perm, h.data(), (size_t)rows * 4, hipMemcpyHostToDevice));
@@ -133,10 +158,16 @@ int main() {
   if (run("write random (default)", [&] { scatter<true, false><<<grid, 1024>>>(tb, perm, rows, per_wave); })) return 1;
   if (run("gather random NB8", [&] { gather<8><<<grid, 1024>>>(tb, perm, rows, per_wave, out); })) return 1;
   if (run("gather random NB16", [&] { gather<16><<<grid, 1024>>>(tb, perm, rows, per_wave, out); })) return 1;
+  if (run("write seq x4 (16 B/lane)", [&] { write_x4<false><<<grid, 1024>>>(tb, rows, per_wave); })) return 1;
+  if (run("write seq x4 NT", [&] { write_x4<true><<<grid, 1024>>>(tb, rows, per_wave); })) return 1;
   auto gb = [&](auto k) { k<<<grid, 1024>>>((const uint8_t*)tb, perm, rows, per_wave, out); };
   if (run("gather random 64B u8 NB16", [&] { gb(gather_n<16, uint8_t, 64>); })) return 1;
   if (run("gather random 64B u16 NB16", [&] { gb(gather_n<16, uint16_t, 64>); })) return 1;
   if (run("gather random 32B u8 NB16", [&] { gb(gather_n<16, uint8_t, 32>); })) return 1;
   if (run("gather random 128B u16 NB16", [&] { gb(gather_n<16, uint16_t, 128>); })) return 1;
+  // wider rows: two / four passes' subsets per row (u32 / u64 per lane)
+  if (run("gather random 256B u32 NB16", [&] { gb(gather_n<16, uint32_t, 256>); })) return 1;
+  if (run("gather random 256B u32 NB8", [&] { gb(gather_n<8, uint32_t, 256>); })) return 1;
+  if (run("gather random 512B u64 NB8", [&] { gb(gather_n<8, uint64_t, 512>); })) return 1;
   return 0;
 }
