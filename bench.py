@@ -122,7 +122,7 @@ def split_mode(n: int, dims: dict) -> bool:
     return mode == "split" or all(float(n) * n * d >= 1e10 for d in dims.values())
 
 
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r3_pmc_engine.json")
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r4_pmc_engine.json")
 
 
 def pmc_traffic(n: int, est: bool):
