@@ -1174,6 +1174,12 @@ __device__ inline void gather_window(const TBT* __restrict__ TB, const uint32_t*
   }
 }
 
+#ifndef VR_XP
+#define VR_XP 0  // timing probes of the prefetching walk's per-pair work (bitmask; wrong scores)
+#endif
+#ifndef VR_TAIL_CHECK
+#define VR_TAIL_CHECK 1  // 0: probe builds only -- the tail invariants never flag
+#endif
 #ifndef VR_XWIN
 #define VR_XWIN 1  // EST 3 / 4 B walk: next window's streams and masks fetched inside the window (0: off)
 #endif
@@ -1319,7 +1325,11 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
           // the window low ends of the window's A positions, lane j = pair j (3 VALU ops)
           const uint32_t la = el.Lu + __umulhi(pa << 1, el.Ru);
           auto recover = [&](uint32_t v, uint32_t j) -> uint32_t {
+#if VR_XP & 4  // timing probe only: one low end for the whole window (no per-pair readlane)
+            return est_recover(v, readlane_u32(la, 0));
+#else
             return est_recover(v, est_lo_b<EST>(el, pa, la, j, lane, v));
+#endif
           };
           auto fast_proc = [&](uint64_t& a64, uint32_t& c1) {
             return [&](int h, uint32_t* cur) {
@@ -1330,8 +1340,16 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
                 const uint32_t mk = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
                 const uint32_t yb = y & mk;
                 if (j < 63) {
+#if VR_XP & 1  // timing probe only (wrong scores): no 64-bit multiply-add
+                  a64 = (a64 & ~0xffffffffull) | (uint32_t)((uint32_t)a64 + (yb ^ c1));
+#else
                   a64 += (uint64_t)yb * c1;
+#endif
+#if VR_XP & 2  // timing probe only: no 64-bit running sum
+                  c1 ^= yb & 1u;
+#else
                   St += yb;
+#endif
                   c1 -= mk;
                 } else {
                   S = yb;
@@ -1577,7 +1595,7 @@ __global__ void k_tail_top(const uint64_t* __restrict__ fpart0, uint32_t nblk,
   const bool broken = lane < nl && !forced_nan &&
                       (P != (uint64_t)totA[lane] || Ssum != (uint64_t)totA[lane] * ((uint64_t)totA[lane] + 1u));
   // bit 1 (the A walk's window checks set bit 0); benign race: every writer stores old | 2
-  if (__ballot(broken) != 0 && lane == 0) *viol |= 2u;
+  if (VR_TAIL_CHECK && __ballot(broken) != 0 && lane == 0) *viol |= 2u;
   if (lane >= nl) return;
   const u128 Mp = totA[lane];
   const u128 mu = Mp * (Mp + 1) * (Mp + 1);
