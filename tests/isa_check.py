@@ -112,7 +112,7 @@ def check_asm_gathers(code: list[tuple[int, str, int | None]]) -> tuple[int, lis
             addr, ins, tgt = code[i]
             op = ins.split()[0]
             if state:
-                pending = set().union(*[r for r, _ in state])
+                pending = set().union(*[e[0] for e in state])
                 used = _regs(ins.split(None, 1)[1]) if " " in ins else set()
                 hit = used & pending
                 if hit and op != "s_waitcnt":
@@ -121,14 +121,19 @@ def check_asm_gathers(code: list[tuple[int, str, int | None]]) -> tuple[int, lis
                 m = re.search(r"vmcnt\((\d+)\)", ins)
                 if m:
                     keep = int(m.group(1))
-                    state = tuple((r, y) for r, y in state if y < keep)
+                    state = tuple(e for e in state if e[1] < keep)
             elif _VMEM.match(op):
-                state = tuple((r, y + 1) for r, y in state)
+                # at most 63 vector-memory ops are outstanding (6-bit vmcnt): one with 63
+                # younger ones has completed -- this also bounds the states around loops
+                state = tuple((e[0], e[1] + 1, e[2]) for e in state if e[1] + 1 < 63)
                 gm = _SADDR_LOAD.match(ins)
                 if gm:
-                    state = state + ((frozenset(_regs(gm.group(1))), 0),)
+                    # the flag: a streaming (nt) load, i.e. a TB row gather
+                    state = state + ((frozenset(_regs(gm.group(1))), 0, ins.rstrip().endswith(" nt")),)
             if op == "s_endpgm":
-                if state:
+                # a TB row gather still in flight at the end (other saddr loads may be compiler
+                # loads whose value a path never uses: legal, the wave's end waits for them)
+                if any(e[2] for e in state):
                     problems.append(f"{addr:#x}: kernel ends with asm gathers in flight")
                 break
             if op.startswith(("s_setpc", "s_swappc")):

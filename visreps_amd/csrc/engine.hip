@@ -121,12 +121,26 @@ struct EngineCfg {
   int est_mode;       // 1: interval table in LDS, 2: one linear interval in registers
   int est_b;          // log2 of the table interval
   uint32_t est_rows;  // table rows (intervals)
+  uint32_t est_nseg;   // EST B-walk segments (work queue; est_segments)
+  uint32_t est_nsegA;  // EST A-side segments: est_nseg x est_ratioA (k_countA, k_rankA)
+  uint32_t est_ratioA;
   size_t tab;         // EST rank walks' dynamic LDS: [masks] + table
 };
 
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e && *e ? atoi(e) : dflt;
+}
+
+#ifndef VR_SEGS_PER_WAVE
+#define VR_SEGS_PER_WAVE 4  // most EST A-side segments per resident wave (workspace bound)
+#endif
+// EST B walks take segments of >= 256 positions from a work queue, one per resident wave;
+// the A side cuts each of them into est_ratioA (VISREPS_ENGINE_SEGS_A, default and most
+// VR_SEGS_PER_WAVE) for its own queue (k_rankA; k_countA takes them round-robin).
+static uint32_t est_segments(int64_t M, int est_nwaves) {
+  const int64_t by_len = (M + 255) / 256;
+  return (uint32_t)std::max<int64_t>(1, std::min<int64_t>(by_len, (int64_t)est_nwaves));
 }
 
 static EngineCfg engine_cfg(int64_t n) {
@@ -157,6 +171,9 @@ static EngineCfg engine_cfg(int64_t n) {
   c.est_rows = M > 0 ? est_intervals(M, c.est_b) : 0;
   c.est_grid = c.est_lds ? num_cus() * est_wg : c.grid;
   c.est_nwaves = c.est_grid * WAVES_PER_WG;
+  c.est_nseg = est_segments(M, c.est_nwaves);
+  c.est_ratioA = (uint32_t)std::max(1, std::min(VR_SEGS_PER_WAVE, env_int("VISREPS_ENGINE_SEGS_A", VR_SEGS_PER_WAVE)));
+  c.est_nsegA = c.est_nseg * c.est_ratioA;
   c.tab = (c.est_lds ? need : 0) + (c.est_mode == 1 ? (size_t)c.est_rows * row : 0);
   return c;
 }
@@ -188,14 +205,22 @@ struct EngineWs {
   uint2* ftab;          // [EST_NC][64]     EST: {L_c, D_c} per interval (window low end, step)
   uint32_t* viol;       // [EST_MAX_PASSES] EST: pass flagged for the exact re-run;
                         // [EST_MAX_PASSES]: an exact-form pass broke the tail invariants
+  uint32_t* segposA;    // [nsegmax + 1] EST segment starts of the A plan (k_seg_table)
+  uint32_t* segposB;    // [units][nw + 1] ... of each B plan
+  size_t segstride;     // nw + 1
+  uint32_t* queue;      // [QSLOTS] EST work-queue counters of one pass's launches
 };
+constexpr int QSLOTS = 256;
+enum { QS_RANKA = 0, QS_RANKB = 1 };  // queue slots of an EST pass's launches
 
 constexpr int EST_MAX_PASSES = 512;  // passes between two checks of the EST flags
 
 static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t* bytes, int64_t units = 1) {
   const int64_t M = pairs_of(n);
   const size_t nch = plan_nchunks(M);
-  const size_t nsb = scan_blocks((uint32_t)nwaves);
+  // A-side segment partials: up to VR_SEGS_PER_WAVE per wave (EST); B-side: one per wave
+  const size_t nsegmax = (size_t)nwaves * VR_SEGS_PER_WAVE;
+  const size_t nsb = scan_blocks((uint32_t)nsegmax);
   Carver c(base);
   EngineWs e;
   e.c0rel = c.take<uint32_t>((size_t)EST_NC * LANES);
@@ -208,10 +233,14 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
   e.TB = c.take<uint32_t>((size_t)M * (size_t)lw);  // sized for u32
   e.lpA = c.take<uint32_t>(nch * LANES);
   e.baseA = c.take<uint32_t>(nch * LANES);
-  e.segA_tot = c.take<uint32_t>((size_t)nwaves * LANES);
-  e.segA_part = c.take<uint64_t>((size_t)nwaves * LANES * PA_N);
-  e.segA_pre = c.take<uint32_t>((size_t)nwaves * LANES);
+  e.segA_tot = c.take<uint32_t>(nsegmax * LANES);
+  e.segA_part = c.take<uint64_t>(nsegmax * LANES * PA_N);
+  e.segA_pre = c.take<uint32_t>(nsegmax * LANES);
   units = std::max<int64_t>(units, 1);
+  e.segstride = (size_t)nwaves + 1;
+  e.segposA = c.take<uint32_t>(nsegmax + 1);
+  e.segposB = c.take<uint32_t>(e.segstride * (size_t)units);
+  e.queue = c.take<uint32_t>(QSLOTS);
   e.useg = (size_t)nwaves * LANES;
   e.segB_tot = c.take<uint32_t>(e.useg * (size_t)units);
   e.segB_part = c.take<uint64_t>(e.useg * PB_N * (size_t)units);
@@ -351,6 +380,33 @@ __host__ __device__ inline uint32_t seg_of_chunk(uint32_t c, uint32_t nchunks, u
   return (uint32_t)(((uint64_t)(c + 1) * nwaves - 1) / nchunks);
 }
 
+// The EST kernels' work queue: lane 0 takes the next segment index of this launch's
+// counter (a vector atomic), the wave reads it from lane 0.
+__device__ inline uint32_t next_segment(uint32_t* q) {
+  uint32_t s = 0;
+  if ((threadIdx.x & 63) == 0) s = atomicAdd(q, 1u);
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
+}
+
+// EST segment starts of a plan: segpos[s] = the first tie-group start >= s M / nseg
+// (segpos[nseg] = M), a binary search over the G + 1 group starts. Segments may be empty
+// (a tie group longer than M / nseg).
+__global__ void k_seg_table(const uint32_t* __restrict__ gstart, const PlanHeader* __restrict__ hdr, int64_t M,
+                            uint32_t nseg, uint32_t* __restrict__ segpos) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > nseg) return;
+  const uint64_t nominal = (uint64_t)s * (uint64_t)M / nseg;
+  uint32_t lo = 0, hi = hdr->G;  // gstart[hi] = M >= nominal
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if ((uint64_t)gstart[mid] >= nominal)
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  segpos[s] = s == nseg ? (uint32_t)M : gstart[lo];
+}
+
 __device__ inline uint32_t chunk_start(const uint32_t* __restrict__ gstart,
                                        const uint32_t* __restrict__ chunk_g, uint32_t c) {
   return sload(gstart + sload(chunk_g + c));
@@ -486,34 +542,39 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_countA(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gstart,
     const uint32_t* __restrict__ chunk_g, uint32_t nchunks, const uint64_t* __restrict__ gmask,
     int64_t n, int lw, int bits, uint32_t* __restrict__ c0rel, uint32_t* __restrict__ c0seg,
-    uint32_t* __restrict__ seg_tot, uint32_t nseg) {
+    uint32_t* __restrict__ seg_tot, uint32_t nseg, const uint32_t* __restrict__ segpos) {
   extern __shared__ uint64_t smask[];
   const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
   const int lane = threadIdx.x & 63;
   const bool active = FULL || lane < lw;
+  (void)gstart;
+  (void)chunk_g;
+  (void)nchunks;
+  // segments [segpos[s], segpos[s + 1]) round-robin (a count walk is too short per segment
+  // for a shared work-queue counter: 32 k atomics on one address cost more than it saves)
   const uint32_t wave = wave_uniform(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
-  const Segment sg = my_segment(nchunks, nseg, wave);
-  uint32_t cw = 0;
-  if (sg.c0 < sg.c1) {
-    const uint32_t P0 = chunk_start(gstart, chunk_g, sg.c0);
-    const uint32_t P1 = chunk_start(gstart, chunk_g, sg.c1);
-    const uint32_t bmask = (1u << bits) - 1u;
-    uint32_t w0 = P0 & ~63u;
-    uint32_t cd = (w0 + lane >= P0 && w0 + lane < P1) ? codes[w0 + lane] : 0u;
-    for (; w0 < P1; w0 += 64) {
-      const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
-      if (w0 + 64 < P1) {
-        const uint32_t q = w0 + 64 + lane;
-        cd = q < P1 ? codes[q] : 0u;
+  for (uint32_t sidx = wave; sidx < nseg; sidx += gridDim.x * WAVES_PER_WG) {
+    const uint32_t P0 = segpos[sidx], P1 = segpos[sidx + 1];
+    uint32_t cw = 0;
+    if (P0 < P1) {
+      const uint32_t bmask = (1u << bits) - 1u;
+      uint32_t w0 = P0 & ~63u;
+      uint32_t cd = (w0 + lane >= P0 && w0 + lane < P1) ? codes[w0 + lane] : 0u;
+      for (; w0 < P1; w0 += 64) {
+        const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+        if (w0 + 64 < P1) {
+          const uint32_t q = w0 + 64 + lane;
+          cd = q < P1 ? codes[q] : 0u;
+        }
+        if ((w0 & bmask) == 0 && w0 >= P0) {  // boundary q = w0: count before it
+          c0rel[(size_t)(w0 >> bits) * LANES + lane] = cw;
+          if (lane == 0) c0seg[w0 >> bits] = sidx;
+        }
+        cw += popc64(x);
       }
-      if ((w0 & bmask) == 0 && w0 >= P0) {  // boundary q = w0: count before it
-        c0rel[(size_t)(w0 >> bits) * LANES + lane] = cw;
-        if (lane == 0) c0seg[w0 >> bits] = wave;
-      }
-      cw += popc64(x);
     }
+    seg_tot[(size_t)sidx * LANES + lane] = cw;
   }
-  seg_tot[(size_t)wave * LANES + lane] = cw;
 }
 
 // Interval c of the EST table from the included counts at its two boundaries: c0 = segment
@@ -642,7 +703,7 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
     const uint32_t* __restrict__ chunk_g, const uint32_t* __restrict__ gflag, uint32_t nchunks,
     const uint64_t* __restrict__ gmask, int64_t n, TBT* __restrict__ TB, int lw,
     uint32_t* __restrict__ lpA, uint32_t* __restrict__ seg_tot, uint64_t* __restrict__ seg_part,
-    uint32_t nseg, EstA est) {
+    uint32_t nseg, EstA est, const uint32_t* __restrict__ segpos, uint32_t* __restrict__ queue) {
   static_assert(!EST || sizeof(TBT) == 2, "EST ranks are u16");
   constexpr bool TRI = EST >= 5;  // triangle-order TB rows (EST 5 / 6)
   static_assert(!TRI || FULL, "triangle-order passes use whole 64-lane rows");
@@ -663,139 +724,149 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
   const bool active = FULL || lane < lw;
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
   const uint32_t wave = wave_uniform(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
-  const Segment sg = my_segment(nchunks, nseg, wave);
-
-  uint64_t tie = 0;  // sum over groups of k^3 - k (k < 2^16)
-  u128 tie_big = 0;  //   (k >= 2^16)
-  uint32_t cw = 0;   // included count before the window (segment-relative)
   bool bad = false;  // EST: a stored rank is not recoverable from its 16 bits
-  if (sg.c0 < sg.c1) {
-    // EST: 2 x (included pairs before this segment); exact form: 0
-    const uint32_t y0 = EST ? 2u * est.segpre[(size_t)wave * LANES + lane] : 0u;
-    const uint32_t P0 = chunk_start(gstart, chunk_g, sg.c0);
-    const uint32_t P1 = chunk_start(gstart, chunk_g, sg.c1);
-    uint32_t cn = sg.c0;  // next chunk whose start is not yet recorded
-    uint32_t pn = P0;
-    uint32_t lp = 0;      // count at the current chunk's start (exact form)
-    while (cn < sg.c1 && pn == P0) {
-      if (!EST) lpA[(size_t)cn * LANES + lane] = 0;
-      ++cn;
-      pn = cn < sg.c1 ? chunk_start(gstart, chunk_g, cn) : P1;
-    }
-    uint32_t gs = P0, cgs = 0;  // open group start and the count before it
-    // close the open group [gs, xe) given ce = included count before xe
-    auto close = [&](uint32_t xe, uint32_t ce) {
-      tie_add<BIGT>(tie, tie_big, ce - cgs);
-      if (active) {
-        if constexpr (TRI)
-          store_rows_tri<EST>(reinterpret_cast<uint16_t*>(TB), gs, xe - gs, lane, y0 + cgs + ce + 1u, el, bad,
-                              row_t);
-        else if constexpr (EST)
-          store_rows_est<EST>(reinterpret_cast<uint16_t*>(TB), stride, gs, xe - gs, lane, y0 + cgs + ce + 1u,
-                              el, bad);
-        else
-          store_rows<FULL, TBT>(TB, stride, gs, xe - gs, lane, (TBT)(cgs + ce + 1u - 2u * lp));
-      }
-      gs = xe;
-      cgs = ce;
-      while (cn < sg.c1 && pn == xe) {  // chunk boundaries are group starts
-        if (!EST) lpA[(size_t)cn * LANES + lane] = ce;
-        lp = ce;
+  // One segment [P0, P1) = chunks [c0, c1) (exact form) or a work-queue segment (EST:
+  // segpos, no chunk bookkeeping), partial sums at index sidx (k_rankB's walk_segment)
+  auto walk_segment = [&](uint32_t sidx, uint32_t c0, uint32_t c1, uint32_t P0, uint32_t P1) {
+    uint64_t tie = 0;  // sum over groups of k^3 - k (k < 2^16)
+    u128 tie_big = 0;  //   (k >= 2^16)
+    uint32_t cw = 0;   // included count before the window (segment-relative)
+    if (P0 < P1) {
+      // EST: 2 x (included pairs before this segment); exact form: 0
+      const uint32_t y0 = EST ? 2u * est.segpre[(size_t)sidx * LANES + lane] : 0u;
+      uint32_t cn = c0;  // next chunk whose start is not yet recorded
+      uint32_t pn = P0;
+      uint32_t lp = 0;      // count at the current chunk's start (exact form)
+      while (cn < c1 && pn == P0) {
+        if (!EST) lpA[(size_t)cn * LANES + lane] = 0;
         ++cn;
-        pn = cn < sg.c1 ? chunk_start(gstart, chunk_g, cn) : P1;
+        pn = cn < c1 ? chunk_start(gstart, chunk_g, cn) : P1;
       }
-    };
-    uint32_t w0 = P0 & ~63u;
-    // next window's codes (vector, lane j = pair w0 + j) and flags (scalar), one ahead
-    uint32_t cd = (w0 + lane >= P0 && w0 + lane < P1) ? codes[w0 + lane] : 0u;
-    uint32_t f0 = sload(gflag + (w0 >> 5)), f1 = sload(gflag + (w0 >> 5) + 1);
-    for (; w0 < P1; w0 += 64) {
-      if constexpr (TRI) {
-        tl = (w0 + lane >= P0 && w0 + lane < P1) ? tri32(cd, (uint32_t)n) : 0u;
-        tg = tri_tag<EST>(el, w0 + (uint32_t)lane);
-        wt = w0;
-      }
-#if VR_PROBE_WBA  // timing probe only (wrong scores): k_rankA without mask lookups / transposes
-      const uint64_t x = active ? (0xF7DFBEFDFBF7EFDFull ^ ((uint64_t)(cd & 7u) << 3)) : 0ull;
-#else
-      const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
-#endif
-      uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
-      asm volatile("" ::"v"(x) : "memory");
-      if constexpr (EST) {
-        // Every group that starts and ends in this window has y = y0 + cgs + ce + 1 in
-        // [Y0, Y0 + 128] (Y0 = y0 + 2 cw + 1: cw <= cgs <= ce <= cw + 64), and lo is monotone,
-        // in [lo(w0), lo(w0 + 63)]: these two checks make all of them recoverable. Longer
-        // groups are checked where they close.
-        if (VR_EST_CHECK) {
-          const uint32_t Y0 = y0 + 2u * cw + 1u;
-          bad |= est_bad(Y0, est_lo_t<EST>(el, w0 + 63u, lane)) || est_bad(Y0 + 128u, est_lo_t<EST>(el, w0, lane));
+      uint32_t gs = P0, cgs = 0;  // open group start and the count before it
+      // close the open group [gs, xe) given ce = included count before xe
+      auto close = [&](uint32_t xe, uint32_t ce) {
+        tie_add<BIGT>(tie, tie_big, ce - cgs);
+        if (active) {
+          if constexpr (TRI)
+            store_rows_tri<EST>(reinterpret_cast<uint16_t*>(TB), gs, xe - gs, lane, y0 + cgs + ce + 1u, el, bad,
+                                row_t);
+          else if constexpr (EST)
+            store_rows_est<EST>(reinterpret_cast<uint16_t*>(TB), stride, gs, xe - gs, lane, y0 + cgs + ce + 1u,
+                                el, bad);
+          else
+            store_rows<FULL, TBT>(TB, stride, gs, xe - gs, lane, (TBT)(cgs + ce + 1u - 2u * lp));
         }
-      }
-      if (w0 + 64 < P1) {
-        const uint32_t q = w0 + 64 + lane;
-        cd = q < P1 ? codes[q] : 0u;
-        f0 = sload(gflag + ((w0 + 64) >> 5));
-        f1 = sload(gflag + ((w0 + 64) >> 5) + 1);
-      }
-      if (F == ~0ull) {  // every position starts a group: close the carried one, then
-        close(w0, cw);   // 63 singletons need only a running count
-        if (cn >= sg.c1 || pn > w0 + 63u) {
-          uint32_t t = EST ? y0 + 2u * cw + 1u : 2u * (cw - lp) + 1u;
-          TBT* row = TB + (size_t)w0 * stride + lane;
-          if constexpr (TRI) {
-#pragma unroll
+        gs = xe;
+        cgs = ce;
+        while (cn < c1 && pn == xe) {  // chunk boundaries are group starts
+          if (!EST) lpA[(size_t)cn * LANES + lane] = ce;
+          lp = ce;
+          ++cn;
+          pn = cn < c1 ? chunk_start(gstart, chunk_g, cn) : P1;
+        }
+      };
+      uint32_t w0 = P0 & ~63u;
+      // next window's codes (vector, lane j = pair w0 + j) and flags (scalar), one ahead
+      uint32_t cd = (w0 + lane >= P0 && w0 + lane < P1) ? codes[w0 + lane] : 0u;
+      uint32_t f0 = sload(gflag + (w0 >> 5)), f1 = sload(gflag + (w0 >> 5) + 1);
+      for (; w0 < P1; w0 += 64) {
+        if constexpr (TRI) {
+          tl = (w0 + lane >= P0 && w0 + lane < P1) ? tri32(cd, (uint32_t)n) : 0u;
+          tg = tri_tag<EST>(el, w0 + (uint32_t)lane);
+          wt = w0;
+        }
+  #if VR_PROBE_WBA  // timing probe only (wrong scores): k_rankA without mask lookups / transposes
+        const uint64_t x = active ? (0xF7DFBEFDFBF7EFDFull ^ ((uint64_t)(cd & 7u) << 3)) : 0ull;
+  #else
+        const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+  #endif
+        uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
+        asm volatile("" ::"v"(x) : "memory");
+        if constexpr (EST) {
+          // Every group that starts and ends in this window has y = y0 + cgs + ce + 1 in
+          // [Y0, Y0 + 128] (Y0 = y0 + 2 cw + 1: cw <= cgs <= ce <= cw + 64), and lo is monotone,
+          // in [lo(w0), lo(w0 + 63)]: these two checks make all of them recoverable. Longer
+          // groups are checked where they close.
+          if (VR_EST_CHECK) {
+            const uint32_t Y0 = y0 + 2u * cw + 1u;
+            bad |= est_bad(Y0, est_lo_t<EST>(el, w0 + 63u, lane)) || est_bad(Y0 + 128u, est_lo_t<EST>(el, w0, lane));
+          }
+        }
+        if (w0 + 64 < P1) {
+          const uint32_t q = w0 + 64 + lane;
+          cd = q < P1 ? codes[q] : 0u;
+          f0 = sload(gflag + ((w0 + 64) >> 5));
+          f1 = sload(gflag + ((w0 + 64) >> 5) + 1);
+        }
+        if (F == ~0ull) {  // every position starts a group: close the carried one, then
+          close(w0, cw);   // 63 singletons need only a running count
+          if (cn >= c1 || pn > w0 + 63u) {
+            uint32_t t = EST ? y0 + 2u * cw + 1u : 2u * (cw - lp) + 1u;
+            TBT* row = TB + (size_t)w0 * stride + lane;
+            if constexpr (TRI) {
+  #pragma unroll
+              for (int j = 0; j < 63; ++j) {
+                const uint32_t bit = (uint32_t)(x >> j) & 1u;
+                const uint32_t v = t + bit;
+                const uint32_t pc = readlane_u32(tg, j);
+                tb_store((TBT)(lane == LANES - 1 ? pc : v), TB + (size_t)readlane_u32(tl, j) * LANES + lane);
+                t = v + bit;
+              }
+            } else {
+  #if VR_PROBE_STW  // timing probe only (wrong TB layout): one 4-byte store per two rows
+            uint32_t* row2 = reinterpret_cast<uint32_t*>(TB + (size_t)w0 * stride) + lane;
+  #pragma unroll
+            for (int j = 0; j < 62; j += 2) {
+              const uint32_t b0 = (uint32_t)(x >> j) & 1u, b1 = (uint32_t)(x >> (j + 1)) & 1u;
+              const uint32_t v0 = t + b0, v1 = v0 + b0 + b1;
+              if (active) __builtin_nontemporal_store(v0 | (v1 << 16), row2 + (size_t)j * stride / 2);
+              t = v1 + b1;
+            }
+            if (active) tb_store((TBT)t, row + (size_t)62 * stride);
+  #else
+  #pragma unroll
             for (int j = 0; j < 63; ++j) {
               const uint32_t bit = (uint32_t)(x >> j) & 1u;
               const uint32_t v = t + bit;
-              const uint32_t pc = readlane_u32(tg, j);
-              tb_store((TBT)(lane == LANES - 1 ? pc : v), TB + (size_t)readlane_u32(tl, j) * LANES + lane);
+              if (active) tb_store((TBT)v, row + (size_t)j * stride);
               t = v + bit;
             }
+  #endif
+            }
+            gs = w0 + 63u;
+            cgs = cw + popc64(x & lowmask(63));
+            F = 0;
           } else {
-#if VR_PROBE_STW  // timing probe only (wrong TB layout): one 4-byte store per two rows
-          uint32_t* row2 = reinterpret_cast<uint32_t*>(TB + (size_t)w0 * stride) + lane;
-#pragma unroll
-          for (int j = 0; j < 62; j += 2) {
-            const uint32_t b0 = (uint32_t)(x >> j) & 1u, b1 = (uint32_t)(x >> (j + 1)) & 1u;
-            const uint32_t v0 = t + b0, v1 = v0 + b0 + b1;
-            if (active) __builtin_nontemporal_store(v0 | (v1 << 16), row2 + (size_t)j * stride / 2);
-            t = v1 + b1;
+            F &= ~1ull;
           }
-          if (active) tb_store((TBT)t, row + (size_t)62 * stride);
-#else
-#pragma unroll
-          for (int j = 0; j < 63; ++j) {
-            const uint32_t bit = (uint32_t)(x >> j) & 1u;
-            const uint32_t v = t + bit;
-            if (active) tb_store((TBT)v, row + (size_t)j * stride);
-            t = v + bit;
-          }
-#endif
-          }
-          gs = w0 + 63u;
-          cgs = cw + popc64(x & lowmask(63));
-          F = 0;
-        } else {
-          F &= ~1ull;
         }
+        while (F) {
+          const uint32_t b = (uint32_t)__builtin_ctzll(F);
+          F &= F - 1;
+          close(w0 + b, cw + popc64(x & lowmask(b)));
+        }
+        cw += popc64(x);
       }
-      while (F) {
-        const uint32_t b = (uint32_t)__builtin_ctzll(F);
-        F &= F - 1;
-        close(w0 + b, cw + popc64(x & lowmask(b)));
-      }
-      cw += popc64(x);
+      if ((P1 & 63u) == 0) close(P1, cw);  // a 64-aligned segment end is in no window
     }
-    if ((P1 & 63u) == 0) close(P1, cw);  // a 64-aligned segment end is in no window
-  }
-  const size_t o = (size_t)wave * LANES + lane, fs = (size_t)nseg * LANES;
-  const u128 t = tie_big + tie;
-  seg_tot[o] = cw;
-  seg_part[PA_TIEL * fs + o] = (uint64_t)t;
-  seg_part[PA_TIEH * fs + o] = (uint64_t)(t >> 64);
-  if constexpr (EST) {
+    const size_t o = (size_t)sidx * LANES + lane, fs = (size_t)nseg * LANES;
+    const u128 t = tie_big + tie;
+    seg_tot[o] = cw;
+    seg_part[PA_TIEL * fs + o] = (uint64_t)t;
+    seg_part[PA_TIEH * fs + o] = (uint64_t)(t >> 64);
+  };
+  if constexpr (EST != 0) {
+    for (;;) {
+      const uint32_t sidx = next_segment(queue);
+      if (sidx >= nseg) break;
+      walk_segment(sidx, 0u, 0u, segpos[sidx], segpos[sidx + 1]);
+    }
     if (__ballot(bad && lane < est.nl) != 0 && lane == 0) *est.viol = 1u;  // benign race: every writer stores 1
+  } else {
+    const Segment sg = my_segment(nchunks, nseg, wave);
+    const bool any = sg.c0 < sg.c1;
+    walk_segment(wave, sg.c0, sg.c1, any ? chunk_start(gstart, chunk_g, sg.c0) : 0u,
+                 any ? chunk_start(gstart, chunk_g, sg.c1) : 0u);
   }
 }
 
@@ -1180,6 +1251,12 @@ __device__ inline void gather_window(const TBT* __restrict__ TB, const uint32_t*
 #ifndef VR_TAIL_CHECK
 #define VR_TAIL_CHECK 1  // 0: probe builds only -- the tail invariants never flag
 #endif
+#ifndef VR_PROBE_WT
+#define VR_PROBE_WT 0  // timing probe: per-wave start / end clocks of the last k_rankB launch
+#endif
+#if VR_PROBE_WT
+__device__ uint64_t g_wt[2 * 16384];
+#endif
 #ifndef VR_XWIN
 #define VR_XWIN 1  // EST 3 / 4 B walk: next window's streams and masks fetched inside the window (0: off)
 #endif
@@ -1218,7 +1295,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
     const uint32_t* __restrict__ posA_byB, const uint32_t* __restrict__ chunkA_byB,
     const uint32_t* __restrict__ baseA, uint32_t* __restrict__ seg_tot,
     uint64_t* __restrict__ seg_part, uint32_t nseg, const uint2* __restrict__ ftab,
-    uint32_t tabrows, int bits) {
+    uint32_t tabrows, int bits, const uint32_t* __restrict__ segpos, uint32_t* __restrict__ queue) {
   static_assert(!EST || sizeof(TBT) == 2, "EST ranks are u16");
   constexpr int NB = EST ? EBB : BB;  // pairs per gather batch
   extern __shared__ uint64_t smask[];
@@ -1229,268 +1306,290 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
   const bool active = FULL || lane < lw;
   const uint32_t stride = FULL ? (uint32_t)LANES : (uint32_t)lw;
   const uint32_t wave = wave_uniform(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
-  const Segment sg = my_segment(nchunks, nseg, wave);
-  u128 acc = 0;       // sum over B groups of S y'_B
-  uint64_t St = 0;    // sum of S (= sum of included yA)
-  uint64_t tie = 0;   // sum of k^3 - k
-  u128 tie_big = 0;
-  uint32_t cw = 0;
-  if (sg.c0 < sg.c1) {
-    const uint32_t P0 = chunk_start(gstart, chunk_g, sg.c0);
-    const uint32_t P1 = chunk_start(gstart, chunk_g, sg.c1);
-    uint32_t cgs = 0;
-    uint64_t S = 0;  // sum of included yA (absolute doubled A midranks) in the open group
-    auto close = [&](uint32_t ce) {
-      const uint32_t y = cgs + ce + 1u;
-      acc += (u128)S * y;
-      St += S;
-      tie_add<BIGT>(tie, tie_big, ce - cgs);
-      S = 0;
-      cgs = ce;
-    };
-    // EST 3 / 4 (small tie groups): the prefetching walk, which computes the window low
-    // ends from the A positions (a join's streamed low ends, VISREPS_ENGINE_LO_JOIN=1, hold
-    // the same values and are not read)
-    constexpr bool XW = VR_XWIN && (EST == 3 || EST == 4) && !BIGT;
-    constexpr bool walked = XW;
-    if constexpr (XW) {
-      static_assert(EBB == 8, "prefetching batches are 8 pairs");
-      {
-        const uint16_t* TB16 = reinterpret_cast<const uint16_t*>(TB);
-        uint32_t lane_bt;
-        asm("" : "=v"(lane_bt) : "0"((uint32_t)lane * 2u));
-        // stream offset of window wv: lanes past the segment end re-read its last position
-        auto voff_of = [&](uint32_t wv) -> uint32_t {
-          const uint32_t lim = wave_uniform(min(63u, P1 - 1u - wv));
-          return min((uint32_t)lane, lim) * 4u;
-        };
-        // inclusion bits of window wv from its two mask words per lane
-        auto bits_of = [&](uint32_t wv, uint64_t ma, uint64_t mb) -> uint64_t {
-          const uint32_t pos = wv + (uint32_t)lane;
-          const uint64_t v = transpose64((pos >= P0 && pos < P1) ? (ma & mb) : 0ull, lane);
-          return active ? v : 0ull;
-        };
-        uint32_t w = P0 & ~63u;
-        uint32_t cd, pa;
-        xw_ld2(codes + w, posA_byB + w, voff_of(w), cd, pa);
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(cd), "+v"(pa) : : "memory");
-        uint64_t x;
-        if constexpr (!LDS) {
-          uint64_t ma, mb;
-          xw_ldm(m, cd, ma, mb);
-          asm volatile("s_waitcnt vmcnt(0)" : "+v"(ma), "+v"(mb) : : "memory");
-          x = bits_of(w, ma, mb);
-        } else {
-          x = window_bits(m, cd, w, P0, P1, lane, active);
-        }
-        for (;;) {
-          const bool more = w + 64 < P1;
-          const uint32_t wn = more ? w + 64 : w;
-          uint32_t cdn, pan;
-          const uint64_t F = restrict_flags(((uint64_t)sload(gflag + (w >> 5) + 1) << 32) | sload(gflag + (w >> 5)), w,
-                                            P0, P1);
-          uint64_t xn = 0;
-          // the window's batch pipeline; proc(h, ya) consumes batch h's recovered A ranks
-          // (issued inside each of its two instances: a load in flight across the branch into
-          // them would be copied between registers before its wait)
-          auto pipeline = [&](auto&& proc) {
-            uint64_t ma = 0, mb = 0;
-            uint32_t t[2][EBB];
-            xw_ld2(codes + wn, posA_byB + wn, voff_of(wn), cdn, pan);  // S(w+1)
-            gather_issue_t(TB16, stride, pa, 0, lane_bt, t[0]);
-#pragma unroll
-            for (int h = 0; h < 64 / EBB; ++h) {
-              uint32_t(&cur)[EBB] = t[h & 1];
-              if (h + 1 < 64 / EBB) {
-                gather_issue_t(TB16, stride, pa, (h + 1) * EBB, lane_bt, t[(h + 1) & 1]);
-                gather_wait_n<EBB>(cur);
-                if (h == 0) asm volatile("" : "+v"(cdn), "+v"(pan));  // S(w+1): older than G[0]
-                if constexpr (!LDS) {
-                  if (h == 1) xw_ldm(m, cdn, ma, mb);  // M(w+1), behind G[2]
-                }
-                if (h == 2) {  // only G[3] may be in flight: M(w+1) is retired
+#if VR_PROBE_WT
+  if (lane == 0 && wave < 16384u) g_wt[wave] = wall_clock64();
+#endif
+  // One segment [P0, P1) of B positions (a B tie-group start each), partial sums at index
+  // sidx. EST passes: segments of ~M / est_nseg positions (segpos, k_seg_table) taken from
+  // a work queue until none is left, so waves that run slow take fewer of them and the
+  // launch does not end on a tail of late waves; the partial sums stay indexed by segment,
+  // so the scores do not depend on which wave walked what. Exact form: the wave's static
+  // chunk range.
+  auto walk_segment = [&](uint32_t sidx, uint32_t P0, uint32_t P1) {
+    u128 acc = 0;       // sum over B groups of S y'_B
+    uint64_t St = 0;    // sum of S (= sum of included yA)
+    uint64_t tie = 0;   // sum of k^3 - k
+    u128 tie_big = 0;
+    uint32_t cw = 0;
+    if (P0 < P1) {
+      uint32_t cgs = 0;
+      uint64_t S = 0;  // sum of included yA (absolute doubled A midranks) in the open group
+      auto close = [&](uint32_t ce) {
+        const uint32_t y = cgs + ce + 1u;
+        acc += (u128)S * y;
+        St += S;
+        tie_add<BIGT>(tie, tie_big, ce - cgs);
+        S = 0;
+        cgs = ce;
+      };
+      // EST 3 / 4 (small tie groups): the prefetching walk, which computes the window low
+      // ends from the A positions (a join's streamed low ends, VISREPS_ENGINE_LO_JOIN=1, hold
+      // the same values and are not read)
+      constexpr bool XW = VR_XWIN && (EST == 3 || EST == 4) && !BIGT;
+      constexpr bool walked = XW;
+      if constexpr (XW) {
+        static_assert(EBB == 8, "prefetching batches are 8 pairs");
+        {
+          const uint16_t* TB16 = reinterpret_cast<const uint16_t*>(TB);
+          uint32_t lane_bt;
+          asm("" : "=v"(lane_bt) : "0"((uint32_t)lane * 2u));
+          // stream offset of window wv: lanes past the segment end re-read its last position
+          auto voff_of = [&](uint32_t wv) -> uint32_t {
+            const uint32_t lim = wave_uniform(min(63u, P1 - 1u - wv));
+            return min((uint32_t)lane, lim) * 4u;
+          };
+          // inclusion bits of window wv from its two mask words per lane
+          auto bits_of = [&](uint32_t wv, uint64_t ma, uint64_t mb) -> uint64_t {
+            const uint32_t pos = wv + (uint32_t)lane;
+            const uint64_t v = transpose64((pos >= P0 && pos < P1) ? (ma & mb) : 0ull, lane);
+            return active ? v : 0ull;
+          };
+          uint32_t w = P0 & ~63u;
+          uint32_t cd, pa;
+          xw_ld2(codes + w, posA_byB + w, voff_of(w), cd, pa);
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(cd), "+v"(pa) : : "memory");
+          uint64_t x;
+          if constexpr (!LDS) {
+            uint64_t ma, mb;
+            xw_ldm(m, cd, ma, mb);
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(ma), "+v"(mb) : : "memory");
+            x = bits_of(w, ma, mb);
+          } else {
+            x = window_bits(m, cd, w, P0, P1, lane, active);
+          }
+          for (;;) {
+            const bool more = w + 64 < P1;
+            const uint32_t wn = more ? w + 64 : w;
+            uint32_t cdn, pan;
+            const uint64_t F = restrict_flags(((uint64_t)sload(gflag + (w >> 5) + 1) << 32) | sload(gflag + (w >> 5)), w,
+                                              P0, P1);
+            uint64_t xn = 0;
+            // the window's batch pipeline; proc(h, ya) consumes batch h's recovered A ranks
+            // (issued inside each of its two instances: a load in flight across the branch into
+            // them would be copied between registers before its wait)
+            auto pipeline = [&](auto&& proc) {
+              uint64_t ma = 0, mb = 0;
+              uint32_t t[2][EBB];
+              xw_ld2(codes + wn, posA_byB + wn, voff_of(wn), cdn, pan);  // S(w+1)
+              gather_issue_t(TB16, stride, pa, 0, lane_bt, t[0]);
+  #pragma unroll
+              for (int h = 0; h < 64 / EBB; ++h) {
+                uint32_t(&cur)[EBB] = t[h & 1];
+                if (h + 1 < 64 / EBB) {
+                  gather_issue_t(TB16, stride, pa, (h + 1) * EBB, lane_bt, t[(h + 1) & 1]);
+                  gather_wait_n<EBB>(cur);
+                  if (h == 0) asm volatile("" : "+v"(cdn), "+v"(pan));  // S(w+1): older than G[0]
                   if constexpr (!LDS) {
-                    asm volatile("" : "+v"(ma), "+v"(mb));
-                    xn = bits_of(wn, ma, mb);
+                    if (h == 1) xw_ldm(m, cdn, ma, mb);  // M(w+1), behind G[2]
+                  }
+                  if (h == 2) {  // only G[3] may be in flight: M(w+1) is retired
+                    if constexpr (!LDS) {
+                      asm volatile("" : "+v"(ma), "+v"(mb));
+                      xn = bits_of(wn, ma, mb);
+                    } else {
+                      xn = window_bits(m, cdn, wn, P0, P1, lane, active);
+                    }
+                  }
+                } else {
+                  gather_wait_n<0>(cur);
+                }
+                proc(h, cur);
+              }
+            };
+            // the window low ends of the window's A positions, lane j = pair j (3 VALU ops)
+            const uint32_t la = el.Lu + __umulhi(pa << 1, el.Ru);
+            auto recover = [&](uint32_t v, uint32_t j) -> uint32_t {
+  #if VR_XP & 4  // timing probe only: one low end for the whole window (no per-pair readlane)
+              return est_recover(v, readlane_u32(la, 0));
+  #else
+              return est_recover(v, est_lo_b<EST>(el, pa, la, j, lane, v));
+  #endif
+            };
+            auto fast_proc = [&](uint64_t& a64, uint32_t& c1) {
+              return [&](int h, uint32_t* cur) {
+  #pragma unroll
+                for (int q = 0; q < EBB; ++q) {
+                  const uint32_t j = h * EBB + q;
+                  const uint32_t y = recover(cur[q], j);
+                  const uint32_t mk = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
+                  const uint32_t yb = y & mk;
+                  if (j < 63) {
+  #if VR_XP & 1  // timing probe only (wrong scores): no 64-bit multiply-add
+                    a64 = (a64 & ~0xffffffffull) | (uint32_t)((uint32_t)a64 + (yb ^ c1));
+  #else
+                    a64 += (uint64_t)yb * c1;
+  #endif
+  #if VR_XP & 2  // timing probe only: no 64-bit running sum
+                    c1 ^= yb & 1u;
+  #else
+                    St += yb;
+  #endif
+                    c1 -= mk;
                   } else {
-                    xn = window_bits(m, cdn, wn, P0, P1, lane, active);
+                    S = yb;
+                    cgs = c1 - 1u;
                   }
                 }
-              } else {
-                gather_wait_n<0>(cur);
-              }
-              proc(h, cur);
-            }
-          };
-          // the window low ends of the window's A positions, lane j = pair j (3 VALU ops)
-          const uint32_t la = el.Lu + __umulhi(pa << 1, el.Ru);
-          auto recover = [&](uint32_t v, uint32_t j) -> uint32_t {
-#if VR_XP & 4  // timing probe only: one low end for the whole window (no per-pair readlane)
-            return est_recover(v, readlane_u32(la, 0));
-#else
-            return est_recover(v, est_lo_b<EST>(el, pa, la, j, lane, v));
-#endif
-          };
-          auto fast_proc = [&](uint64_t& a64, uint32_t& c1) {
-            return [&](int h, uint32_t* cur) {
-#pragma unroll
+              };
+            };
+            auto slow_proc = [&](int h, uint32_t* cur) {
+  #pragma unroll
               for (int q = 0; q < EBB; ++q) {
                 const uint32_t j = h * EBB + q;
                 const uint32_t y = recover(cur[q], j);
-                const uint32_t mk = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
-                const uint32_t yb = y & mk;
-                if (j < 63) {
-#if VR_XP & 1  // timing probe only (wrong scores): no 64-bit multiply-add
-                  a64 = (a64 & ~0xffffffffull) | (uint32_t)((uint32_t)a64 + (yb ^ c1));
-#else
-                  a64 += (uint64_t)yb * c1;
-#endif
-#if VR_XP & 2  // timing probe only: no 64-bit running sum
-                  c1 ^= yb & 1u;
-#else
-                  St += yb;
-#endif
-                  c1 -= mk;
-                } else {
-                  S = yb;
-                  cgs = c1 - 1u;
-                }
+                if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
+                S += ((x >> j) & 1ull) ? (uint64_t)y : 0ull;
               }
             };
-          };
-          auto slow_proc = [&](int h, uint32_t* cur) {
-#pragma unroll
-            for (int q = 0; q < EBB; ++q) {
-              const uint32_t j = h * EBB + q;
-              const uint32_t y = recover(cur[q], j);
-              if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
-              S += ((x >> j) & 1ull) ? (uint64_t)y : 0ull;
+            if (F == ~0ull) {  // every position starts a group (the per-window form below explains)
+              close(cw);
+              uint64_t a64 = 0;
+              uint32_t c1 = cw + 1u;
+              pipeline(fast_proc(a64, c1));
+              acc += (u128)a64 * 2u;
+            } else {
+              pipeline(slow_proc);
             }
-          };
-          if (F == ~0ull) {  // every position starts a group (the per-window form below explains)
-            close(cw);
-            uint64_t a64 = 0;
-            uint32_t c1 = cw + 1u;
-            pipeline(fast_proc(a64, c1));
-            acc += (u128)a64 * 2u;
-          } else {
-            pipeline(slow_proc);
+            cw += popc64(x);
+            if (!more) break;
+            w = wn;
+            cd = cdn;
+            pa = pan;
+            x = xn;
           }
-          cw += popc64(x);
-          if (!more) break;
-          w = wn;
-          cd = cdn;
-          pa = pan;
-          x = xn;
         }
       }
-    }
-    uint32_t w0 = P0 & ~63u;
-    auto fetch = [&](uint32_t w, uint32_t& pa, uint32_t& ca, uint32_t& cd, uint32_t& f0,
-                     uint32_t& f1) {
-      const uint32_t pos = w + (uint32_t)lane;
-      const bool valid = pos >= P0 && pos < P1;
-      if constexpr (EST >= 5) {  // triangle-order TB: the row is the pair's triangle index
+      uint32_t w0 = P0 & ~63u;
+      auto fetch = [&](uint32_t w, uint32_t& pa, uint32_t& ca, uint32_t& cd, uint32_t& f0,
+                       uint32_t& f1) {
+        const uint32_t pos = w + (uint32_t)lane;
+        const bool valid = pos >= P0 && pos < P1;
+        if constexpr (EST >= 5) {  // triangle-order TB: the row is the pair's triangle index
+          cd = valid ? codes[pos] : 0u;
+          pa = valid ? tri32(cd, (uint32_t)n) : 0u;
+          ca = 0u;
+          f0 = sload(gflag + (w >> 5));
+          f1 = sload(gflag + (w >> 5) + 1);
+          return;
+        }
+        pa = valid ? posA_byB[pos] : 0u;
+        // EST 3/4: the window low end of the pair's A position, L + (2 posA R >> 32), computed
+        // here per lane for the window's 64 pairs (three VALU ops per window lane, no stream),
+        // or streamed from the join (VISREPS_ENGINE_LO_JOIN=1, A/B)
+        if constexpr (EST >= 3)
+          ca = !valid ? 0u : chunkA_byB ? chunkA_byB[pos] : el.Lu + __umulhi(pa << 1, el.Ru);
+        else
+          ca = (!EST && valid) ? chunkA_byB[pos] : 0u;
         cd = valid ? codes[pos] : 0u;
-        pa = valid ? tri32(cd, (uint32_t)n) : 0u;
-        ca = 0u;
         f0 = sload(gflag + (w >> 5));
         f1 = sload(gflag + (w >> 5) + 1);
-        return;
-      }
-      pa = valid ? posA_byB[pos] : 0u;
-      // EST 3/4: the window low end of the pair's A position, L + (2 posA R >> 32), computed
-      // here per lane for the window's 64 pairs (three VALU ops per window lane, no stream),
-      // or streamed from the join (VISREPS_ENGINE_LO_JOIN=1, A/B)
-      if constexpr (EST >= 3)
-        ca = !valid ? 0u : chunkA_byB ? chunkA_byB[pos] : el.Lu + __umulhi(pa << 1, el.Ru);
-      else
-        ca = (!EST && valid) ? chunkA_byB[pos] : 0u;
-      cd = valid ? codes[pos] : 0u;
-      f0 = sload(gflag + (w >> 5));
-      f1 = sload(gflag + (w >> 5) + 1);
-    };
-    uint32_t pa = 0, ca = 0, cd = 0, f0 = 0, f1 = 0;
-    if constexpr (!walked) fetch(w0, pa, ca, cd, f0, f1);
-    for (; !walked && w0 < P1; w0 += 64) {
-      const uint32_t pa_c = pa, ca_c = ca;
-      uint32_t lane_b4, lane_bt;  // opaque per window, so the base + lane sum is not hoisted
-      asm("" : "=v"(lane_b4) : "0"((uint32_t)lane * 4u));
-      asm("" : "=v"(lane_bt) : "0"((uint32_t)lane * (uint32_t)sizeof(TBT)));
-#if VR_PROBE_WB  // timing probe only (wrong scores): no mask lookups, no transpose
-      const uint64_t x = active ? (0xF7DFBEFDFBF7EFDFull ^ ((uint64_t)(cd & 7u) << 3)) : 0ull;
-#else
-      const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
-#endif
-      const uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
-      if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
-      auto gather = [&](auto&& fn) {
-        if constexpr (EST)
-          gather_window_est<EST>(reinterpret_cast<const uint16_t*>(TB), stride, el, pa_c, ca_c, lane_bt, lane, fn);
-        else
-          gather_window<TBT>(TB, baseA, stride, pa_c, ca_c, lane_bt, lane_b4, fn);
       };
-      if (F == ~0ull) {
-        // Every position starts a group (the normal case for continuous RDMs): after
-        // closing the carried group, positions 0..62 are singletons, whose tie term is 0
-        // and whose doubled midrank is 2 (c + 1) with c the included count before them;
-        // position 63 opens the next group. The singleton products yA (c + 1) stay below
-        // 2^50 (yA < 2^32, segment counts < 2^18), so a window sums them in 64 bits.
-        close(cw);
-        uint64_t a64 = 0;
-        uint32_t c1 = cw + 1u;  // 1 + included count before position j
-        gather([&](int h, uint32_t* ya) {
-#pragma unroll
-          for (int q = 0; q < NB; ++q) {
-            const uint32_t j = h * NB + q;
-            // m = -(bit j of x): one sign-extending bit-field extract serves as the select
-            // mask and the count increment (c1 - m = c1 + bit)
-            const uint32_t m = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
-            const uint32_t yb = ya[q] & m;  // x is 0 on inactive lanes
-            if (j < 63) {
-#if VR_PROBE_ACC == 1
-              a64 += yb ^ c1;
-              St += yb;
-              c1 -= m;
-#elif VR_PROBE_ACC == 2
-              a64 += yb ^ c1;
-              c1 -= m;
-#elif VR_PROBE_ACC == 3
-              c1 += yb;
-#else
-              a64 += (uint64_t)yb * c1;
-              St += yb;
-              c1 -= m;
-#endif
-            } else {
-              S = yb;
-              cgs = c1 - 1u;
+      uint32_t pa = 0, ca = 0, cd = 0, f0 = 0, f1 = 0;
+      if constexpr (!walked) fetch(w0, pa, ca, cd, f0, f1);
+      for (; !walked && w0 < P1; w0 += 64) {
+        const uint32_t pa_c = pa, ca_c = ca;
+        uint32_t lane_b4, lane_bt;  // opaque per window, so the base + lane sum is not hoisted
+        asm("" : "=v"(lane_b4) : "0"((uint32_t)lane * 4u));
+        asm("" : "=v"(lane_bt) : "0"((uint32_t)lane * (uint32_t)sizeof(TBT)));
+  #if VR_PROBE_WB  // timing probe only (wrong scores): no mask lookups, no transpose
+        const uint64_t x = active ? (0xF7DFBEFDFBF7EFDFull ^ ((uint64_t)(cd & 7u) << 3)) : 0ull;
+  #else
+        const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+  #endif
+        const uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
+        if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
+        auto gather = [&](auto&& fn) {
+          if constexpr (EST)
+            gather_window_est<EST>(reinterpret_cast<const uint16_t*>(TB), stride, el, pa_c, ca_c, lane_bt, lane, fn);
+          else
+            gather_window<TBT>(TB, baseA, stride, pa_c, ca_c, lane_bt, lane_b4, fn);
+        };
+        if (F == ~0ull) {
+          // Every position starts a group (the normal case for continuous RDMs): after
+          // closing the carried group, positions 0..62 are singletons, whose tie term is 0
+          // and whose doubled midrank is 2 (c + 1) with c the included count before them;
+          // position 63 opens the next group. The singleton products yA (c + 1) stay below
+          // 2^50 (yA < 2^32, segment counts < 2^18), so a window sums them in 64 bits.
+          close(cw);
+          uint64_t a64 = 0;
+          uint32_t c1 = cw + 1u;  // 1 + included count before position j
+          gather([&](int h, uint32_t* ya) {
+  #pragma unroll
+            for (int q = 0; q < NB; ++q) {
+              const uint32_t j = h * NB + q;
+              // m = -(bit j of x): one sign-extending bit-field extract serves as the select
+              // mask and the count increment (c1 - m = c1 + bit)
+              const uint32_t m = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
+              const uint32_t yb = ya[q] & m;  // x is 0 on inactive lanes
+              if (j < 63) {
+  #if VR_PROBE_ACC == 1
+                a64 += yb ^ c1;
+                St += yb;
+                c1 -= m;
+  #elif VR_PROBE_ACC == 2
+                a64 += yb ^ c1;
+                c1 -= m;
+  #elif VR_PROBE_ACC == 3
+                c1 += yb;
+  #else
+                a64 += (uint64_t)yb * c1;
+                St += yb;
+                c1 -= m;
+  #endif
+              } else {
+                S = yb;
+                cgs = c1 - 1u;
+              }
             }
-          }
-        });
-        acc += (u128)a64 * 2u;
-      } else {
-        gather([&](int h, uint32_t* ya) {
-#pragma unroll
-          for (int q = 0; q < NB; ++q) {
-            const uint32_t j = h * NB + q;
-            if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
-            S += ((x >> j) & 1ull) ? (uint64_t)ya[q] : 0ull;  // x is 0 on inactive lanes
-          }
-        });
+          });
+          acc += (u128)a64 * 2u;
+        } else {
+          gather([&](int h, uint32_t* ya) {
+  #pragma unroll
+            for (int q = 0; q < NB; ++q) {
+              const uint32_t j = h * NB + q;
+              if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
+              S += ((x >> j) & 1ull) ? (uint64_t)ya[q] : 0ull;  // x is 0 on inactive lanes
+            }
+          });
+        }
+        cw += popc64(x);
       }
-      cw += popc64(x);
+      if ((P1 & 63u) == 0) close(cw);  // a 64-aligned segment end is in no window
     }
-    if ((P1 & 63u) == 0) close(cw);  // a 64-aligned segment end is in no window
+    const size_t o = (size_t)sidx * LANES + lane, fs = (size_t)nseg * LANES;
+    const u128 tt = tie_big + tie;
+    seg_tot[o] = cw;
+    seg_part[PB_ACCL * fs + o] = (uint64_t)acc;
+    seg_part[PB_ACCH * fs + o] = (uint64_t)(acc >> 64);
+    seg_part[PB_ST * fs + o] = St;
+    seg_part[PB_TIEL * fs + o] = (uint64_t)tt;
+    seg_part[PB_TIEH * fs + o] = (uint64_t)(tt >> 64);
+  };
+  if constexpr (EST != 0) {
+    for (;;) {
+      const uint32_t s = next_segment(queue);
+      if (s >= nseg) break;
+      walk_segment(s, segpos[s], segpos[s + 1]);
+    }
+  } else {
+    const Segment sg = my_segment(nchunks, nseg, wave);
+    const bool any = sg.c0 < sg.c1;
+    walk_segment(wave, any ? chunk_start(gstart, chunk_g, sg.c0) : 0u, any ? chunk_start(gstart, chunk_g, sg.c1) : 0u);
   }
-  const size_t o = (size_t)wave * LANES + lane, fs = (size_t)nseg * LANES;
-  const u128 tt = tie_big + tie;
-  seg_tot[o] = cw;
-  seg_part[PB_ACCL * fs + o] = (uint64_t)acc;
-  seg_part[PB_ACCH * fs + o] = (uint64_t)(acc >> 64);
-  seg_part[PB_ST * fs + o] = St;
-  seg_part[PB_TIEL * fs + o] = (uint64_t)tt;
-  seg_part[PB_TIEH * fs + o] = (uint64_t)(tt >> 64);
+#if VR_PROBE_WT
+  if (lane == 0 && wave < 16384u) g_wt[16384u + wave] = wall_clock64();
+#endif
 }
 
 // ---------------------------------------------------------------------------------
@@ -1517,11 +1616,12 @@ __device__ inline u128 ld128(const uint64_t* p, size_t lo, size_t hi) {
 constexpr int FP_N = 8;  // fpart fields: tA lo/hi, tB lo/hi, X lo/hi, T, S
 __global__ __launch_bounds__(1024) void k_tail_part(
     const uint64_t* __restrict__ segA_part, const uint64_t* __restrict__ segB_part0,
-    const uint32_t* __restrict__ segB_tot0, uint32_t nseg, size_t ustride, uint64_t* __restrict__ fpart0) {
+    const uint32_t* __restrict__ segB_tot0, uint32_t nseg, size_t ustride, uint64_t* __restrict__ fpart0,
+    uint32_t ratioA) {
   __shared__ u128 red[3][16][LANES];
   __shared__ uint64_t red64[2][16][LANES];
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
-  const size_t fs = (size_t)nseg * LANES;
+  const size_t fs = (size_t)nseg * LANES, fsA = fs * ratioA;
   const uint64_t* segB_part = segB_part0 + blockIdx.y * ustride * PB_N;
   const uint32_t* segB_tot = segB_tot0 + blockIdx.y * ustride;
   constexpr int PER = SCAN_SEGS / 16;
@@ -1532,7 +1632,10 @@ __global__ __launch_bounds__(1024) void k_tail_part(
     if (s0 + i >= nseg) break;
     const size_t o = (size_t)(s0 + i) * LANES + lane;
     const uint64_t st = segB_part[PB_ST * fs + o];
-    tA += ld128(segA_part, PA_TIEL * fs + o, PA_TIEH * fs + o);
+    for (uint32_t r = 0; r < ratioA; ++r) {  // the A segments inside B segment s0 + i (any order: exact sums)
+      const size_t oa = ((size_t)(s0 + i) * ratioA + r) * LANES + lane;
+      tA += ld128(segA_part, PA_TIEL * fsA + oa, PA_TIEH * fsA + oa);
+    }
     tB += ld128(segB_part, PB_TIEL * fs + o, PB_TIEH * fs + o);
     X += ld128(segB_part, PB_ACCL * fs + o, PB_ACCH * fs + o) + 2 * (u128)T * st;
     S += st;
@@ -1645,7 +1748,7 @@ static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const
     KtScope kt(KT_RANKA, (double)M, st);
     k_rankA<LDS, FULL, TBT, BTA, false><<<cfg.grid, ENG_THREADS, cfg.lds, st>>>(
         A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<TBT*>(E.TB), lw, E.lpA,
-        E.segA_tot, E.segA_part, nseg, EstA{});
+        E.segA_tot, E.segA_part, nseg, EstA{}, nullptr, nullptr);
     VR_CHECK_LAUNCH();
   }
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
@@ -1669,13 +1772,13 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
   }
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
-  const uint32_t nseg = (uint32_t)cfg.est_nwaves;
+  const uint32_t nseg = cfg.est_nsegA;
   const int bits = cfg.est_b;
   const uint32_t nc = cfg.est_rows;
   {
     KtScope kt(KT_COUNTA, (double)M, st);
     k_countA<CL, FULL><<<cfg.est_grid, ENG_THREADS, CL ? (size_t)n * sizeof(uint64_t) : 0, st>>>(
-        A.codes, A.gstart, A.chunk_g, nch, E.masks, n, lw, bits, E.c0rel, E.c0seg, E.segA_tot, nseg);
+        A.codes, A.gstart, A.chunk_g, nch, E.masks, n, lw, bits, E.c0rel, E.c0seg, E.segA_tot, nseg, E.segposA);
     VR_CHECK_LAUNCH();
   }
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
@@ -1691,7 +1794,7 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
     KtScope kt(KT_RANKA, (double)M, st);
     k_rankA<CL, FULL, uint16_t, BTA, EM><<<cfg.est_grid, ENG_THREADS, cfg.tab, st>>>(
         A.codes, A.gstart, A.chunk_g, A.gflag, nch, E.masks, n, static_cast<uint16_t*>(E.TB), lw, E.lpA,
-        E.segA_tot, E.segA_part, nseg, est);
+        E.segA_tot, E.segA_part, nseg, est, E.segposA, E.queue + QS_RANKA);
     VR_CHECK_LAUNCH();
   }
   return VR_OK;
@@ -1712,14 +1815,14 @@ static int est_predict(const PlanView& A, int64_t n, const EngineWs& E, int lw, 
   }
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
-  const uint32_t nseg = (uint32_t)cfg.est_nwaves;
+  const uint32_t nseg = cfg.est_nsegA;
   int b = 12;
   while (((M + ((int64_t)1 << b) - 1) >> b) > (int64_t)EST_NC) ++b;
   const uint32_t nc = est_intervals(M, b);
   {
     KtScope kt(KT_COUNTA, (double)M, st);
     k_countA<CL, FULL><<<cfg.est_grid, ENG_THREADS, CL ? (size_t)n * sizeof(uint64_t) : 0, st>>>(
-        A.codes, A.gstart, A.chunk_g, nch, E.masks, n, lw, b, E.c0rel, E.c0seg, E.segA_tot, nseg);
+        A.codes, A.gstart, A.chunk_g, nch, E.masks, n, lw, b, E.c0rel, E.c0seg, E.segA_tot, nseg, E.segposA);
     VR_CHECK_LAUNCH();
   }
   VR_TRY(lane_scan(E.segA_tot, nseg, E.bsum, E.segA_pre, E.totA, st));
@@ -1746,14 +1849,22 @@ static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* c
   }
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
-  const uint32_t nseg = (uint32_t)(EST ? cfg.est_nwaves : cfg.nwaves);
+  const uint32_t nseg = EST ? cfg.est_nseg : (uint32_t)cfg.nwaves;
   const size_t us = (size_t)E.useg * (size_t)u;
+  // EST: unit u's B segment starts and its queue counter (slots past QSLOTS are reused, each
+  // cleared right before its launch)
+  const uint32_t* segpos = EST ? E.segposB + E.segstride * (size_t)u : nullptr;
+  uint32_t* q = nullptr;
+  if constexpr (EST != 0) {
+    q = E.queue + QS_RANKB + (size_t)u % (size_t)(QSLOTS - QS_RANKB);
+    if (u >= QSLOTS - QS_RANKB) VR_CHECK_HIP(hipMemsetAsync(q, 0, sizeof(uint32_t), st));
+  }
   {
     KtScope kt(EST == 4 || EST == 6 ? KT_RANKB_FULL : EST ? KT_RANKB_EST : KT_RANKB_EXACT, (double)M, st);
     k_rankB<LDS, FULL, TBT, BTB, EST><<<EST ? cfg.est_grid : cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
         B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
         posA_byB, chunkA_byB, E.baseA, E.segB_tot + us, E.segB_part + us * PB_N, nseg, E.ftab,
-        EST ? cfg.est_rows : 0, EST ? cfg.est_b : 0);
+        EST ? cfg.est_rows : 0, EST ? cfg.est_b : 0, segpos, q);
     VR_CHECK_LAUNCH();
   }
   return VR_OK;
@@ -1762,8 +1873,9 @@ static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* c
 // Tail of a pass for units [0, nb) (their B walks done): the nl scores of each, unit j's at
 // scores + j * score_ld. nan_b[j]: unit j's B plan holds a NaN. *viol <- 1 when a unit's
 // sums break the invariants (k_tail_top).
-static int tail_units(const EngineWs& E, int64_t nb, uint32_t nseg, bool a_nan, const std::vector<char>& nan_b,
-                      int nl, double* scores, int64_t score_ld, uint32_t* viol, hipStream_t st) {
+static int tail_units(const EngineWs& E, int64_t nb, uint32_t nseg, uint32_t ratioA, bool a_nan,
+                      const std::vector<char>& nan_b, int nl, double* scores, int64_t score_ld, uint32_t* viol,
+                      hipStream_t st) {
   const uint32_t nsb = scan_blocks(nseg);
   for (int64_t u0 = 0; u0 < nb; u0 += 64) {  // 64 units per launch (the NaN bitmask)
     const int64_t cnt = std::min<int64_t>(64, nb - u0);
@@ -1772,7 +1884,7 @@ static int tail_units(const EngineWs& E, int64_t nb, uint32_t nseg, bool a_nan, 
       if (nan_b[(size_t)(u0 + j)]) nan_units |= 1ull << j;
     const size_t us = (size_t)E.useg * (size_t)u0;
     k_tail_part<<<dim3(nsb, (unsigned)cnt), 1024, 0, st>>>(E.segA_part, E.segB_part + us * PB_N,
-                                                            E.segB_tot + us, nseg, E.useg, E.fpart);
+                                                            E.segB_tot + us, nseg, E.useg, E.fpart, ratioA);
     VR_CHECK_LAUNCH();
     k_tail_top<<<(unsigned)cnt, LANES, 0, st>>>(E.fpart, nsb, E.totA, a_nan ? 1 : 0, nan_units, nl,
                                                 scores + u0 * score_ld, score_ld, viol);
@@ -1888,6 +2000,17 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
   // the EST 3 estimate checked against the first pass's A counts before any join or pass
   // (VISREPS_ENGINE_EST_PREDICT=0: skip the check; a failing estimate is then caught by the
   // first pass's flags, at the cost of that pass)
+  // EST segment starts of the A plan and of every B plan (k_seg_table), once per call
+  if (est) {
+    const uint32_t ns = cfg.est_nseg, nsA = cfg.est_nsegA;
+    k_seg_table<<<(nsA + 256) / 256, 256, 0, st>>>(A.gstart, A.hdr, M, nsA, E.segposA);
+    VR_CHECK_LAUNCH();
+    for (int64_t j = 0; j < nb; ++j) {
+      k_seg_table<<<(ns + 256) / 256, 256, 0, st>>>(Bs[j].gstart, Bs[j].hdr, M, ns,
+                                                    E.segposB + E.segstride * (size_t)j);
+      VR_CHECK_LAUNCH();
+    }
+  }
   bool predicted_bad = false;
   if (est && cfg.est_mode == 3 && env_int("VISREPS_ENGINE_EST_PREDICT", 1) != 0) {
     const int64_t sub0 = tri ? LANES - 1 : lw;
@@ -1913,7 +2036,7 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
                   ? walk_b<Tg::lds, Tg::full, TBT, true, 0>(Bs[j], pj, cj, n, E, lw, j, cfg, st)
                   : walk_b<Tg::lds, Tg::full, TBT, false, 0>(Bs[j], pj, cj, n, E, lw, j, cfg, st)));
     }
-    return tail_units(E, nb, (uint32_t)cfg.nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0, score_ld, xbad,
+    return tail_units(E, nb, (uint32_t)cfg.nwaves, 1u, h[0].has_nan != 0, nan_b, nl, scores + set0, score_ld, xbad,
                       st);
   };
   // subsets [s0, total) in exact passes of lw
@@ -1947,6 +2070,8 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
           const int64_t set0 = p * sub;
           const int nl = (int)std::min<int64_t>(sub, total - set0);
           VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E.masks, n, st));
+          VR_CHECK_HIP(hipMemsetAsync(E.queue, 0, sizeof(uint32_t) * (size_t)std::min<int64_t>(QS_RANKB + nb, QSLOTS),
+                                      st));  // this pass's work-queue counters
           uint32_t* viol = E.viol + (p - p0);
           auto run_pass = [&](auto em) -> int {
             constexpr int EM = decltype(em)::value;
@@ -1968,7 +2093,7 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
                             ? walk_b<Tg::lds, Tg::full, uint16_t, true, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)
                             : walk_b<Tg::lds, Tg::full, uint16_t, false, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)));
               }
-              return tail_units(E, nb, (uint32_t)cfg.est_nwaves, h[0].has_nan != 0, nan_b, nl, scores + set0,
+              return tail_units(E, nb, cfg.est_nseg, cfg.est_ratioA, h[0].has_nan != 0, nan_b, nl, scores + set0,
                                 score_ld, viol, st);
             }
           };
@@ -2084,6 +2209,12 @@ extern "C" {
 int64_t vr_engine_est_reruns(void) { return g_est_reruns.load(); }
 int64_t vr_engine_est_tail_flags(void) { return g_est_tail_flags.load(); }
 int64_t vr_engine_est_predicted(void) { return g_est_predicted.load(); }
+#if VR_PROBE_WT
+// probe builds only: the wave start / end clocks (wall_clock64, 100 MHz) of the last k_rankB
+int vr_probe_wave_times(uint64_t* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wt), sizeof(uint64_t) * 2 * 16384) == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t vr_bootstrap_workspace(int64_t n) {
   size_t b = 0;
