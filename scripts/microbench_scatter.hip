@@ -113,6 +113,34 @@ __global__ __launch_bounds__(1024) void write_x4(uint16_t* __restrict__ tb, uint
   }
 }
 
+// the gather with the B walk's two 4-B streams per pair (codes, A positions) read
+// sequentially beside it: the rows come from the streamed positions, as in k_rankB
+template <int NB>
+__global__ __launch_bounds__(1024) void gather_streams(const uint16_t* __restrict__ tb, const uint32_t* __restrict__ perm,
+                                                       const uint32_t* __restrict__ codes, uint32_t rows,
+                                                       uint32_t per_wave, uint32_t* out) {
+  const uint32_t wave = blockIdx.x * 16 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t r0 = wave * per_wave;
+  uint32_t acc = 0;
+  for (uint32_t r = r0; r < r0 + per_wave && r < rows; r += 64) {
+    const uint32_t pr = (r + lane < rows) ? perm[r + lane] : 0u;
+    const uint32_t cd = (r + lane < rows) ? codes[r + lane] : 0u;
+    acc ^= cd;
+#pragma unroll
+    for (int h = 0; h < 64; h += NB) {
+      uint32_t v[NB];
+#pragma unroll
+      for (int t = 0; t < NB; ++t) {
+        const uint32_t row = (uint32_t)__builtin_amdgcn_readlane((int)pr, h + t);
+        v[t] = __builtin_nontemporal_load(tb + (size_t)row * 64 + lane);
+      }
+#pragma unroll
+      for (int t = 0; t < NB; ++t) acc += v[t];
+    }
+  }
+  out[wave * 64 + lane] = acc;
+}
+
 int main() {
   const uint32_t rows = 49995000u;  // M at N = 10k
   std::vector<uint32_t> h(rows);
@@ -160,6 +188,11 @@ int main() {
   if (run("gather random NB16", [&] { gather<16><<<grid, 1024>>>(tb, perm, rows, per_wave, out); })) return 1;
   if (run("write seq x4 (16 B/lane)", [&] { write_x4<false><<<grid, 1024>>>(tb, rows, per_wave); })) return 1;
   if (run("write seq x4 NT", [&] { write_x4<true><<<grid, 1024>>>(tb, rows, per_wave); })) return 1;
+  uint32_t* codes2;
+  CK(hipMalloc(&codes2, (size_t)rows * 4));
+  CK(hipMemset(codes2, 1, (size_t)rows * 4));
+  if (run("gather random + 2 streams NB8", [&] { gather_streams<8><<<grid, 1024>>>(tb, perm, codes2, rows, per_wave, out); })) return 1;
+  if (run("gather random + 2 streams NB16", [&] { gather_streams<16><<<grid, 1024>>>(tb, perm, codes2, rows, per_wave, out); })) return 1;
   auto gb = [&](auto k) { k<<<grid, 1024>>>((const uint8_t*)tb, perm, rows, per_wave, out); };
   if (run("gather random 64B u8 NB16", [&] { gb(gather_n<16, uint8_t, 64>); })) return 1;
   if (run("gather random 64B u16 NB16", [&] { gb(gather_n<16, uint16_t, 64>); })) return 1;

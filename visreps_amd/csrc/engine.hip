@@ -1367,12 +1367,15 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
           } else {
             x = window_bits(m, cd, w, P0, P1, lane, active);
           }
+          // group-start flags of the window (scalar loads), fetched one window ahead
+          uint32_t f0 = sload(gflag + (w >> 5)), f1 = sload(gflag + (w >> 5) + 1);
           for (;;) {
             const bool more = w + 64 < P1;
             const uint32_t wn = more ? w + 64 : w;
             uint32_t cdn, pan;
-            const uint64_t F = restrict_flags(((uint64_t)sload(gflag + (w >> 5) + 1) << 32) | sload(gflag + (w >> 5)), w,
-                                              P0, P1);
+            const uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w, P0, P1);
+            f0 = sload(gflag + (wn >> 5));
+            f1 = sload(gflag + (wn >> 5) + 1);
             uint64_t xn = 0;
             // the window's batch pipeline; proc(h, ya) consumes batch h's recovered A ranks
             // (issued inside each of its two instances: a load in flight across the branch into
