@@ -1,5 +1,5 @@
 #!/bin/bash
-# Triangle-order TB (EST 5/6, default) vs the A-order TB + joins (VISREPS_ENGINE_TRI=0):
+# Triangle-order TB (EST 5/6, opt-in VISREPS_ENGINE_TRI=1) vs the default A-order TB + joins:
 # engine parity tests, then one bench line of each form (no CPU baseline, no extra legs).
 # Usage (via gpurun): bash scripts/gpu_tri_ab.sh <tag> [test files...]
 set -o pipefail
