@@ -182,6 +182,25 @@ int vr_bootstrap_spearman_multi(const void* plan_a, const void* const* planBs, i
                                 int64_t n, const int32_t* idx, int64_t k, int64_t n_sets,
                                 int full_first, double* scores, int64_t ld_scores, void* ws,
                                 size_t ws_bytes, void* stream);
+/* Shared joins for units that share their B plan across up to 4 A plans (the neural RDMs of
+ * the regions one model layer is scored against; the per-unit joins of
+ * vr_bootstrap_spearman_multi, evals.py:355-373's loop over regions). vr_engine_posmap4
+ * interleaves the A plans' pair -> position maps into 16-B records (posmap4: workspace of
+ * vr_engine_posmap4_bytes(n)); vr_engine_join4 then gives, for one B plan, posA[i][q] = the
+ * position in A plan i of B's pair at position q (M u32 each) with one 16-B gather per pair,
+ * where one join per unit gathers a random line per pair for each A plan. */
+size_t vr_engine_posmap4_bytes(int64_t n);
+int vr_engine_posmap4(const void* const* plan_as, int64_t n_a, int64_t n, void* posmap4, void* stream);
+int vr_engine_join4(const void* posmap4, int64_t n_a, const void* plan_b, int64_t n, uint32_t* const* posA,
+                    void* stream);
+/* vr_bootstrap_spearman_multi with every unit's A positions already joined (posA[j], M u32,
+ * from vr_engine_join4 against this call's A plan): the EST passes read them and skip the
+ * per-unit joins; an exact-form fallback rewrites posA[j] with the same values. Workspace
+ * as vr_bootstrap_spearman_multi. */
+int vr_bootstrap_spearman_multi_joined(const void* plan_a, const void* const* planBs, int64_t n_b, int64_t n,
+                                       const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
+                                       double* scores, int64_t ld_scores, uint32_t* const* posA, void* ws,
+                                       size_t ws_bytes, void* stream);
 
 /* Passes of the bootstrap engines run in a one-gather-per-pair form (absolute ranks kept
  * modulo 2^16 and recovered against a count estimate). A pass whose ranks the estimate

@@ -183,6 +183,25 @@ def test_structured_rdm_goes_exact_up_front(dev, monkeypatch):
     assert np.array_equal(late, ref)
 
 
+@pytest.mark.parametrize("form", ["1", "0"])
+def test_shared_joins_equal_per_unit_joins(dev, form):
+    # SharedJoins (one 16-B gather per model pair for up to 4 neural plans) + the joined
+    # multi call against the plain multi call, EST and exact forms, 3 and 1 A plans
+    n = 1800
+    neurals = [R.RankPlan(_rdm(dev, n, 90 + 10 * i, 60 + i)) for i in range(3)]
+    models = [R.RankPlan(_rdm(dev, n, 70, 70, relu=True)), R.RankPlan(_rdm(dev, n, 150, 71))]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 100)
+    with _engine_form(form):
+        for group in (neurals, neurals[:1]):
+            sj = R.SharedJoins(group)
+            joins = [sj.join(pm) for pm in models]  # joins[m][a]
+            for a, pn in enumerate(group):
+                ref = R.bootstrap_spearman_multi(pn, models, idx, full_first=True).cpu().numpy()
+                got = R.bootstrap_spearman_multi(pn, models, idx, full_first=True,
+                                                 joined=[joins[m][a] for m in range(len(models))]).cpu().numpy()
+                assert np.array_equal(got, ref)
+
+
 def test_half_tied_rdm_exact_join_is_fast(dev):
     # One tie group over half the 12.5 M pairs (n = 5000): it spans ~1000 of the exact
     # form's group-aligned chunks, so the join's chunk lookup must be a binary search

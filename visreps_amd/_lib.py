@@ -103,6 +103,13 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _c_sz, _vp],
     ),
+    "vr_bootstrap_spearman_multi_joined": (
+        ctypes.c_int,
+        [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _vp, _c_sz, _vp],
+    ),
+    "vr_engine_posmap4_bytes": (_c_sz, [_c_i64]),
+    "vr_engine_posmap4": (ctypes.c_int, [_vp, _c_i64, _c_i64, _vp, _vp]),
+    "vr_engine_join4": (ctypes.c_int, [_vp, _c_i64, _vp, _c_i64, _vp, _vp]),
     "vr_engine_est_reruns": (_c_i64, []),
     "vr_engine_est_tail_flags": (_c_i64, []),
     "vr_engine_est_predicted": (_c_i64, []),

@@ -216,11 +216,14 @@ def bootstrap_spearman_multi(
     idx: Optional[np.ndarray | torch.Tensor],
     *,
     full_first: bool = True,
+    joined: Optional[Sequence[torch.Tensor]] = None,
 ) -> torch.Tensor:
     """Spearman of every plan in plans_b against plan_a on the same subsets:
     (len(plans_b), total) float64 scores on the device. Row j equals
     bootstrap_spearman(plans_b[j], plan_a, idx) bit for bit; plan_a's rank walk runs
-    once per pass of 64 subsets for all of them (a neural RDM against every layer)."""
+    once per pass of 64 subsets for all of them (a neural RDM against every layer).
+    joined[j]: plans_b[j]'s pairs already joined to plan_a (SharedJoins), so the call skips
+    its per-unit joins (vr_bootstrap_spearman_multi_joined)."""
     plans_b = list(plans_b)
     for pb in plans_b:
         if pb.n != plan_a.n or pb.device != plan_a.device:
@@ -237,15 +240,65 @@ def bootstrap_spearman_multi(
     ws = workspace.get(dev, L.vr_bootstrap_multi_workspace(n, nb), "engine")
     ptrs = (ctypes.c_void_p * nb)(*[_ptr(pb.buf) for pb in plans_b])
     with torch.cuda.device(dev):
-        check(
-            L.vr_bootstrap_spearman_multi(
-                _ptr(plan_a.buf), ctypes.cast(ptrs, ctypes.c_void_p), nb, n,
-                _ptr(idx_t) if idx_t.numel() else None, k, n_sets, int(full_first),
-                _ptr(scores), total, _ptr(ws), ws.numel(), stream_of(dev),
-            ),
-            "vr_bootstrap_spearman_multi",
-        )
+        if joined is None:
+            check(
+                L.vr_bootstrap_spearman_multi(
+                    _ptr(plan_a.buf), ctypes.cast(ptrs, ctypes.c_void_p), nb, n,
+                    _ptr(idx_t) if idx_t.numel() else None, k, n_sets, int(full_first),
+                    _ptr(scores), total, _ptr(ws), ws.numel(), stream_of(dev),
+                ),
+                "vr_bootstrap_spearman_multi",
+            )
+        else:
+            joined = list(joined)
+            M = n * (n - 1) // 2
+            if len(joined) != nb or any(t.dtype != torch.int32 or t.numel() != M or t.device != dev
+                                        or not t.is_contiguous() for t in joined):
+                raise ValueError("joined: one contiguous int32 tensor of M pairs per B plan, on the plans' device")
+            jp = (ctypes.c_void_p * nb)(*[_ptr(t) for t in joined])
+            check(
+                L.vr_bootstrap_spearman_multi_joined(
+                    _ptr(plan_a.buf), ctypes.cast(ptrs, ctypes.c_void_p), nb, n,
+                    _ptr(idx_t) if idx_t.numel() else None, k, n_sets, int(full_first),
+                    _ptr(scores), total, ctypes.cast(jp, ctypes.c_void_p), _ptr(ws), ws.numel(), stream_of(dev),
+                ),
+                "vr_bootstrap_spearman_multi_joined",
+            )
     return scores
+
+
+class SharedJoins:
+    """The joins of up to 4 A plans (the neural RDMs of a model layer's regions) with any B
+    plan, one 16-B gather per B pair instead of one random line per pair and A plan
+    (vr_engine_posmap4 once, then vr_engine_join4 per B plan). join(plan_b) -> one int32
+    tensor of M positions per A plan, for bootstrap_spearman_multi(..., joined=...)."""
+
+    def __init__(self, plans_a: Sequence[RankPlan]):
+        self.plans_a = list(plans_a)
+        if not 1 <= len(self.plans_a) <= 4:
+            raise ValueError("SharedJoins takes 1 to 4 A plans")
+        pa0 = self.plans_a[0]
+        for pa in self.plans_a:
+            if pa.n != pa0.n or pa.device != pa0.device:
+                raise ValueError("rank plans must describe RDMs of the same size and device")
+        self.n, self.device = pa0.n, pa0.device
+        L = lib()
+        self.pm4 = torch.empty(int(L.vr_engine_posmap4_bytes(self.n)), dtype=torch.uint8, device=self.device)
+        ptrs = (ctypes.c_void_p * len(self.plans_a))(*[_ptr(pa.buf) for pa in self.plans_a])
+        with torch.cuda.device(self.device):
+            check(L.vr_engine_posmap4(ctypes.cast(ptrs, ctypes.c_void_p), len(self.plans_a), self.n, _ptr(self.pm4),
+                                      stream_of(self.device)), "vr_engine_posmap4")
+
+    def join(self, plan_b: RankPlan) -> List[torch.Tensor]:
+        if plan_b.n != self.n or plan_b.device != self.device:
+            raise ValueError("rank plans must describe RDMs of the same size and device")
+        M = self.n * (self.n - 1) // 2
+        outs = [torch.empty(M, dtype=torch.int32, device=self.device) for _ in self.plans_a]
+        op = (ctypes.c_void_p * len(outs))(*[_ptr(t) for t in outs])
+        with torch.cuda.device(self.device):
+            check(lib().vr_engine_join4(_ptr(self.pm4), len(outs), _ptr(plan_b.buf), self.n,
+                                        ctypes.cast(op, ctypes.c_void_p), stream_of(self.device)), "vr_engine_join4")
+        return outs
 
 
 def _idx_tensor(idx, dev: torch.device) -> torch.Tensor:

@@ -124,6 +124,7 @@ struct EngineCfg {
   uint32_t est_nseg;   // EST B-walk segments (work queue; est_segments)
   uint32_t est_nsegA;  // EST A-side segments: est_nseg x est_ratioA (k_countA, k_rankA)
   uint32_t est_ratioA;
+  bool prejoined = false;  // the units' A positions arrive joined (vr_bootstrap_spearman_multi_joined)
   size_t tab;         // EST rank walks' dynamic LDS: [masks] + table
 };
 
@@ -300,6 +301,32 @@ __global__ void k_join_lo(const uint32_t* __restrict__ posA_byB, int64_t M, uint
                           uint32_t Lu, uint32_t Ru) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < M) second[i] = Lu + __umulhi(posA_byB[i] << 1, Ru);
+}
+
+// Shared joins: the position maps of up to 4 A plans interleaved into 16-B records, so one
+// random 16-B gather per B pair gives its A position in every one of them (k_join4) where
+// separate joins each pay a random line per pair for 4 B.
+struct Maps4 {
+  const uint32_t* p[4];
+};
+struct Outs4 {
+  uint32_t* p[4];
+};
+__global__ void k_posmap4(Maps4 m, int na, int64_t M, uint4* __restrict__ pm4) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= M) return;
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  for (int i = 0; i < na; ++i) v[i] = __builtin_nontemporal_load(m.p[i] + q);
+  pm4[q] = make_uint4(v[0], v[1], v[2], v[3]);
+}
+__global__ void k_join4(const uint32_t* __restrict__ codesB, int64_t M, int64_t n, const uint4* __restrict__ pm4,
+                        int na, Outs4 out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const uint32_t cb = __builtin_nontemporal_load(codesB + i);
+  const uint4 r = pm4[tri_index(cb >> 16, cb & 0xffffu, (uint64_t)n)];
+  const uint32_t v[4] = {r.x, r.y, r.z, r.w};
+  for (int a = 0; a < na; ++a) __builtin_nontemporal_store(v[a], out.p[a] + i);
 }
 
 // bit w of masks[x] <- x in subset (set0 + w); subset 0 is "all stimuli" when full_first.
@@ -2024,7 +2051,10 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
       return est_predict<Tg::lds, Tg::full>(A, n, E, lw, nl0, full_first != 0, cfg, e3, st, predicted_bad);
     }));
   }
-  if (!tri && !predicted_bad) VR_TRY(join(!est ? JOIN_CHUNK : (lo_join ? JOIN_LO : JOIN_NONE)));
+  // (pre-joined units already hold their A positions: an EST call reading only those skips
+  // the join; an exact-form one rewrites them with the same values beside the A chunks)
+  if (!tri && !predicted_bad && !(cfg.prejoined && est && !lo_join))
+    VR_TRY(join(!est ? JOIN_CHUNK : (lo_join ? JOIN_LO : JOIN_NONE)));
   // the exact chunk-base form of subsets [set0, set0 + nl), nl <= lw
   auto exact_pass = [&](auto tag, int64_t set0, int nl) -> int {
     using Tg = decltype(tag);
@@ -2281,6 +2311,80 @@ int vr_bootstrap_spearman_multi(const void* planA, const void* const* planBs, in
   for (int64_t j = 0; j < n_b; ++j) Bs.push_back(plan_layout(const_cast<void*>(planBs[j]), n));
   return run_engine_multi(A, Bs.data(), n_b, n, idx, k, n_sets, full_first, scores, ld_scores,
                           joins.data(), E, LANES, cfg, as_stream(stream));
+}
+
+int vr_bootstrap_spearman_multi_joined(const void* planA, const void* const* planBs, int64_t n_b, int64_t n,
+                                const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
+                                double* scores, int64_t ld_scores, uint32_t* const* posA, void* ws,
+                                size_t ws_bytes, void* stream) {
+  VR_REQUIRE(n >= 0 && n <= 65535, "vr_bootstrap_spearman_multi_joined: n=%lld out of range", (long long)n);
+  VR_REQUIRE(n_b >= 0, "vr_bootstrap_spearman_multi_joined: n_b=%lld", (long long)n_b);
+  VR_REQUIRE(planA && (n_b == 0 || (planBs && scores)), "vr_bootstrap_spearman_multi_joined: null pointer");
+  VR_REQUIRE(k >= 0 && k <= n && n_sets >= 0, "vr_bootstrap_spearman_multi_joined: bad k=%lld sets=%lld",
+             (long long)k, (long long)n_sets);
+  VR_REQUIRE(idx != nullptr || n_sets == 0 || k == 0, "vr_bootstrap_spearman_multi_joined: null idx");
+  const int64_t total = n_sets + (full_first ? 1 : 0);
+  VR_REQUIRE(n_b <= 1 || ld_scores >= total, "vr_bootstrap_spearman_multi_joined: ld_scores %lld < %lld",
+             (long long)ld_scores, (long long)total);
+  for (int64_t j = 0; j < n_b; ++j)
+    VR_REQUIRE(planBs[j] != nullptr, "vr_bootstrap_spearman_multi_joined: planBs[%lld] is null", (long long)j);
+  VR_REQUIRE(n_b == 0 || posA != nullptr, "vr_bootstrap_spearman_multi_joined: null posA");
+  for (int64_t j = 0; j < n_b; ++j)
+    VR_REQUIRE(posA[j] != nullptr, "vr_bootstrap_spearman_multi_joined: posA[%lld] is null", (long long)j);
+  EngineCfg cfg = engine_cfg(n);
+  cfg.prejoined = true;
+  const size_t need = multi_layout(nullptr, n, n_b, cfg.nwaves, nullptr, nullptr);
+  if (ws_bytes < need || ws == nullptr) {
+    set_error("vr_bootstrap_spearman_multi_joined: workspace %zu < %zu", ws_bytes, need);
+    return VR_EWORKSPACE;
+  }
+  EngineWs E;
+  std::vector<uint32_t*> joins;
+  multi_layout(ws, n, n_b, cfg.nwaves, &E, &joins);
+  for (int64_t j = 0; j < n_b; ++j) joins[(size_t)(2 * j)] = posA[j];
+  const PlanView A = plan_layout(const_cast<void*>(planA), n);
+  std::vector<PlanView> Bs;
+  for (int64_t j = 0; j < n_b; ++j) Bs.push_back(plan_layout(const_cast<void*>(planBs[j]), n));
+  return run_engine_multi(A, Bs.data(), n_b, n, idx, k, n_sets, full_first, scores, ld_scores,
+                          joins.data(), E, LANES, cfg, as_stream(stream));
+}
+
+size_t vr_engine_posmap4_bytes(int64_t n) { return (size_t)pairs_of(n) * sizeof(uint4); }
+
+int vr_engine_posmap4(const void* const* planAs, int64_t n_a, int64_t n, void* posmap4, void* stream) {
+  VR_REQUIRE(n >= 2 && n <= 65535, "vr_engine_posmap4: n=%lld out of range", (long long)n);
+  VR_REQUIRE(n_a >= 1 && n_a <= 4, "vr_engine_posmap4: n_a=%lld not in [1, 4]", (long long)n_a);
+  VR_REQUIRE(planAs && posmap4, "vr_engine_posmap4: null pointer");
+  Maps4 m{{nullptr, nullptr, nullptr, nullptr}};
+  for (int64_t i = 0; i < n_a; ++i) {
+    VR_REQUIRE(planAs[i] != nullptr, "vr_engine_posmap4: planAs[%lld] is null", (long long)i);
+    m.p[i] = plan_layout(const_cast<void*>(planAs[i]), n).pos_map;
+  }
+  const int64_t M = pairs_of(n);
+  k_posmap4<<<(unsigned)((M + 255) / 256), 256, 0, as_stream(stream)>>>(m, (int)n_a, M,
+                                                                         static_cast<uint4*>(posmap4));
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+int vr_engine_join4(const void* posmap4, int64_t n_a, const void* planB, int64_t n, uint32_t* const* posA,
+                    void* stream) {
+  VR_REQUIRE(n >= 2 && n <= 65535, "vr_engine_join4: n=%lld out of range", (long long)n);
+  VR_REQUIRE(n_a >= 1 && n_a <= 4, "vr_engine_join4: n_a=%lld not in [1, 4]", (long long)n_a);
+  VR_REQUIRE(posmap4 && planB && posA, "vr_engine_join4: null pointer");
+  Outs4 o{{nullptr, nullptr, nullptr, nullptr}};
+  for (int64_t i = 0; i < n_a; ++i) {
+    VR_REQUIRE(posA[i] != nullptr, "vr_engine_join4: posA[%lld] is null", (long long)i);
+    o.p[i] = posA[i];
+  }
+  const int64_t M = pairs_of(n);
+  const PlanView B = plan_layout(const_cast<void*>(planB), n);
+  hipStream_t st = as_stream(stream);
+  KtScope kt(KT_JOIN, (double)M, st);
+  k_join4<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(B.codes, M, n, static_cast<const uint4*>(posmap4), (int)n_a,
+                                                       o);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
 }
 
 size_t vr_bootstrap_spearman_workspace(int64_t n) {

@@ -690,11 +690,14 @@ def engine_pair_bytes(est: Optional[bool] = None, tri: bool = False) -> Tuple[in
     return 4 + 4 + 128, 4 + 4 + lo + 128, 4 + 4 + 4 + lo
 
 
-def engine_call_bytes(n: int, subsets: int, units: int) -> float:
+def engine_call_bytes(n: int, subsets: int, units: int, joined: bool = False) -> float:
     """Algorithmic HBM bytes of one engine call: `units` B plans against one A plan over
-    `subsets` subsets (64 per pass; 63 in the triangle-order form)."""
+    `subsets` subsets (64 per pass; 63 in the triangle-order form); joined: the units' joins
+    were done beforehand (SharedJoins, counted by shared_join_bytes)."""
     tri = engine_tri(n)
     a, b, j = engine_pair_bytes(tri=tri)
+    if joined:
+        j = 0
     M = n * (n - 1) // 2
     passes = -(-subsets // (63 if tri else 64))
     return float(M) * (passes * (a + units * b) + units * j)
@@ -715,21 +718,60 @@ def run_unit(plan_m: R.RankPlan, plan_n: R.RankPlan, idx: Optional[np.ndarray],
     return scores
 
 
+def shared_join_bytes(n: int, n_a: int, n_b: int) -> float:
+    """Algorithmic bytes of SharedJoins over n_a A plans and n_b B plans: the interleave
+    (4 B read per A plan, 16 B written per pair) and per B plan its codes 4 + the 16-B record
+    gather + 4 B written per A plan."""
+    M = n * (n - 1) // 2
+    return float(M) * (4 * n_a + 16 + n_b * (4 + 16 + 4 * n_a))
+
+
 def run_group(plan_n: R.RankPlan, plans_m: Sequence[R.RankPlan], idx: Optional[np.ndarray],
-              times: Optional[StepTimes] = None) -> torch.Tensor:
+              times: Optional[StepTimes] = None, joined: Optional[Sequence[torch.Tensor]] = None) -> torch.Tensor:
     """Units (m, n) for every model plan m against one neural plan n in one engine call:
-    (len(plans_m), 1 + n_boot) scores; the neural plan's rank walk is shared."""
+    (len(plans_m), 1 + n_boot) scores; the neural plan's rank walk is shared. joined: the
+    units' A positions from SharedJoins."""
     ev = None
     if times is not None:
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-    scores = R.bootstrap_spearman_multi(plan_n, plans_m, idx, full_first=True)
+    if joined is None:
+        scores = R.bootstrap_spearman_multi(plan_n, plans_m, idx, full_first=True)
+    else:
+        scores = R.bootstrap_spearman_multi(plan_n, plans_m, idx, full_first=True, joined=joined)
     if times is not None:
         ev[1].record()
         nb = 0 if idx is None else len(idx)
-        times.record("engine", ev[0], ev[1], engine_call_bytes(plan_n.n, nb + 1, len(plans_m)),
+        times.record("engine", ev[0], ev[1], engine_call_bytes(plan_n.n, nb + 1, len(plans_m), joined is not None),
                      calls=len(plans_m), ref=engine_bytes(plan_n.n, nb) * len(plans_m))
     return scores
+
+
+def shared_joins(pns: Dict[str, R.RankPlan], by_region: Dict[str, List[str]], mplans: Dict[str, R.RankPlan],
+                 times: Optional[StepTimes] = None) -> Dict[Tuple[str, str], torch.Tensor]:
+    """A positions of every (point, region) unit, regions in groups of up to 4 sharing one
+    16-B gather per model pair (SharedJoins): {(p, r): int32 (M,)}. A group's record table
+    exists only while its model joins run."""
+    out: Dict[Tuple[str, str], torch.Tensor] = {}
+    regions = list(by_region)
+    for g0 in range(0, len(regions), 4):
+        grp = regions[g0:g0 + 4]
+        ev = None
+        if times is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        sj = R.SharedJoins([pns[r] for r in grp])
+        pts = sorted({p for r in grp for p in by_region[r]}, key=lambda p: list(mplans).index(p))
+        for p in pts:
+            outs = sj.join(mplans[p])
+            for r, t in zip(grp, outs):
+                if p in by_region[r]:
+                    out[(p, r)] = t
+        del sj
+        if times is not None:
+            ev[1].record()
+            times.record("engine", ev[0], ev[1], shared_join_bytes(pns[grp[0]].n, len(grp), len(pts)), calls=0)
+    return out
 
 
 def unit_split(units: Sequence, world: int) -> List[Tuple[int, int]]:
@@ -898,9 +940,23 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
     by_region: Dict[str, List[str]] = {}
     for p, r in mine:
         by_region.setdefault(r, []).append(p)
+    # Shared joins (the default engine, >= 2 regions on this rank, VISREPS_SHARED_JOINS not 0,
+    # and the join arrays -- 4 B per pair and unit -- within a quarter of the free memory):
+    # every model pair gathers its positions in up to 4 neural plans at once
+    joined = None
+    if (group_fn is run_group and plan_fn is R.RankPlan and len(by_region) >= 2 and n_boot > 0
+            and os.environ.get("VISREPS_SHARED_JOINS", "1") != "0"):
+        dev = neural_rdms[mine[0][1]].device
+        need = 4.0 * (n * (n - 1) // 2) * (len(mine) + 4)
+        if dev.type == "cuda" and need <= 0.25 * torch.cuda.mem_get_info(dev)[0]:
+            pns = {r: (plans[("n", r)] if ("n", r) in plans else plan_fn(neural_rdms[r])) for r in by_region}
+            joined = shared_joins(pns, by_region, mplans, times)
     for r, pts in by_region.items():
-        pn = plans[("n", r)] if ("n", r) in plans else plan_fn(neural_rdms[r])
-        out = group_fn(pn, [mplans[p] for p in pts], idx, times)
+        pn = plans[("n", r)] if ("n", r) in plans else (pns[r] if joined is not None else plan_fn(neural_rdms[r]))
+        if joined is not None:
+            out = group_fn(pn, [mplans[p] for p in pts], idx, times, joined=[joined.pop((p, r)) for p in pts])
+        else:
+            out = group_fn(pn, [mplans[p] for p in pts], idx, times)
         for j, p in enumerate(pts):
             local[(p, r)] = np.asarray(torch.as_tensor(out[j]).cpu())
         del pn
