@@ -577,13 +577,16 @@ def main():
             roof["traffic_over_algorithmic"] = round(rb_pmc["bytes_per_launch"] / rb["bytes_per_launch"], 3)
         roof_engine = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(eng_gbs / HBM_PEAK_GBS, 4),
-                       "scope": ("whole engine calls (vr_bootstrap_spearman_multi: joins, A walks, B walks, "
-                                 "tails), HIP events around each call"),
+                       "scope": ("whole engine calls (vr_bootstrap_spearman_multi[_joined]: A walks, B walks, "
+                                 "tails, per-unit joins) and the shared joins before them (k_posmap4 + k_join4), "
+                                 "HIP events around each"),
                        "algorithmic_bytes_per_unit": round(times.engine_bytes / calls),
                        "algorithmic_bytes_model": (f"per pair: A side {a_b} B per pass (count pre-pass codes 4, "
                                                    "rank walk codes 4 + 128 B TB row write; shared by the "
                                                    f"call's units), B walk {b_b} B per pass and unit, join "
-                                                   f"{j_b} B per unit"),
+                                                   f"{j_b} B per unit, or with shared joins per model pair codes 4 + "
+                                                   "16-B record gather + 4 B per region written, and the 16-B "
+                                                   "record table built once (pipeline.shared_join_bytes)"),
                        "avg_unit_ms": round(unit_ms, 3),
                        "traffic_per_unit": round(pmc["bytes_per_unit"]) if pmc else None,
                        "reference_equivalent_gbs": round(ref_gbs, 1),
