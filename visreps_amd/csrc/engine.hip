@@ -2042,7 +2042,9 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
     }
   }
   bool predicted_bad = false;
-  if (est && cfg.est_mode == 3 && env_int("VISREPS_ENGINE_EST_PREDICT", 1) != 0) {
+  // (only when some lane holds a bootstrap subset: the full-set lane is exact by
+  // construction, and a point-only call -- phase 1's 56 -- would pay a host sync for nothing)
+  if (est && cfg.est_mode == 3 && n_sets > 0 && env_int("VISREPS_ENGINE_EST_PREDICT", 1) != 0) {
     const int64_t sub0 = tri ? LANES - 1 : lw;
     const int nl0 = (int)std::min<int64_t>(sub0, total);
     VR_TRY(build_pass_masks(idx, k, 0, nl0, full_first, E.masks, n, st));
