@@ -356,3 +356,23 @@ def test_gloo_phase1_points_dealt_over_ranks(tmp_path, world):
         got = {kv.split(":")[0]: float(kv.split(":")[1]) for kv in pairs}
         assert all(abs(got[p] - want[p]) < 1e-12 for p in full), (got, want)
         assert best == max(full, key=lambda p: (want[p], -list(full).index(p)))
+
+
+def test_engine_byte_models(monkeypatch):
+    # pipeline's algorithmic byte models (bench.py's engine roofline): EST passes move 136 B
+    # per pair and unit in the B walk (codes 4 + A position 4 + the 128-B TB row) and 136 B
+    # per pair in the A side; the per-unit join 12 B (VISREPS_ENGINE_LO_JOIN=1: + 4 + 4);
+    # a joined call (SharedJoins) leaves its joins to shared_join_bytes
+    import visreps_amd.pipeline as P
+
+    monkeypatch.delenv("VISREPS_ENGINE_LO_JOIN", raising=False)
+    monkeypatch.delenv("VISREPS_ENGINE_TRI", raising=False)
+    assert P.engine_pair_bytes(True) == (136, 136, 12)
+    monkeypatch.setenv("VISREPS_ENGINE_LO_JOIN", "1")
+    assert P.engine_pair_bytes(True) == (136, 140, 16)
+    monkeypatch.delenv("VISREPS_ENGINE_LO_JOIN")
+    n, M = 10000, 10000 * 9999 // 2
+    per = P.engine_call_bytes(n, 1001, 14)
+    assert per == M * (16 * (136 + 14 * 136) + 14 * 12)
+    assert P.engine_call_bytes(n, 1001, 14, joined=True) == M * 16 * (136 + 14 * 136)
+    assert P.shared_join_bytes(n, 4, 14) == M * (16 + 16 + 14 * (4 + 16 + 16))
