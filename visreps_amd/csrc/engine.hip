@@ -140,10 +140,8 @@ static int env_int(const char* name, int dflt) {
 // the A side cuts each of them into est_ratioA (VISREPS_ENGINE_SEGS_A, default and most
 // VR_SEGS_PER_WAVE) for its own queue (k_rankA; k_countA takes them round-robin).
 static uint32_t est_segments(int64_t M, int est_nwaves) {
-  // VISREPS_ENGINE_SEGS_B: B-walk segments per resident wave (A/B; default 1)
-  const int per = std::max(1, std::min(VR_SEGS_PER_WAVE, env_int("VISREPS_ENGINE_SEGS_B", 1)));
   const int64_t by_len = (M + 255) / 256;
-  return (uint32_t)std::max<int64_t>(1, std::min<int64_t>(by_len, (int64_t)per * est_nwaves));
+  return (uint32_t)std::max<int64_t>(1, std::min<int64_t>(by_len, (int64_t)est_nwaves));
 }
 
 static EngineCfg engine_cfg(int64_t n) {
@@ -176,9 +174,6 @@ static EngineCfg engine_cfg(int64_t n) {
   c.est_nwaves = c.est_grid * WAVES_PER_WG;
   c.est_nseg = est_segments(M, c.est_nwaves);
   c.est_ratioA = (uint32_t)std::max(1, std::min(VR_SEGS_PER_WAVE, env_int("VISREPS_ENGINE_SEGS_A", VR_SEGS_PER_WAVE)));
-  // the A side has at most VR_SEGS_PER_WAVE segments per wave in all (workspace bound)
-  while (c.est_ratioA > 1 && (uint64_t)c.est_nseg * c.est_ratioA > (uint64_t)VR_SEGS_PER_WAVE * c.est_nwaves)
-    --c.est_ratioA;
   c.est_nsegA = c.est_nseg * c.est_ratioA;
   c.tab = (c.est_lds ? need : 0) + (c.est_mode == 1 ? (size_t)c.est_rows * row : 0);
   return c;
@@ -212,8 +207,8 @@ struct EngineWs {
   uint32_t* viol;       // [EST_MAX_PASSES] EST: pass flagged for the exact re-run;
                         // [EST_MAX_PASSES]: an exact-form pass broke the tail invariants
   uint32_t* segposA;    // [nsegmax + 1] EST segment starts of the A plan (k_seg_table)
-  uint32_t* segposB;    // [units][nsegmax + 1] ... of each B plan
-  size_t segstride;     // nsegmax + 1
+  uint32_t* segposB;    // [units][nw + 1] ... of each B plan
+  size_t segstride;     // nw + 1
   uint32_t* queue;      // [QSLOTS] EST work-queue counters of one pass's launches
 };
 constexpr int QSLOTS = 256;
@@ -224,7 +219,7 @@ constexpr int EST_MAX_PASSES = 512;  // passes between two checks of the EST fla
 static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t* bytes, int64_t units = 1) {
   const int64_t M = pairs_of(n);
   const size_t nch = plan_nchunks(M);
-  // segment partials: up to VR_SEGS_PER_WAVE per wave (EST A side; B side with VISREPS_ENGINE_SEGS_B)
+  // A-side segment partials: up to VR_SEGS_PER_WAVE per wave (EST); B-side: one per wave
   const size_t nsegmax = (size_t)nwaves * VR_SEGS_PER_WAVE;
   const size_t nsb = scan_blocks((uint32_t)nsegmax);
   Carver c(base);
@@ -243,11 +238,11 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
   e.segA_part = c.take<uint64_t>(nsegmax * LANES * PA_N);
   e.segA_pre = c.take<uint32_t>(nsegmax * LANES);
   units = std::max<int64_t>(units, 1);
-  e.segstride = nsegmax + 1;
+  e.segstride = (size_t)nwaves + 1;
   e.segposA = c.take<uint32_t>(nsegmax + 1);
   e.segposB = c.take<uint32_t>(e.segstride * (size_t)units);
   e.queue = c.take<uint32_t>(QSLOTS);
-  e.useg = nsegmax * LANES;
+  e.useg = (size_t)nwaves * LANES;
   e.segB_tot = c.take<uint32_t>(e.useg * (size_t)units);
   e.segB_part = c.take<uint64_t>(e.useg * PB_N * (size_t)units);
   e.bsum = c.take<uint32_t>(nsb * LANES);
