@@ -174,6 +174,9 @@ static EngineCfg engine_cfg(int64_t n) {
   c.est_nwaves = c.est_grid * WAVES_PER_WG;
   c.est_nseg = est_segments(M, c.est_nwaves);
   c.est_ratioA = (uint32_t)std::max(1, std::min(VR_SEGS_PER_WAVE, env_int("VISREPS_ENGINE_SEGS_A", VR_SEGS_PER_WAVE)));
+  // A segments of >= 1024 positions: small triangles (phase 1's M ~ 5e5) keep one per B
+  // segment, where thousands of one-window segments would queue on a single counter
+  while (c.est_ratioA > 1 && (uint64_t)c.est_nseg * c.est_ratioA * 1024u > (uint64_t)M) --c.est_ratioA;
   c.est_nsegA = c.est_nseg * c.est_ratioA;
   c.tab = (c.est_lds ? need : 0) + (c.est_mode == 1 ? (size_t)c.est_rows * row : 0);
   return c;
