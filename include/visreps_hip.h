@@ -195,8 +195,11 @@ int vr_engine_join4(const void* posmap4, int64_t n_a, const void* plan_b, int64_
                     void* stream);
 /* vr_bootstrap_spearman_multi with every unit's A positions already joined (posA[j], M u32,
  * from vr_engine_join4 against this call's A plan): the EST passes read them and skip the
- * per-unit joins; an exact-form fallback rewrites posA[j] with the same values. Workspace
- * as vr_bootstrap_spearman_multi. */
+ * per-unit joins. posA is in/out: an exact-form pass (a flagged EST pass re-run, or
+ * VISREPS_ENGINE_EST=0) rewrites posA[j] in place, with the same values, beside its A chunks.
+ * Workspace vr_bootstrap_multi_joined_workspace(n, n_b): 4 B per pair and unit less than
+ * vr_bootstrap_multi_workspace (no posA arrays carved for units after the first). */
+size_t vr_bootstrap_multi_joined_workspace(int64_t n, int64_t n_b);
 int vr_bootstrap_spearman_multi_joined(const void* plan_a, const void* const* planBs, int64_t n_b, int64_t n,
                                        const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
                                        double* scores, int64_t ld_scores, uint32_t* const* posA, void* ws,
@@ -214,6 +217,10 @@ int64_t vr_engine_est_reruns(void);
 /* Of those re-runs, the passes only the tail invariants flagged: the A walk's window checks
  * passed, so the B side recovered a wrong rank (0 unless a bug or a fault injection). */
 int64_t vr_engine_est_tail_flags(void);
+/* Test hook, not for product use: from the next engine call on, after the A walk of EST
+ * pass `pass` one TB row's lanes 1..63 are corrupted (a B-side error the A walk cannot
+ * see), so the tail invariants and the exact re-run can be tested. -1 (the default) = off. */
+int vr_test_engine_inject(int64_t pass);
 /* Engine calls whose first pass's A counts (a count pre-pass before any EST pass) already
  * put some subset's ranks outside the EST 3 window, so the whole call ran in the exact form
  * without spending a flagged EST pass (VISREPS_ENGINE_EST_PREDICT=0 disables the check). */
@@ -250,6 +257,16 @@ int vr_bootstrap_spearman_f32(const float* A, const float* B, int64_t n, int64_t
 size_t vr_kendall_triu_workspace(int64_t n);
 int vr_kendall_triu_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out,
                         void* ws, size_t ws_bytes, void* stream);
+
+/* Kendall tau-a of two plain fp64 vectors of length m: replaces `_kendall_tau_a(x, y)`
+ * itself (visreps/analysis/rsa.py:22-40; imported by the reference's
+ * tests/test_rsa_bootstrap.py:46). Every unordered pair compared in fp64, exact integer
+ * discordant / tie counts, then the same tau-b -> tau-a conversion as vr_kendall_triu_f32.
+ * x, y, out [dev]; out = NaN for m < 2, a NaN element or a constant vector. m <= 2^22
+ * (O(m^2) pair work; RDM triangles go through vr_kendall_triu_f32). */
+size_t vr_kendall_vec_workspace(int64_t m);
+int vr_kendall_tau_a_f64(const double* x, const double* y, int64_t m, double* out, void* ws,
+                         size_t ws_bytes, void* stream);
 
 /* Bootstrapped Kendall RSA on two rank plans: the bootstrap loop of evals.py:355-373 /
  * rsa.py:233-261 with compare_method="kendall". Arguments as
@@ -354,6 +371,23 @@ size_t vr_rdm_sharded_workspace(int64_t n, int64_t d, int world);
 int vr_rdm_pearson_sharded(const float* X_local, int64_t rows_local, int64_t n, int64_t d, int64_t ldx, float* rdm,
                            int64_t ldr, float correction, void* comm, int rank, int world, void* ws, size_t ws_bytes,
                            void* stream);
+
+/* The collective behind the sharded entry points, as a table: all_gather(send, recv, bytes,
+ * user, stream) must leave rank r's `bytes` of send at recv + r * bytes on every rank, ordered
+ * on `stream`, and return 0 (non-zero fails the call with VR_EHIP). vr_comm_rccl fills the table
+ * with RCCL's ncclAllGather over `nccl_comm` (what vr_rdm_pearson_sharded uses); a caller with
+ * another transport (MPI, a host loopback in tests) fills it itself. */
+typedef int (*vr_allgather_fn)(const void* send, void* recv, size_t bytes, void* user, void* stream);
+typedef struct vr_comm {
+  int world;
+  int rank;
+  vr_allgather_fn all_gather;
+  void* user;
+} vr_comm;
+int vr_comm_rccl(vr_comm* out, void* nccl_comm, int world, int rank);
+int vr_rdm_pearson_sharded_comm(const float* X_local, int64_t rows_local, int64_t n, int64_t d, int64_t ldx,
+                                float* rdm, int64_t ldr, float correction, const vr_comm* comm, void* ws,
+                                size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------
  * Image preprocessing: the eval loaders' get_transform (visreps/dataloaders/obj_cls.py:

@@ -376,3 +376,41 @@ def test_engine_byte_models(monkeypatch):
     assert per == M * (16 * (136 + 14 * 136) + 14 * 12)
     assert P.engine_call_bytes(n, 1001, 14, joined=True) == M * 16 * (136 + 14 * 136)
     assert P.shared_join_bytes(n, 4, 14) == M * (16 + 16 + 14 * (4 + 16 + 16))
+
+
+@pytest.mark.parametrize("recv", [[[3, 0, 2], [1, 4, 0], [0, 0, 5]], [[2, 2], [0, 3]]])
+def test_list_all_to_all_views_match_all_to_all_single_layout(monkeypatch, recv):
+    # the RCCL branch of _all_to_all_rows (list all_to_all into views of `out`) has
+    # no multi-rank run on CPU. Emulate `world` ranks in one process: each rank's call records
+    # its send parts and receive views; a loopback then does the exchange (recv view j of rank
+    # i <- send part i of rank j). Every rank's `out` must equal all_to_all_single's layout:
+    # rank j's rows at offset sum(recv_rows[:j]), zero-row blocks included.
+    world = len(recv)
+    calls = []
+    monkeypatch.setattr(P, "_list_all_to_all", lambda out, pg: True)
+
+    def fake_all_to_all(outs, ins, group=None, async_op=False):  # noqa: ARG001
+        assert len(outs) == len(ins) == world
+        calls.append((outs, ins))
+        return P._Done()
+
+    monkeypatch.setattr(P.dist, "all_to_all", fake_all_to_all)
+    # recv[i][j] = rows rank i receives from rank j = rows rank j sends to rank i
+    sends = [[torch.full((recv[i][j], 3), float(100 * j + 10 * i), dtype=torch.float32)
+              + torch.arange(recv[i][j], dtype=torch.float32)[:, None] if recv[i][j] else None
+              for i in range(world)] for j in range(world)]
+    outs = []
+    for r in range(world):
+        _, out, _ = P._all_to_all_rows(sends[r], recv[r], (3,), torch.float32, "cpu", None)
+        outs.append(out)
+    for i in range(world):  # the loopback exchange
+        for j in range(world):
+            views = calls[i][0]
+            part = calls[j][1][i]
+            assert views[j].shape == part.shape
+            views[j].copy_(part)
+    for i in range(world):
+        want = torch.cat([sends[j][i] if sends[j][i] is not None else torch.empty((0, 3))
+                          for j in range(world)], 0)
+        assert torch.equal(outs[i], want)
+        assert outs[i].shape[0] == sum(recv[i])

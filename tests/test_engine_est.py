@@ -243,9 +243,12 @@ def test_b_side_error_is_flagged_and_rerun(dev, monkeypatch, inject):
     idx = bootstrap_indices(42, n, int(0.9 * n), nb)
     pa, pb = R.RankPlan(a), R.RankPlan(b)
     clean = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
-    monkeypatch.setenv("VISREPS_ENGINE_INJECT", str(inject))
     r0, t0 = int(lib().vr_engine_est_reruns()), int(lib().vr_engine_est_tail_flags())
-    got = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    lib().vr_test_engine_inject(inject)  # test-only export (no environment switch in the library)
+    try:
+        got = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    finally:
+        lib().vr_test_engine_inject(-1)
     reruns = int(lib().vr_engine_est_reruns()) - r0
     assert reruns >= 1, "the injected B-side error must flag its pass"
     assert int(lib().vr_engine_est_tail_flags()) - t0 == 1, "flagged by the tail invariants (the A walk cannot see it)"

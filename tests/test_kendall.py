@@ -168,3 +168,60 @@ def test_kendall_configs1_size_vs_oracle(dev):
                   d_point=abs(float(scores[0]) - ref_point), d_draw999=abs(float(scores[1000]) - ref_late))
     assert _close(float(scores[0]), ref_point), (scores[0], ref_point)
     assert _close(float(scores[1000]), ref_late), (scores[1000], ref_late)
+
+
+# -------------------------------------------------------------------- _kendall_tau_a(x, y)
+# The reference's tests call `_kendall_tau_a` itself on short vectors
+# (/root/reference/tests/test_rsa_bootstrap.py:350-420, 1120-1175). These are their known
+# answers, run on the product's vr_kendall_tau_a_f64, plus scipy-pinned random cases.
+def test_vec_known_answers(dev):
+    x = np.array([1.0, 2.0, 3.0, 4.0, 5.0])
+    assert R._kendall_tau_a(x, x)[0] == pytest.approx(1.0, abs=1e-12)  # :353-357
+    assert R._kendall_tau_a(x, x[::-1].copy())[0] == pytest.approx(-1.0, abs=1e-12)  # :359-364
+    y = np.array([1.0, 3.0, 2.0, 5.0, 4.0])  # :366-372: no ties, tau-a == tau-b
+    assert R._kendall_tau_a(x, y)[0] == pytest.approx(O._kendall_tau_a(x, y)[0], abs=1e-15)
+    # :383-394: 3 elements, C = 1, D = 2 -> -1/3
+    assert R._kendall_tau_a(np.array([1.0, 2.0, 3.0]), np.array([3.0, 1.0, 2.0]))[0] == pytest.approx(
+        O._kendall_tau_a(np.array([1.0, 2.0, 3.0]), np.array([3.0, 1.0, 2.0]))[0], abs=1e-15)
+    assert math.isnan(R._kendall_tau_a(np.array([1.0]), np.array([1.0]))[0])  # :396-400
+    assert math.isnan(R._kendall_tau_a(np.ones(4), np.arange(4.0))[0])  # :415-420 all tied
+    assert math.isnan(R._kendall_tau_a(np.array([]), np.array([]))[0])
+    t, p = R._kendall_tau_a(x, y)
+    assert math.isnan(p)  # the reference returns (tau_a, nan)
+    with pytest.raises(ValueError):
+        R._kendall_tau_a(np.arange(3.0), np.arange(4.0))
+
+
+@pytest.mark.parametrize("m,levels,seed", [(2, None, 0), (5, 3, 1), (100, None, 2), (257, 5, 3),
+                                           (1000, None, 4), (1000, 7, 5), (4097, 40, 6), (20000, 300, 7)])
+def test_vec_matches_oracle(dev, m, levels, seed):
+    # ties in x, y and jointly (levels), ragged lengths across the 256-row / 4096-column
+    # tiles; bit-equal to scipy's tau-b + the reference's conversion (same counts, same order)
+    r = np.random.RandomState(seed)
+    x, y = r.randn(m), r.randn(m) + 0.3 * r.randn(m)
+    if levels:
+        x, y = np.floor(x * levels / 3), np.floor(y * levels / 3)
+    y = 0.5 * x + y
+    got = R._kendall_tau_a(x, y)[0]
+    ref = O._kendall_tau_a(x, y)[0]
+    assert _close(got, ref, 0.0) or abs(got - ref) <= 1e-15, (got, ref)
+
+
+def test_vec_nan_signed_zero_and_ints(dev):
+    x = np.array([0.0, -0.0, 1.0, 2.0])
+    y = np.array([1.0, 2.0, 2.0, 3.0])
+    assert R._kendall_tau_a(x, y)[0] == O._kendall_tau_a(x, y)[0]  # -0.0 ties +0.0
+    assert math.isnan(R._kendall_tau_a(np.array([1.0, np.nan, 3.0]), np.arange(3.0))[0])
+    xi, yi = np.array([3, 1, 2, 2, 5]), np.array([1, 1, 2, 3, 4])  # integer inputs
+    assert R._kendall_tau_a(xi, yi)[0] == O._kendall_tau_a(xi.astype(float), yi.astype(float))[0]
+    xt = torch.tensor([1.0, 2.0, 3.0, 0.5])  # torch tensors are accepted
+    assert R._kendall_tau_a(xt, xt * 2)[0] == 1.0
+
+
+def test_vec_on_rdm_triangles_equals_triu_path(dev):
+    # /root/reference/tests/test_rsa_bootstrap.py:1077-1099: compute_rdm_correlation(...,
+    # "Kendall") equals _kendall_tau_a on the upper-triangle vectors
+    a, b = _rdm(120, 11, levels=9), _rdm(120, 12)
+    iu = np.triu_indices(120, 1)
+    got = R._kendall_tau_a(a[iu], b[iu])[0]
+    assert got == R.compute_rdm_correlation(torch.from_numpy(a), torch.from_numpy(b), correlation="Kendall")

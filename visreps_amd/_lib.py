@@ -99,6 +99,7 @@ _PROTOTYPES = {
         [_vp, _vp, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _vp, _c_sz, _vp],
     ),
     "vr_bootstrap_multi_workspace": (_c_sz, [_c_i64, _c_i64]),
+    "vr_bootstrap_multi_joined_workspace": (_c_sz, [_c_i64, _c_i64]),
     "vr_bootstrap_spearman_multi": (
         ctypes.c_int,
         [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _c_sz, _vp],
@@ -112,6 +113,7 @@ _PROTOTYPES = {
     "vr_engine_join4": (ctypes.c_int, [_vp, _c_i64, _vp, _c_i64, _vp, _vp]),
     "vr_engine_est_reruns": (_c_i64, []),
     "vr_engine_est_tail_flags": (_c_i64, []),
+    "vr_test_engine_inject": (ctypes.c_int, [_c_i64]),
     "vr_engine_est_predicted": (_c_i64, []),
     "vr_ktimer_enable": (ctypes.c_int, [ctypes.c_int]),
     "vr_trace_mark": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp]),
@@ -127,6 +129,8 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp],
     ),
+    "vr_kendall_vec_workspace": (_c_sz, [_c_i64]),
+    "vr_kendall_tau_a_f64": (ctypes.c_int, [_vp, _vp, _c_i64, _vp, _vp, _c_sz, _vp]),
     "vr_bootstrap_kendall_workspace": (_c_sz, [_c_i64, _c_i64]),
     "vr_bootstrap_kendall_plans": (
         ctypes.c_int,
@@ -181,6 +185,11 @@ _PROTOTYPES = {
         [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _vp, ctypes.c_int, ctypes.c_int, _vp,
          _c_sz, _vp],
     ),
+    "vr_comm_rccl": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
+    "vr_rdm_pearson_sharded_comm": (
+        ctypes.c_int,
+        [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _c_i64, ctypes.c_float, _vp, _vp, _c_sz, _vp],
+    ),
     "vr_rdm_tiles_pack": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_i64, _vp, _vp]),
     "vr_rdm_tiles_unpack": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp]),
     "vr_transform_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_int]),
@@ -198,6 +207,14 @@ _PROTOTYPES = {
 }
 
 EXPORTED_SYMBOLS = tuple(_PROTOTYPES)
+
+# typedef int (*vr_allgather_fn)(const void* send, void* recv, size_t bytes, void* user, void* stream)
+VR_ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _vp, _c_sz, _vp, _vp)
+
+
+class VrComm(ctypes.Structure):
+    """struct vr_comm (include/visreps_hip.h): the collective table of the sharded entry points."""
+    _fields_ = [("world", ctypes.c_int), ("rank", ctypes.c_int), ("all_gather", VR_ALLGATHER_FN), ("user", _vp)]
 
 _lib = None
 _lock = threading.Lock()

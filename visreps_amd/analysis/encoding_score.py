@@ -147,6 +147,10 @@ def _eig(K: torch.Tensor):
 
 
 def _gram64(x: torch.Tensor, rows: bool) -> torch.Tensor:
+    if x.dtype == torch.float64:
+        # the kernel reads fp32 (exact products in fp64); a silent cast would drop the low bits
+        raise TypeError("gram64 / gram64_cols take fp32 (or narrower) input: cast float64 data "
+                        "explicitly, knowing the fp32 rounding")
     dev = _device(x)
     x = x.to(dev, torch.float32)
     if x.ndim != 2 or x.stride(1) != 1:
@@ -264,6 +268,14 @@ def _znorm_fit(X):
     return _znorm(X, mean, std), mean, std
 
 
+def _flatten_to_cpu(acts) -> Dict[str, torch.Tensor]:
+    """Flatten 4-D -> 2-D and return CPU float32 copies; the input dict is not mutated
+    (encoding_score.py:39-44). compute_encoding_score keeps activations on the device
+    (_flatten); this is the reference's host-side helper, kept for its callers."""
+    return {layer: (a.flatten(start_dim=1) if a.ndim > 2 else a).cpu().float()
+            for layer, a in acts.items()}
+
+
 def _flatten(acts, dev) -> Dict[str, torch.Tensor]:
     """Flatten 4-D -> 2-D float32 on the device; new tensors, inputs untouched
     (encoding_score.py:40-45)."""
@@ -272,10 +284,18 @@ def _flatten(acts, dev) -> Dict[str, torch.Tensor]:
 
 
 def _fit_and_score(X_fit: torch.Tensor, Y_fit: torch.Tensor, X_new: torch.Tensor,
-                   Y_new: torch.Tensor, alphas):
+                   Y_new: torch.Tensor, alphas, backend=None):  # noqa: ARG001
     """RidgeCV on (X_fit, Y_fit), predictions for X_new and their mean Pearson r against
     Y_new (encoding_score.py:47-62). One fp64 Gram of the stacked rows gives both kernel
-    blocks."""
+    blocks. `backend` (the reference's himalaya backend) is accepted and unused: the
+    arrays go to X_fit's HIP device. X_new / Y_new may be CPU tensors, as the reference
+    allows for X_te."""
+    X_fit = torch.as_tensor(X_fit)
+    dev = _device(X_fit)
+    X_fit = X_fit.to(dev)
+    Y_fit = torch.as_tensor(Y_fit).to(dev)
+    X_new = torch.as_tensor(X_new).to(dev, X_fit.dtype)
+    Y_new = torch.as_tensor(Y_new).to(dev)
     n_fit, p = X_fit.shape
     if p < n_fit:  # narrow layer: p x p Grams per fold (primal)
         pred, _ = ridge_cv_predict_primal(X_fit, Y_fit, X_new, alphas)

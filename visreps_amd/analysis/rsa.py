@@ -46,6 +46,7 @@ __all__ = [
     "percentile",
     "_rank",
     "_concept_average_exact",
+    "_kendall_tau_a",
 ]
 
 _VALID_RDM = {"pearson", "spearman"}
@@ -237,7 +238,8 @@ def bootstrap_spearman_multi(
     if total == 0 or nb == 0:
         return scores
     L = lib()
-    ws = workspace.get(dev, L.vr_bootstrap_multi_workspace(n, nb), "engine")
+    ws = workspace.get(dev, (L.vr_bootstrap_multi_workspace if joined is None
+                             else L.vr_bootstrap_multi_joined_workspace)(n, nb), "engine")
     ptrs = (ctypes.c_void_p * nb)(*[_ptr(pb.buf) for pb in plans_b])
     with torch.cuda.device(dev):
         if joined is None:
@@ -356,6 +358,34 @@ def percentile(scores: np.ndarray, q: float) -> float:
 # -----------------------------------------------------------------------------
 # RDM comparison
 # -----------------------------------------------------------------------------
+def _kendall_tau_a(x, y) -> tuple:
+    """Kendall tau-a of two 1-D arrays, returned as (tau_a, nan) (rsa.py:22-40).
+
+    The reference takes scipy's tau-b and rescales it by sqrt((n0 - t_x)(n0 - t_y)) / n0.
+    Here vr_kendall_tau_a_f64 compares every pair in fp64 with exact integer discordant and
+    tie counts, then applies the same fp64 conversion. The result is NaN for fewer than two
+    elements, for any NaN element and for a constant input. Arrays of unequal length raise
+    ValueError, as scipy.stats.kendalltau does."""
+    xa = np.asarray(x.detach().cpu() if isinstance(x, torch.Tensor) else x, dtype=np.float64).ravel()
+    ya = np.asarray(y.detach().cpu() if isinstance(y, torch.Tensor) else y, dtype=np.float64).ravel()
+    if xa.size != ya.size:
+        raise ValueError("All inputs to `kendalltau` must be of the same size, found x-size %d and y-size %d"
+                         % (xa.size, ya.size))
+    m = int(xa.size)
+    if m < 2:
+        return (float("nan"), float("nan"))
+    dev = _device_for()
+    xd = torch.from_numpy(np.ascontiguousarray(xa)).to(dev)
+    yd = torch.from_numpy(np.ascontiguousarray(ya)).to(dev)
+    out = torch.empty(1, dtype=torch.float64, device=dev)
+    L = lib()
+    ws = workspace.get(dev, L.vr_kendall_vec_workspace(m), "kendall_vec")
+    with torch.cuda.device(dev):
+        check(L.vr_kendall_tau_a_f64(_ptr(xd), _ptr(yd), m, _ptr(out), _ptr(ws), ws.numel(), stream_of(dev)),
+              "vr_kendall_tau_a_f64")
+    return (float(out.item()), float("nan"))
+
+
 def compute_rdm_correlation(
     rdm1: torch.Tensor, rdm2: torch.Tensor, *, correlation: str = "Kendall"
 ) -> float:

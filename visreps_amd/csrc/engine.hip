@@ -1951,10 +1951,13 @@ static int with_pass_tag(bool lds, bool full, bool narrow, Fn&& fn) {
 // full_first), 64 per pass. joins: nb pairs of M-element (posA_byB, chunkA_byB) arrays.
 // Passes run in the EST form; the few it flags (and every pass, with VISREPS_ENGINE_EST=0)
 // run in the exact chunk-base form, which needs the chunkA joins too.
-// Test hook (VISREPS_ENGINE_INJECT=p): after the A walk of EST pass p, add 1 to the TB
-// entries of lanes 1..63 of one pair row -- a B-side recovery error the A walk's checks
-// cannot see. The tail's invariants must flag the pass and the exact re-run must restore
-// every score (tests/test_engine_est.py).
+// Test hook (vr_test_engine_inject(p), a test-only export; -1 = off, the default): after
+// the A walk of EST pass p, add 1 to the TB entries of lanes 1..63 of one pair row -- a
+// B-side recovery error the A walk's checks cannot see. The tail's invariants must flag
+// the pass and the exact re-run must restore every score (tests/test_engine_est.py). No
+// environment variable is read: the product path cannot be switched into it by accident.
+static std::atomic<int64_t> g_test_inject{-1};
+
 __global__ void k_inject_tb(uint16_t* __restrict__ TB, uint32_t row, int stride, int lanes) {
   const int lane = threadIdx.x;
   if (lane >= 1 && lane < lanes) TB[(size_t)row * stride + lane] += 1u;
@@ -1966,7 +1969,7 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
                                  const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st) {
   const int64_t M = pairs_of(n);
   uint32_t* const xbad = E.viol + EST_MAX_PASSES;  // exact-form passes' invariant flag
-  const int64_t inject = env_int("VISREPS_ENGINE_INJECT", -1);
+  const int64_t inject = g_test_inject.load(std::memory_order_relaxed);
   const int64_t total = n_sets + (full_first ? 1 : 0);
   if (total == 0 || nb == 0) return VR_OK;
   if (M == 0) {  // no pairs: every score is NaN (scipy on empty input)
@@ -2195,9 +2198,10 @@ static int run_engine(const PlanView& A, const PlanView& B, int64_t n, const int
 }
 
 // Workspace of the multi-B engine: the engine scratch, then the joins of B 1..nb-1 (B 0
-// uses the engine's own join arrays).
+// uses the engine's own join arrays). prejoined (the caller passes every unit's A positions,
+// vr_bootstrap_spearman_multi_joined): only the second array of each later unit is carved.
 static size_t multi_layout(void* base, int64_t n, int64_t nb, int nwaves, EngineWs* E,
-                           std::vector<uint32_t*>* joins) {
+                           std::vector<uint32_t*>* joins, bool prejoined = false) {
   size_t eb = 0;
   const EngineWs e = engine_layout(base, n, LANES, nwaves, &eb, nb);
   const int64_t M = pairs_of(n);
@@ -2208,7 +2212,7 @@ static size_t multi_layout(void* base, int64_t n, int64_t nb, int nwaves, Engine
     (*joins)[1] = e.chunkA_byB;
   }
   for (int64_t j = 1; j < nb; ++j) {
-    uint32_t* p = c.take<uint32_t>((size_t)M);
+    uint32_t* p = prejoined ? nullptr : c.take<uint32_t>((size_t)M);
     uint32_t* q = c.take<uint32_t>((size_t)M);
     if (joins) {
       (*joins)[2 * j] = p;
@@ -2247,6 +2251,10 @@ extern "C" {
 int64_t vr_engine_est_reruns(void) { return g_est_reruns.load(); }
 int64_t vr_engine_est_tail_flags(void) { return g_est_tail_flags.load(); }
 int64_t vr_engine_est_predicted(void) { return g_est_predicted.load(); }
+int vr_test_engine_inject(int64_t pass) {
+  g_test_inject.store(pass < 0 ? -1 : pass);
+  return VR_OK;
+}
 #if VR_PROBE_WT
 // probe builds only: the wave start / end clocks (wall_clock64, 100 MHz) of the last k_rankB
 int vr_probe_wave_times(uint64_t* host) {
@@ -2318,6 +2326,12 @@ int vr_bootstrap_spearman_multi(const void* planA, const void* const* planBs, in
                           joins.data(), E, LANES, cfg, as_stream(stream));
 }
 
+size_t vr_bootstrap_multi_joined_workspace(int64_t n, int64_t n_b) {
+  n = n < 0 ? 0 : n;
+  n_b = n_b < 1 ? 1 : n_b;
+  return multi_layout(nullptr, n, n_b, engine_cfg(n).nwaves, nullptr, nullptr, true);
+}
+
 int vr_bootstrap_spearman_multi_joined(const void* planA, const void* const* planBs, int64_t n_b, int64_t n,
                                 const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
                                 double* scores, int64_t ld_scores, uint32_t* const* posA, void* ws,
@@ -2338,14 +2352,14 @@ int vr_bootstrap_spearman_multi_joined(const void* planA, const void* const* pla
     VR_REQUIRE(posA[j] != nullptr, "vr_bootstrap_spearman_multi_joined: posA[%lld] is null", (long long)j);
   EngineCfg cfg = engine_cfg(n);
   cfg.prejoined = true;
-  const size_t need = multi_layout(nullptr, n, n_b, cfg.nwaves, nullptr, nullptr);
+  const size_t need = multi_layout(nullptr, n, n_b, cfg.nwaves, nullptr, nullptr, true);
   if (ws_bytes < need || ws == nullptr) {
     set_error("vr_bootstrap_spearman_multi_joined: workspace %zu < %zu", ws_bytes, need);
     return VR_EWORKSPACE;
   }
   EngineWs E;
   std::vector<uint32_t*> joins;
-  multi_layout(ws, n, n_b, cfg.nwaves, &E, &joins);
+  multi_layout(ws, n, n_b, cfg.nwaves, &E, &joins, true);
   for (int64_t j = 0; j < n_b; ++j) joins[(size_t)(2 * j)] = posA[j];
   const PlanView A = plan_layout(const_cast<void*>(planA), n);
   std::vector<PlanView> Bs;

@@ -548,6 +548,97 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
   return VR_OK;
 }
 
+// ---------------------------------------------------------------------------------
+// Kendall tau-a of two plain vectors (rsa.py:22-40 `_kendall_tau_a(x, y)` itself, which the
+// reference's tests call on short arrays and on RDM triangles): every unordered pair (i, j)
+// compared directly in fp64, exact integer counts. A block holds KV_ROWS rows i in
+// registers and streams a KV_COLS-wide strip of j > i through LDS; counts go through a
+// wave reduction into one u64 atomic per field and block (integer adds: order-free).
+// ---------------------------------------------------------------------------------
+constexpr int KV_ROWS = 256;
+constexpr int KV_COLS = 4096;
+
+__device__ inline uint64_t wave_sum_u64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(KV_ROWS) void k_kendall_vec_pairs(const double* __restrict__ x,
+                                                               const double* __restrict__ y, int64_t m,
+                                                               uint64_t* __restrict__ tot) {
+  __shared__ double sx[KV_ROWS], sy[KV_ROWS];
+  const int64_t i = (int64_t)blockIdx.x * KV_ROWS + threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * KV_ROWS;  // the block's first row
+  const int64_t c0 = (int64_t)blockIdx.y * KV_COLS;
+  const int64_t c1 = c0 + KV_COLS < m ? c0 + KV_COLS : m;
+  if (c1 <= r0 + 1) return;  // the strip holds no j > i for any row of the block
+  const double xi = i < m ? x[i] : 0.0, yi = i < m ? y[i] : 0.0;
+  uint64_t dis = 0, xt = 0, yt = 0, nt = 0;
+  for (int64_t t0 = c0 > r0 ? c0 : r0; t0 < c1; t0 += KV_ROWS) {
+    __syncthreads();
+    const int64_t j = t0 + threadIdx.x;
+    sx[threadIdx.x] = j < c1 ? x[j] : 0.0;
+    sy[threadIdx.x] = j < c1 ? y[j] : 0.0;
+    __syncthreads();
+    const int cnt = (int)((c1 - t0) < KV_ROWS ? (c1 - t0) : KV_ROWS);
+    uint32_t d = 0, a = 0, b = 0, ab = 0;
+    if (i < m) {
+      // only j > i: the tile's entries from i + 1 - t0 on
+      for (int q = i + 1 - t0 > 0 ? (int)(i + 1 - t0) : 0; q < cnt; ++q) {
+        const double xj = sx[q], yj = sy[q];
+        const bool tx = xi == xj, ty = yi == yj;
+        const bool gx = xi > xj, gy = yi > yj;
+        d += (!tx && !ty && gx != gy) ? 1u : 0u;
+        a += tx ? 1u : 0u;
+        b += ty ? 1u : 0u;
+        ab += (tx && ty) ? 1u : 0u;
+      }
+    }
+    dis += d;
+    xt += a;
+    yt += b;
+    nt += ab;
+  }
+  dis = wave_sum_u64(dis);
+  xt = wave_sum_u64(xt);
+  yt = wave_sum_u64(yt);
+  nt = wave_sum_u64(nt);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd((unsigned long long*)&tot[KF_DIS], (unsigned long long)dis);
+    atomicAdd((unsigned long long*)&tot[KF_XTIE], (unsigned long long)xt);
+    atomicAdd((unsigned long long*)&tot[KF_YTIE], (unsigned long long)yt);
+    atomicAdd((unsigned long long*)&tot[KF_NTIE], (unsigned long long)nt);
+  }
+}
+
+__global__ void k_kendall_vec_init(const double* __restrict__ x, const double* __restrict__ y, int64_t m,
+                                   uint64_t* __restrict__ tot, uint32_t* __restrict__ nan_flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < KF_N) tot[i] = i == KF_INCL ? (uint64_t)m : 0ull;
+  if (i < m && (x[i] != x[i] || y[i] != y[i])) atomicOr(nan_flag, 1u);  // nan_policy='propagate'
+}
+
+__global__ void k_kendall_vec_final(const uint64_t* __restrict__ tot, const uint32_t* __restrict__ nan_flag,
+                                    double* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  if (*nan_flag) {
+    out[0] = __builtin_nan("");
+    return;
+  }
+  // k_kfinal's fp64 order for one set (cap 1)
+  const uint64_t t = tot[KF_INCL] * (tot[KF_INCL] - 1) / 2;
+  const uint64_t dis = tot[KF_DIS], xt = tot[KF_XTIE], yt = tot[KF_YTIE], nt = tot[KF_NTIE];
+  double r = __builtin_nan("");
+  if (xt != t && yt != t) {
+    const int64_t cmd = (int64_t)(t - xt - yt + nt) - 2 * (int64_t)dis;
+    double taub = (double)cmd / sqrt((double)(t - xt)) / sqrt((double)(t - yt));
+    taub = fmin(1.0, fmax(-1.0, taub));
+    const double denom = sqrt((double)(t - xt) * (double)(t - yt));
+    r = denom == 0.0 ? __builtin_nan("") : taub * denom / (double)t;
+  }
+  out[0] = r;
+}
+
 static size_t k_oneshot_bytes(int64_t n, int64_t cap, int nwaves, void* base, PlanView* A, PlanView* B,
                               PlanBuildWs* PW, KendallWs* W) {
   Carver c(base);
@@ -626,6 +717,39 @@ int vr_kendall_triu_f32(const float* A, const float* B, int64_t n, int64_t ld, d
   VR_TRY(build_plan(A, n, ld, PA, PW, st));
   VR_TRY(build_plan(B, n, ld, PB, PW, st));
   return run_kendall(PA, PB, n, nullptr, 0, 0, 1, out, W, 1, cfg, st);
+}
+
+size_t vr_kendall_vec_workspace(int64_t m) {
+  (void)m;
+  return 256;  // KF_N u64 totals + the NaN flag
+}
+
+int vr_kendall_tau_a_f64(const double* x, const double* y, int64_t m, double* out, void* ws, size_t ws_bytes,
+                         void* stream) {
+  VR_REQUIRE(m >= 0 && m <= ((int64_t)1 << 22), "vr_kendall_tau_a_f64: m=%lld out of range (<= 2^22)",
+             (long long)m);
+  VR_REQUIRE(out != nullptr && (m == 0 || (x != nullptr && y != nullptr)), "vr_kendall_tau_a_f64: null pointer");
+  if (ws == nullptr || ws_bytes < vr_kendall_vec_workspace(m)) {
+    set_error("vr_kendall_tau_a_f64: workspace %zu < %zu", ws_bytes, vr_kendall_vec_workspace(m));
+    return VR_EWORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (m < 2) {  // rsa.py:25-26: fewer than two elements -> NaN
+    k_kfill_nan<<<1, 64, 0, st>>>(out, 1);
+    VR_CHECK_LAUNCH();
+    return VR_OK;
+  }
+  uint64_t* tot = static_cast<uint64_t*>(ws);
+  uint32_t* nan_flag = reinterpret_cast<uint32_t*>(tot + KF_N);
+  VR_CHECK_HIP(hipMemsetAsync(nan_flag, 0, sizeof(uint32_t), st));
+  k_kendall_vec_init<<<blocks_for(std::max<int64_t>(m, KF_N), 256), 256, 0, st>>>(x, y, m, tot, nan_flag);
+  VR_CHECK_LAUNCH();
+  const dim3 grid((unsigned)((m + KV_ROWS - 1) / KV_ROWS), (unsigned)((m + KV_COLS - 1) / KV_COLS));
+  k_kendall_vec_pairs<<<grid, KV_ROWS, 0, st>>>(x, y, m, tot);
+  VR_CHECK_LAUNCH();
+  k_kendall_vec_final<<<1, 64, 0, st>>>(tot, nan_flag, out);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
 }
 
 }  // extern "C"

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "common.h"
+#include "../../include/visreps_hip.h"
 
 extern "C" {
 int64_t vr_rdm_tile_count(int64_t n);
@@ -195,6 +196,23 @@ __global__ void k_unpack_stats(const float* __restrict__ in, int64_t rows, float
   }
 }
 
+// vr_comm's all_gather over RCCL: user = the ncclComm_t
+int rccl_all_gather(const void* send, void* recv, size_t bytes, void* user, void* stream) {
+  const int rc = rccl().all_gather(send, recv, bytes, NCCL_INT8, user, as_stream(stream));
+  if (rc != 0) set_error("ncclAllGather failed: %s", rccl().error_string(rc));
+  return rc;
+}
+
+#define VR_ALLGATHER(C, send, recv, bytes, stream)                                                  \
+  do {                                                                                              \
+    clear_error();                                                                                  \
+    const int rc_ = (C)->all_gather((send), (recv), (bytes), (C)->user, (stream));                  \
+    if (rc_ != 0) {                                                                                 \
+      if (vr_last_error()[0] == 0) set_error("vr_comm all_gather failed (rc %d, %s:%d)", rc_, __FILE__, __LINE__); \
+      return VR_EHIP;                                                                               \
+    }                                                                                               \
+  } while (0)
+
 }  // namespace
 }  // namespace vr
 
@@ -246,18 +264,39 @@ size_t vr_rdm_sharded_workspace(int64_t n, int64_t d, int world) {
   return b;
 }
 
+int vr_comm_rccl(vr_comm* out, void* nccl_comm, int world, int rank) {
+  VR_REQUIRE(out && nccl_comm && world >= 1 && rank >= 0 && rank < world, "vr_comm_rccl: bad arguments");
+  VR_REQUIRE(rccl().ok, "vr_comm_rccl: librccl.so.1 not found");
+  out->world = world;
+  out->rank = rank;
+  out->all_gather = rccl_all_gather;
+  out->user = nccl_comm;
+  return VR_OK;
+}
+
 int vr_rdm_pearson_sharded(const float* X_local, int64_t rows_local, int64_t n, int64_t d, int64_t ldx,
                            float* rdm, int64_t ldr, float correction, void* comm, int rank, int world, void* ws,
                            size_t ws_bytes, void* stream) {
   clear_error();
+  VR_REQUIRE(comm != nullptr, "vr_rdm_pearson_sharded: null comm");
+  vr_comm c;
+  VR_TRY(vr_comm_rccl(&c, comm, world, rank));
+  return vr_rdm_pearson_sharded_comm(X_local, rows_local, n, d, ldx, rdm, ldr, correction, &c, ws, ws_bytes, stream);
+}
+
+int vr_rdm_pearson_sharded_comm(const float* X_local, int64_t rows_local, int64_t n, int64_t d, int64_t ldx,
+                                float* rdm, int64_t ldr, float correction, const vr_comm* C, void* ws,
+                                size_t ws_bytes, void* stream) {
+  clear_error();
+  VR_REQUIRE(C != nullptr && C->all_gather != nullptr, "vr_rdm_pearson_sharded: null comm table");
+  const int world = C->world, rank = C->rank;
   VR_REQUIRE(n >= 1 && d >= 1 && ldx >= d && ldr >= n && world >= 1 && rank >= 0 && rank < world,
              "vr_rdm_pearson_sharded: bad shape n=%lld d=%lld world=%d rank=%d", (long long)n, (long long)d, world,
              rank);
   VR_REQUIRE(rows_local >= 0 && rows_local <= (n + world - 1) / world,
              "vr_rdm_pearson_sharded: %lld local rows (blocks hold at most ceil(n / world) = %lld)",
              (long long)rows_local, (long long)((n + world - 1) / world));
-  VR_REQUIRE(rdm && comm && ws && (rows_local == 0 || X_local), "vr_rdm_pearson_sharded: null pointer");
-  VR_REQUIRE(rccl().ok, "vr_rdm_pearson_sharded: librccl.so.1 not found");
+  VR_REQUIRE(rdm && ws && (rows_local == 0 || X_local), "vr_rdm_pearson_sharded: null pointer");
   const ShardLayout L = shard_layout(n, d, world);
   size_t need = 0;
   const ShardWs W = shard_ws(ws, L, n, world, &need);
@@ -268,7 +307,7 @@ int vr_rdm_pearson_sharded(const float* X_local, int64_t rows_local, int64_t n, 
   hipStream_t st = as_stream(stream);
   // 1. block sizes -> row offsets (host)
   VR_CHECK_HIP(hipMemcpyAsync(W.counts + rank, &rows_local, sizeof(int64_t), hipMemcpyHostToDevice, st));
-  VR_RCCL(rccl().all_gather(W.counts + rank, W.counts, sizeof(int64_t), NCCL_INT8, comm, st));
+  VR_ALLGATHER(C, W.counts + rank, W.counts, sizeof(int64_t), stream);
   std::vector<int64_t> counts((size_t)world);
   VR_CHECK_HIP(hipMemcpyAsync(counts.data(), W.counts, counts.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
   VR_CHECK_HIP(hipStreamSynchronize(st));
@@ -287,7 +326,7 @@ int vr_rdm_pearson_sharded(const float* X_local, int64_t rows_local, int64_t n, 
     k_pack_stats<<<(unsigned)((rows_local + 255) / 256), 256, 0, st>>>(W.mean, W.stdv, rows_local, lstats);
     VR_CHECK_LAUNCH();
   }
-  VR_RCCL(rccl().all_gather(W.send, W.recv, W.block_bytes, NCCL_INT8, comm, st));
+  VR_ALLGATHER(C, W.send, W.recv, W.block_bytes, stream);
   int64_t off = 0;
   for (int r = 0; r < world; ++r) {
     const char* blk = W.recv + (size_t)r * W.block_bytes;
@@ -312,8 +351,7 @@ int vr_rdm_pearson_sharded(const float* X_local, int64_t rows_local, int64_t n, 
   if (world > 1) {
     const size_t tile_floats = 128 * 128;
     if (t1 > t0) VR_TRY(vr_rdm_tiles_pack(rdm, ldr, n, t0, t1, W.psend, stream));
-    VR_RCCL(rccl().all_gather(W.psend, W.precv, (size_t)std::max<int64_t>(L.maxt, 1) * tile_floats * sizeof(float),
-                              NCCL_INT8, comm, st));
+    VR_ALLGATHER(C, W.psend, W.precv, (size_t)std::max<int64_t>(L.maxt, 1) * tile_floats * sizeof(float), stream);
     for (int r = 0; r < world; ++r) {
       const int64_t a = L.cuts[(size_t)r], b = L.cuts[(size_t)r + 1];
       if (r == rank || b <= a) continue;

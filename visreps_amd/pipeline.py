@@ -401,6 +401,11 @@ def assign_grams(n: int, width: Dict, consumers: Dict, world: int, split_factor:
     return pieces, load
 
 
+def _list_all_to_all(out: torch.Tensor, pg) -> bool:
+    """RCCL takes the list form of all-to-all (device tensors, no concatenated copies)."""
+    return out.is_cuda and dist.get_backend(pg) == "nccl"
+
+
 def _all_to_all_rows(send_parts: List[Optional[torch.Tensor]], recv_rows: List[int], row_shape, dtype,
                      device, pg, async_op: bool = False):
     """all_to_all_single of row blocks: send_parts[j] (rows, ...) goes to rank j (None = 0
@@ -409,7 +414,7 @@ def _all_to_all_rows(send_parts: List[Optional[torch.Tensor]], recv_rows: List[i
     empty = torch.empty((0,) + tuple(row_shape), dtype=dtype, device=device)
     parts = [pt if pt is not None else empty for pt in send_parts]
     out = torch.empty((sum(recv_rows),) + tuple(row_shape), dtype=dtype, device=device)
-    if out.is_cuda and dist.get_backend(pg) == "nccl":
+    if _list_all_to_all(out, pg):
         # RCCL: the list form (grouped send/recv) sends each part from where it lies and
         # receives into views of `out`: when every rank owns an RDM (distributed_rdm, configs[2])
         # each rank's rows go to all world owners without world concatenated copies of them
@@ -947,19 +952,22 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
     if (group_fn is run_group and plan_fn is R.RankPlan and len(by_region) >= 2 and n_boot > 0
             and os.environ.get("VISREPS_SHARED_JOINS", "1") != "0"):
         dev = neural_rdms[mine[0][1]].device
-        need = 4.0 * (n * (n - 1) // 2) * (len(mine) + 4)
+        # the join arrays (4 B per pair and unit, + the 16-B record table) and the neural
+        # plans built here, which all stay alive until their region's call is done
+        built = sum(1 for r in by_region if ("n", r) not in plans)
+        need = 4.0 * (n * (n - 1) // 2) * (len(mine) + 4) + built * float(lib().vr_rank_plan_bytes(n))
         if dev.type == "cuda" and need <= 0.25 * torch.cuda.mem_get_info(dev)[0]:
             pns = {r: (plans[("n", r)] if ("n", r) in plans else plan_fn(neural_rdms[r])) for r in by_region}
             joined = shared_joins(pns, by_region, mplans, times)
     for r, pts in by_region.items():
-        pn = plans[("n", r)] if ("n", r) in plans else (pns[r] if joined is not None else plan_fn(neural_rdms[r]))
+        pn = plans[("n", r)] if ("n", r) in plans else (pns.pop(r) if joined is not None else plan_fn(neural_rdms[r]))
         if joined is not None:
             out = group_fn(pn, [mplans[p] for p in pts], idx, times, joined=[joined.pop((p, r)) for p in pts])
         else:
             out = group_fn(pn, [mplans[p] for p in pts], idx, times)
         for j, p in enumerate(pts):
             local[(p, r)] = np.asarray(torch.as_tensor(out[j]).cpu())
-        del pn
+        del pn  # the last reference to a plan built here: freed before the next region's call
     del mplans
     if world > 1:
         gathered: List[Dict] = [None] * world
