@@ -122,12 +122,13 @@ def split_mode(n: int, dims: dict) -> bool:
     return mode == "split" or all(float(n) * n * d >= 1e10 for d in dims.values())
 
 
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r4_pmc_engine.json")
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r5_pmc_engine_joined.json")
 
 
 def pmc_traffic(n: int, est: bool):
-    """HBM bytes of the engine from the committed rocprofv3 --pmc passes over one 14-unit
-    engine call on the bench's RDMs (scripts/gpu_pmc_engine.sh): FETCH_SIZE x 2 (the gfx950
+    """HBM bytes of the engine from the committed rocprofv3 --pmc passes over the bench's own
+    engine path on its RDMs (JOINED=1 scripts/gpu_pmc_engine.sh: shared joins + one joined
+    call per region, 56 units): FETCH_SIZE x 2 (the gfx950
     correction, MI355X_MICROARCH.md; calibrated for these 128-B row gathers in
     profiles/r2_fetch_calibration.json) + WRITE_SIZE. A PMC pass cannot share this timed
     run, so the figures come from that separate profile -- and only when it was taken on this
@@ -139,7 +140,8 @@ def pmc_traffic(n: int, est: bool):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("build_id") != build_id() or int(d.get("n", -1)) != n or bool(d.get("est", True)) != est:
+    if (d.get("build_id") != build_id() or int(d.get("n", -1)) != n or bool(d.get("est", True)) != est
+            or not d.get("joined", False)):
         return None
     return d
 
@@ -150,7 +152,8 @@ def kernel_table(kt: dict, steps: int, est: bool, tri: bool = False) -> dict:
     a_b, b_b, j_b = engine_pair_bytes(est, tri)
     bpp = {"k_rankB_est": engine_pair_bytes(True, tri)[1], "k_rankB_full": engine_pair_bytes(True, tri)[1],
            "k_rankB_exact": engine_pair_bytes(False)[1],
-           "k_rankA": 4 + 128, "k_countA": 4, "k_join": j_b}  # k_rankA: codes 4 + TB row write 128
+           "k_rankA": 4 + 128, "k_countA": 4, "k_join": j_b,  # k_rankA: codes 4 + TB row write 128
+           "k_join4": 1}  # k_join4's vr_ktimer units are its algorithmic bytes (codes 4 + 16-B record + 4 per region)
     out = {}
     for k, (ms, n, units) in kt.items():
         e = {"ms_per_step": round(ms / steps, 2), "launches_per_step": round(n / steps, 2),
@@ -322,6 +325,150 @@ def configs3_leg(dev, dims: dict, n_boot: int) -> dict:
             "note": "device-resident synthetic inputs, wall time incl. eigh and host orchestration; outside the timed steps"}
 
 
+def _free_device(dev):
+    from visreps_amd._lib import workspace
+
+    workspace.release()
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+
+
+def _latent_features(dev, n: int, d: int, seed: int, dtype, relu: bool, chunk: int = 8192, zseed: int = 0):
+    """Synthetic (n, d) features with shared latent structure (z W / 8 + 2 noise, as
+    tests/test_benchsize.py's cfg3 data), generated in row chunks to bound the fp32 temporaries.
+    Features made with the same zseed share the stimulus latents z (model vs neural)."""
+    z = torch.randn(n, 64, device=dev, generator=torch.Generator(device=dev).manual_seed(zseed))
+    g = torch.Generator(device=dev).manual_seed(seed)
+    w = torch.randn(64, d, device=dev, generator=g) / 8
+    x = torch.empty((n, d), dtype=dtype, device=dev)
+    for r0 in range(0, n, chunk):
+        r1 = min(n, r0 + chunk)
+        t = z[r0:r1] @ w
+        t += 2 * torch.randn(r1 - r0, d, device=dev, generator=g)
+        if relu:
+            t.relu_()
+        x[r0:r1] = t.to(dtype)
+        del t
+    return x
+
+
+def _rdm_timed(x, reps: int = 1):
+    """compute_rdm(x) after one warm call (workspace allocation, kernel load): the HIP-event
+    time of the whole call (prepass + Gram + epilogue) and the Gram kernels' own time (vr_ktimer
+    k_gram_wide + k_gram_tile), per call."""
+    from visreps_amd.analysis import rsa as R
+
+    rdm = R.compute_rdm(x)
+    del rdm
+    torch.cuda.synchronize()
+    ktimer_enable(True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        rdm = R.compute_rdm(x)
+    e1.record()
+    torch.cuda.synchronize()
+    wide_ms, wide_n, _ = ktimer_read("k_gram_wide")
+    tile_ms, tile_n, _ = ktimer_read("k_gram_tile")
+    ktimer_enable(False)
+    return rdm, e0.elapsed_time(e1) / reps, (wide_ms + tile_ms) / reps, (wide_n + tile_n) / reps
+
+
+def _gram_roof(n: int, d: int, call_ms: float, gram_ms: float) -> dict:
+    flops = float(n) * (n + 1) * d
+    split_peak = BF16_MFMA_PEAK_TF / 3
+    tf_call = flops / (call_ms / 1e3) / 1e12
+    tf_gram = flops / (gram_ms / 1e3) / 1e12 if gram_ms else 0.0
+    return {"bound": "mfma", "achieved": round(tf_call, 2), "peak": round(split_peak, 1), "unit": "TFLOP/s",
+            "frac": round(tf_call / split_peak, 4), "gram_kernels_tflops": round(tf_gram, 2),
+            "gram_kernels_frac": round(tf_gram / split_peak, 4),
+            "frac_of_bf16_dense_peak": round(tf_call / BF16_MFMA_PEAK_TF, 4),
+            "algorithmic_flops": "N(N+1)D per RDM (unique pairs i <= j, 2 FLOP per multiply-add)",
+            "peak_note": ("split ceiling = bf16 dense peak 2516.6 / 3: every k-step is 3 bf16 MFMA products "
+                          "(hi hi + hi lo + lo hi of the centred fp32 values, as the reference centres in fp32 "
+                          "before its matmul, rsa.py:76-90); frac_of_bf16_dense_peak = algorithmic FLOPs / the bf16 dense "
+                          "peak itself (MFMA busy = 3 x that)")}
+
+
+def configs4_leg(dev) -> dict:
+    """BASELINE configs[4]: bf16 features at N = 50,000 -> compute_rdm (rsa.py:59-93; the
+    bf16 entry point vr_rdm_pearson_bf16 widens on the fly, no fp32 copy of the features):
+      * ViT-B/16 block output (197 tokens x 768 = D 151,296, the pca_labels_vit dump's block
+        hook), 15.1 GB of bf16 features;
+      * CLIP ViT-L/14 encode_image embedding, D = 768.
+    Synthetic latent-structured bf16 features of those shapes (the forward passes are
+    covered by tests/test_benchsize.py::test_cfg5_*); HIP events around compute_rdm after one
+    warm call, outside the timed steps."""
+    n = 50000
+    out = {}
+    for name, d, reps in (("vit_b16_block", 151296, 1), ("clip_vit_l14", 768, 5)):
+        _free_device(dev)
+        x = _latent_features(dev, n, d, seed=d, dtype=torch.bfloat16, relu=False)
+        rdm, call_ms, gram_ms, launches = _rdm_timed(x, reps)
+        ok = bool(torch.all(torch.diagonal(rdm) == 0)) and bool(torch.isfinite(rdm[:64]).all())
+        del rdm, x
+        e = {"n": n, "d": d, "dtype": "bf16 features (rsa.py:76 widens to fp32; split-Gram kernels)",
+             "rdm_ms": round(call_ms, 2), "gram_ms": round(gram_ms, 2), "gram_launches": launches,
+             "sane": ok}
+        e["roofline"] = _gram_roof(n, d, call_ms, gram_ms)
+        out[name] = e
+    _free_device(dev)
+    out["note"] = ("one RDM per shape after a warm call; rdm_ms = HIP events around compute_rdm (row statistics "
+                   "+ split prepass + Gram + epilogue), gram_ms = the Gram kernels alone (vr_ktimer); outside "
+                   "the timed steps")
+    return out
+
+
+def configs2_leg(dev) -> dict:
+    """BASELINE configs[2] on one GPU (the N = 1 point of its scaling curve): the NSD
+    73k-stimulus full RDM -- 73,000 x 43,264 fp32 features (AlexNet conv5 width) -> split-Gram
+    compute_rdm (rsa.py:59-93), a 73,000 x 2,000-voxel neural RDM, and the full-triangle
+    Spearman of the two (rsa.py:96-129 at 2.66e9 pairs, vr_spearman_full_f32: radix sort of
+    (key, triangle index) per RDM, midranks, exact integer dot). Synthetic features; HIP events
+    after one warm call; outside the timed steps."""
+    from visreps_amd.analysis import rsa as R
+
+    n, d, v = 73000, 43264, 2000
+    _free_device(dev)
+    x = _latent_features(dev, n, d, seed=7, dtype=torch.float32, relu=True)
+    rdm_m, call_ms, gram_ms, launches = _rdm_timed(x)
+    del x
+    _free_device(dev)
+    y = _latent_features(dev, n, v, seed=8, dtype=torch.float32, relu=False)
+    rdm_n = R.compute_rdm(y)
+    del y
+    _free_device(dev)
+    R.spearman_full(rdm_m[:4096, :4096], rdm_n[:4096, :4096])  # warm (kernels, small workspace)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    rho = R.spearman_full(rdm_m, rdm_n)
+    e1.record()
+    torch.cuda.synchronize()
+    sf_ms = e0.elapsed_time(e1)
+    M = n * (n - 1) // 2
+    # algorithmic bytes per pair of one RDM: key build (rdm read 4 + key/index write 8), LSD
+    # radix sort 4 passes x (read 8 + write 8), tie flags/scan/starts (~16), midranks of A
+    # scattered to triangle order (read 12, write 8) or B's dot (read 12 + 8-B gather) -> ~120 B
+    # per pair and RDM; two RDMs
+    bpp = 2 * 120
+    gbs = bpp * M / (sf_ms / 1e3) / 1e9
+    out = {"n": n, "d": d, "voxels": v, "rdm_ms": round(call_ms, 2), "gram_ms": round(gram_ms, 2),
+           "gram_launches": launches, "roofline_gram": _gram_roof(n, d, call_ms, gram_ms),
+           "spearman_full": {"ms": round(sf_ms, 2), "pairs": M, "rho": rho,
+                             "pairs_per_s": round(M / (sf_ms / 1e3), 1),
+                             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                                          "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                          "algorithmic_bytes_model": "~120 B per pair and RDM (keys 12, radix "
+                                          "sort 4 x 16, tie groups ~16, midrank scatter / dot ~28), 2 RDMs"}},
+           "one_gpu_s": round((call_ms + sf_ms) / 1e3, 3),
+           "note": ("model RDM (73k x 43,264 split Gram) + full-triangle Spearman vs a 73k x 2,000-voxel neural "
+                    "RDM on one GPU; the neural RDM's own build is not in one_gpu_s (it is the same kernel at "
+                    "D = 2,000); extraction of 73k images is not included")}
+    del rdm_m, rdm_n
+    _free_device(dev)
+    return out
+
+
 def _time(fn):
     t = time.perf_counter()
     out = fn()
@@ -400,7 +547,10 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-est-probe", action="store_true")
-    ap.add_argument("--no-extra-legs", action="store_true", help="skip the Kendall and configs[3] legs")
+    ap.add_argument("--no-extra-legs", action="store_true", help="skip the Kendall and configs[2]/[3]/[4] legs")
+    ap.add_argument("--no-exact-step", action="store_true", help="skip the exact-form step after the timed steps")
+    ap.add_argument("--legs", default="kendall,configs3,configs4,configs2",
+                    help="comma list of extra legs (outside the timed steps) to run at N = 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -537,6 +687,32 @@ def main():
         elapsed = float(mx[0])
     per_step = elapsed / args.steps
 
+    first_unit = res[(points[0], "V1")]
+    # the headline for RDMs whose subsets break the EST window (structured fMRI RDMs go exact
+    # up front): one more whole step with every engine pass in the exact chunk-base form
+    exact_step = None
+    if world == 1 and os.environ.get("VISREPS_ENGINE_EST") != "0" and not args.no_exact_step:
+        os.environ["VISREPS_ENGINE_EST"] = "0"
+        try:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            res_x, _, _ = step(StepTimes())
+            torch.cuda.synchronize()
+            exact_step = {"s": round(time.perf_counter() - t, 4),
+                          "max_abs_diff_vs_est_step": float(max(
+                              np.max(np.abs(np.asarray(res_x[u]["bootstrap_scores"] + [res_x[u]["score"]])
+                                            - np.asarray(res[u]["bootstrap_scores"] + [res[u]["score"]])))
+                              for u in res)),
+                          "diff_note": ("the step re-extracts, and the fc GEMMs are not bit-reproducible run to run "
+                                        "(4e-7); on the same RDMs the two forms are bit-equal "
+                                        "(tests/test_engine_est.py, test_benchsize.py)"),
+                          "note": ("one whole configs[1] step (extract -> phase 1 -> RDMs -> 56 units) with "
+                                   "VISREPS_ENGINE_EST=0: every engine pass in the exact chunk-base form, the "
+                                   "cost on RDMs the EST window cannot serve; after the timed steps, "
+                                   "wall clock with synchronize")}
+            del res_x
+        finally:
+            os.environ.pop("VISREPS_ENGINE_EST", None)
     if rank == 0:
         calls = max(1, times.engine_calls)
         unit_ms = times.engine_ms / calls                  # per unit (engine calls cover 14 units)
@@ -575,6 +751,18 @@ def main():
                                    "null: no PMC profile of this build/N/form (scripts/gpu_pmc_engine.sh)")}
         if rb_pmc:
             roof["traffic_over_algorithmic"] = round(rb_pmc["bytes_per_launch"] / rb["bytes_per_launch"], 3)
+        j4 = kernels.get("k_join4")
+        roof_join4 = None
+        if j4 and j4["launches_per_step"]:
+            j4_pmc = (pmc or {}).get("kernels", {}).get("k_join4")
+            roof_join4 = {"bound": "hbm", "achieved": j4["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(j4["gbs"] / HBM_PEAK_GBS, 4), "avg_launch_us": j4["avg_us"],
+                          "launches_per_step": j4["launches_per_step"],
+                          "algorithmic_bytes_per_launch": round(j4["bytes_per_launch"]),
+                          "algorithmic_bytes_model": ("per model pair: codes 4 (stream) + the 16-B position "
+                                                      "record of the 4 neural plans (random gather) + 4 B written "
+                                                      "per region"),
+                          "traffic": round(j4_pmc["bytes_per_launch"]) if j4_pmc else None}
         roof_engine = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(eng_gbs / HBM_PEAK_GBS, 4),
                        "scope": ("whole engine calls (vr_bootstrap_spearman_multi[_joined]: A walks, B walks, "
@@ -616,23 +804,42 @@ def main():
             t = time.perf_counter()
             est_structured = structured_est_probe(N, RankPlan(neural["V1"]), dev)
             log(f"structured-RDM EST probe took {time.perf_counter() - t:.1f}s: {est_structured}")
-        kendall = configs3 = None
-        if world == 1 and N <= 65535 and not args.no_extra_legs:
+        kendall = configs3 = configs4 = configs2 = None
+        legs = set() if args.no_extra_legs or world != 1 or N > 65535 else set(args.legs.split(","))
+        if "kendall" in legs:
             from visreps_amd.analysis.rsa import RankPlan
 
             t = time.perf_counter()
             kendall = kendall_leg(RankPlan(neural["V2"]), RankPlan(neural["V1"]), N, args.boot)
             kendall["note"] = kendall["note"].replace("bench's first point x V1", "the V2 x V1 neural RDMs")
             log(f"kendall leg took {time.perf_counter() - t:.1f}s: {kendall}")
+        if "configs3" in legs:
             t = time.perf_counter()
             configs3 = configs3_leg(dev, dims, args.boot)
             log(f"configs[3] leg took {time.perf_counter() - t:.1f}s: {configs3}")
+        # the big-memory legs run with the step's buffers and the library's scratch released;
+        # a failure is reported in the line, not fatal to it
+        del res
+        for name, fn in (("configs4", configs4_leg), ("configs2", configs2_leg)):
+            if name not in legs:
+                continue
+            t = time.perf_counter()
+            try:
+                r = fn(dev)
+            except Exception as e:  # noqa: BLE001
+                r = {"error": f"{type(e).__name__}: {e}"}
+                _free_device(dev)
+            log(f"{name} leg took {time.perf_counter() - t:.1f}s: {r}")
+            if name == "configs4":
+                configs4 = r
+            else:
+                configs2 = r
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             t = time.perf_counter()
             cpu = cpu_baseline(N, args.boot, dims, NSD_ROIS_4, model, images)
             log(f"cpu baseline sample took {time.perf_counter() - t:.1f}s")
-        first = res[(points[0], "V1")]
+        first = first_unit
         best = {r: b for r, (b, _) in sel.items()}
         line = {
             "metric": METRIC,
@@ -665,13 +872,17 @@ def main():
             "roofline": roof,
             "roofline_engine": roof_engine,
             "roofline_gram": roof_gram,
+            "roofline_join4": roof_join4,
             "kernels_per_step": {k: v for k, v in kernels.items() if v["launches_per_step"]},
             "est_reruns": est_reruns,
             "est_predicted_exact": est_predicted,
             "est_tail_flags": est_tail_flags,
             "est_structured": est_structured,
+            "exact_form_step_s": exact_step,
             "kendall_unit": kendall,
             "configs3": configs3,
+            "configs4": configs4,
+            "configs2_1gpu": configs2,
             "timed_region": ("bracketed by k_trace_mark_begin / k_trace_mark_end dispatches (vr_trace_mark): "
                              "scripts/check_timed_kernels.py lists the kernels between them in a rocprofv3 "
                              "trace (profiles/r3_timed_kernels.json)"),

@@ -15,7 +15,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-ENGINE = ("k_join", "k_masks", "k_countA", "k_c0", "k_rankA", "k_lscan", "k_add_base", "k_rankB", "k_tail")
+ENGINE = ("k_join", "k_posmap", "k_masks", "k_countA", "k_c0", "k_rankA", "k_lscan", "k_add_base", "k_rankB", "k_tail")
 
 
 def per_kernel(path):
@@ -41,9 +41,13 @@ def main(d, units, n=10000):
         kern[k] = {"launches": calls, "fetch_bytes_x2": fb, "write_bytes": wb,
                    "bytes_per_launch": (fb + wb) / max(calls, 1)}
         total += fb + wb
-    out = {"source": (f"rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE (separate passes) over one "
-                      f"{units}-unit vr_bootstrap_spearman_multi call on the bench RDMs "
-                      "(scripts/gpu_pmc_engine.sh); FETCH_SIZE x 2 (gfx950 correction)"),
+    joined = os.environ.get("JOINED", "0") == "1"
+    what = (f"the bench's engine path over {units} units (shared joins: vr_engine_posmap4 + vr_engine_join4 "
+            "per model plan, then one vr_bootstrap_spearman_multi_joined call per region)" if joined else
+            f"one {units}-unit vr_bootstrap_spearman_multi call")
+    out = {"source": (f"rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE (separate passes) over {what} on the bench "
+                      "RDMs (scripts/gpu_pmc_engine.sh); FETCH_SIZE x 2 (gfx950 correction)"),
+           "joined": joined,
            "units_per_call": units, "call_bytes": total, "bytes_per_unit": total / units,
            "kernels": kern, "n": n, "est": os.environ.get("VISREPS_ENGINE_EST") != "0",
            "build_id": build_id()}

@@ -2399,7 +2399,7 @@ int vr_engine_join4(const void* posmap4, int64_t n_a, const void* planB, int64_t
   const int64_t M = pairs_of(n);
   const PlanView B = plan_layout(const_cast<void*>(planB), n);
   hipStream_t st = as_stream(stream);
-  KtScope kt(KT_JOIN, (double)M, st);
+  KtScope kt(KT_JOIN4, (double)M * (4.0 + 16.0 + 4.0 * (double)n_a), st);  // codes + record gather + writes
   k_join4<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(B.codes, M, n, static_cast<const uint4*>(posmap4), (int)n_a,
                                                        o);
   VR_CHECK_LAUNCH();

@@ -98,7 +98,8 @@ enum KtKernel : int {
   KT_RANKB_FULL = 7,  // k_rankB, EST 4: the pass holding the full stimulus set (point estimates)
   KT_KWALK = 8,       // k_kwalk: one Kendall stream walk (inversion level or tie stream) of one pass
   KT_COV = 9,         // k_cov: fp64 MFMA covariance / Gram tiles (PCA covariance, ridge kernel matrix)
-  KT_N = 10
+  KT_JOIN4 = 10,      // k_join4: shared join of one B plan to up to 4 A plans (units = algorithmic bytes)
+  KT_N = 11
 };
 bool ktimer_on();
 struct KtScope {
