@@ -1062,7 +1062,11 @@ __device__ inline void gather_issue_t(const uint16_t* __restrict__ TB, uint32_t 
 #pragma unroll
   for (int q = 0; q < EBB; ++q) {
     const char* trow = reinterpret_cast<const char*>(TB) + (size_t)readlane_u32(pa, j0 + q) * (stride * 2);
+#if VR_XP & 16  // timing probe only (wrong scores): no TB row gathers, the row address stands in
+    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t[q]) : "v"(lane_bt), "s"((uint32_t)(uintptr_t)trow) : "memory");
+#else
     asm volatile("global_load_ushort %0, %1, %2" VR_TB_CACHE : "=v"(t[q]) : "v"(lane_bt), "s"(trow) : "memory");
+#endif
   }
 }
 
@@ -1430,7 +1434,12 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
                       asm volatile("" : "+v"(ma), "+v"(mb));
                       xn = bits_of(wn, ma, mb);
                     } else {
+  #if VR_XP & 8  // timing probe only (wrong scores): the mask lookups without the 64 x 64 transpose
+                      const uint32_t pn = wn + (uint32_t)lane;
+                      xn = (active && pn >= P0 && pn < P1) ? (m[cdn >> 16] & m[cdn & 0xffffu]) : 0ull;
+  #else
                       xn = window_bits(m, cdn, wn, P0, P1, lane, active);
+  #endif
                     }
                   }
                 } else {
