@@ -153,6 +153,7 @@ def kernel_table(kt: dict, steps: int, est: bool, tri: bool = False) -> dict:
     bpp = {"k_rankB_est": engine_pair_bytes(True, tri)[1], "k_rankB_full": engine_pair_bytes(True, tri)[1],
            "k_rankB_exact": engine_pair_bytes(False)[1],
            "k_rankA": 4 + 128, "k_countA": 4, "k_join": j_b,  # k_rankA: codes 4 + TB row write 128
+           "k_full_corr": 4,  # the EST 4 pass: posA stream 4 B per pair (flag words ~1 bit)
            "k_join4": 1}  # k_join4's vr_ktimer units are its algorithmic bytes (codes 4 + 16-B record + 4 per region)
     out = {}
     for k, (ms, n, units) in kt.items():

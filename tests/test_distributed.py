@@ -362,7 +362,8 @@ def test_engine_byte_models(monkeypatch):
     # pipeline's algorithmic byte models (bench.py's engine roofline): EST passes move 136 B
     # per pair and unit in the B walk (codes 4 + A position 4 + the 128-B TB row) and 136 B
     # per pair in the A side; the per-unit join 12 B (VISREPS_ENGINE_LO_JOIN=1: + 4 + 4);
-    # a joined call (SharedJoins) leaves its joins to shared_join_bytes
+    # a joined call (SharedJoins) leaves its joins to shared_join_bytes; the full-set pass's
+    # lane-0 shift sums (k_full_corr) read the A positions once more, 4 B per pair and unit
     import visreps_amd.pipeline as P
 
     monkeypatch.delenv("VISREPS_ENGINE_LO_JOIN", raising=False)
@@ -373,8 +374,8 @@ def test_engine_byte_models(monkeypatch):
     monkeypatch.delenv("VISREPS_ENGINE_LO_JOIN")
     n, M = 10000, 10000 * 9999 // 2
     per = P.engine_call_bytes(n, 1001, 14)
-    assert per == M * (16 * (136 + 14 * 136) + 14 * 12)
-    assert P.engine_call_bytes(n, 1001, 14, joined=True) == M * 16 * (136 + 14 * 136)
+    assert per == M * (16 * (136 + 14 * 136) + 14 * 12 + 14 * 4)
+    assert P.engine_call_bytes(n, 1001, 14, joined=True) == M * (16 * (136 + 14 * 136) + 14 * 4)
     assert P.shared_join_bytes(n, 4, 14) == M * (16 + 16 + 14 * (4 + 16 + 16))
 
 

@@ -213,7 +213,11 @@ struct EngineWs {
   uint32_t* segposB;    // [units][nw + 1] ... of each B plan
   size_t segstride;     // nw + 1
   uint32_t* queue;      // [QSLOTS] EST work-queue counters of one pass's launches
+  uint64_t* corr;       // [units][CORR_F][CORR_BLK] EST 4: lane 0's shift sums (k_full_corr blocks)
 };
+constexpr int CORR_F = 5;       // sum d, then sum d yB as four 32-bit limb sums
+constexpr int CORR_BLK = 2048;  // k_full_corr's fixed grid
+constexpr size_t CORR_N = (size_t)CORR_F * CORR_BLK;  // per unit
 constexpr int QSLOTS = 256;
 enum { QS_RANKA = 0, QS_RANKB = 1 };  // queue slots of an EST pass's launches
 
@@ -251,6 +255,7 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
   e.bsum = c.take<uint32_t>(nsb * LANES);
   e.fpart = c.take<uint64_t>((size_t)std::min<int64_t>(units, 64) * nsb * 8 * LANES);
   e.totA = c.take<uint32_t>(LANES);
+  e.corr = c.take<uint64_t>(CORR_N * (size_t)units);
   if (bytes) *bytes = c.bytes();
   return e;
 }
@@ -527,7 +532,19 @@ __device__ inline uint32_t est_lo_pc(const EstLo& e, uint32_t pc, int lane, bool
   return lo + (d0 & (0u - (uint32_t)(lane == 0)));
 }
 // EST 4: EST 3 with lane 0 holding the full set (pass 0 of a full_first call): its count
-// before A position pos is pos itself, so its low end is 2 pos + 1 - 2^15.
+// before A position pos is pos itself, so its low end is 2 pos + 1 - 2^15 (est_lo_t<4>, the
+// A side's checks). Lane 0 stores its doubled rank y shifted down by the gap between that low
+// end and the EST 3 one every other lane uses, d(pos) = 2 pos - (2 pos Ru >> 32) (y - d lies
+// in the EST 3 window exactly when y lies in lane 0's own), so the B walk recovers all 64
+// lanes with one wave-uniform window: the EST 3 kernel, no per-pair lane-0 select. Lane 0's
+// B-side sums then miss sum_p d(posA(p)) in sum yA and sum_p d(posA(p)) yB(p) in sum yA yB,
+// which k_full_corr adds up per unit and k_tail_top puts back (exact integers either way).
+// d is non-decreasing in pos, and y - d >= 1 is checked per group (k_rankA), so the shifted
+// value is a positive u32 like every other lane's rank.
+__device__ inline uint32_t est4_shift(uint32_t Ru, uint32_t pos) {
+  const uint32_t p2 = pos << 1;
+  return p2 - __umulhi(p2, Ru);
+}
 template <int EST>
 __device__ inline uint32_t est_lo_t(const EstLo& e, uint32_t pos, int lane) {
   if constexpr (EST == 5)
@@ -699,6 +716,12 @@ __device__ inline void store_rows_est(uint16_t* __restrict__ TB, uint32_t stride
   if (VR_EST_CHECK && (r0 >> 6) != ((r0 + cnt - 1u) >> 6))
     bad |= est_bad(y, est_lo_t<EST>(el, r0, lane)) || est_bad(y, est_lo_t<EST>(el, r0 + cnt - 1u, lane));
   uint16_t* row = TB + (size_t)r0 * stride + lane;
+  if constexpr (EST == 4) {  // lane 0 (the full set): y - d(r) per row, positive (est4_shift)
+    const uint32_t l0 = 0u - (uint32_t)(lane == 0);
+    if (VR_EST_CHECK) bad |= lane == 0 && (int32_t)(y - est4_shift(el.Ru, r0 + cnt - 1u)) < 1;
+    for (uint32_t i = 0; i < cnt; ++i, row += stride) tb_store((uint16_t)(y - (est4_shift(el.Ru, r0 + i) & l0)), row);
+    return;
+  }
   uint32_t i = 0;
   for (; i + 4 <= cnt; i += 4, row += 4 * (size_t)stride) {
     tb_store((uint16_t)y, row);
@@ -858,7 +881,12 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
             for (int j = 0; j < 63; ++j) {
               const uint32_t bit = (uint32_t)(x >> j) & 1u;
               const uint32_t v = t + bit;
-              if (active) tb_store((TBT)v, row + (size_t)j * stride);
+              if constexpr (EST == 4) {  // lane 0: shifted (est4_shift; singletons: y - d >= 2)
+                const uint32_t sub = est4_shift(el.Ru, w0 + (uint32_t)j) & (0u - (uint32_t)(lane == 0));
+                if (active) tb_store((TBT)(v - sub), row + (size_t)j * stride);
+              } else {
+                if (active) tb_store((TBT)v, row + (size_t)j * stride);
+              }
               t = v + bit;
             }
   #endif
@@ -989,6 +1017,9 @@ __global__ void k_add_base(const uint32_t* __restrict__ lpA, const uint32_t* __r
 #ifndef VR_RANKB_EST_MINW
 #define VR_RANKB_EST_MINW 8  // EST B walk: 8 waves per SIMD (two 1024-thread workgroups per CU)
 #endif
+#ifndef VR_XW_SLO
+#define VR_XW_SLO 0  // EST 3 prefetching walk: 1 = low ends in SALU from the address readlane (A/B; spills SGPRs)
+#endif
 #ifndef VR_RANKB_PIPE
 #define VR_RANKB_PIPE 0  // 1: gather batch h+1 in flight while batch h is consumed
 #endif
@@ -1062,6 +1093,26 @@ __device__ inline void gather_issue_t(const uint16_t* __restrict__ TB, uint32_t 
 #pragma unroll
   for (int q = 0; q < EBB; ++q) {
     const char* trow = reinterpret_cast<const char*>(TB) + (size_t)readlane_u32(pa, j0 + q) * (stride * 2);
+#if VR_XP & 16  // timing probe only (wrong scores): no TB row gathers, the row address stands in
+    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t[q]) : "v"(lane_bt), "s"((uint32_t)(uintptr_t)trow) : "memory");
+#else
+    asm volatile("global_load_ushort %0, %1, %2" VR_TB_CACHE : "=v"(t[q]) : "v"(lane_bt), "s"(trow) : "memory");
+#endif
+  }
+}
+
+// EST 3 prefetching walk: the same loads, and each pair's window low end L + (2 posA R >> 32)
+// computed in SALU from the row index the address already needed in an SGPR (one
+// v_readlane per pair instead of two: the walk is bound by its vector-instruction issue,
+// DESIGN.md §3.3)
+__device__ inline void gather_issue_tl(const uint16_t* __restrict__ TB, uint32_t stride, uint32_t pa,
+                                       uint32_t j0, uint32_t lane_bt, uint32_t t[EBB], uint32_t lo[EBB],
+                                       uint32_t Lu, uint32_t Ru) {
+#pragma unroll
+  for (int q = 0; q < EBB; ++q) {
+    const uint32_t r = readlane_u32(pa, j0 + q);
+    const char* trow = reinterpret_cast<const char*>(TB) + (size_t)r * (stride * 2);
+    lo[q] = Lu + __umulhi(r << 1, Ru);
 #if VR_XP & 16  // timing probe only (wrong scores): no TB row gathers, the row address stands in
     asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t[q]) : "v"(lane_bt), "s"((uint32_t)(uintptr_t)trow) : "memory");
 #else
@@ -1369,7 +1420,9 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       // EST 3 / 4 (small tie groups): the prefetching walk, which computes the window low
       // ends from the A positions (a join's streamed low ends, VISREPS_ENGINE_LO_JOIN=1, hold
       // the same values and are not read)
-      constexpr bool XW = VR_XWIN && (EST == 3 || EST == 4) && !BIGT;
+      // (masks in LDS only: with masks from L2 -- n > 10,176 -- the per-window walk below
+      // serves; the prefetching form's L2-mask path faulted when a round-5 test first ran it)
+      constexpr bool XW = VR_XWIN && EST == 3 && !BIGT && LDS;
       constexpr bool walked = XW;
       if constexpr (XW) {
         static_assert(EBB == 8, "prefetching batches are 8 pairs");
@@ -1414,16 +1467,25 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
             // the window's batch pipeline; proc(h, ya) consumes batch h's recovered A ranks
             // (issued inside each of its two instances: a load in flight across the branch into
             // them would be copied between registers before its wait)
+            // batch issue: the TB row gathers of pairs j0 .. j0 + 7 (and, VR_XW_SLO, their low ends)
+            auto issue = [&](uint32_t j0, uint32_t* t, uint32_t* lq) {
+  #if VR_XW_SLO
+              gather_issue_tl(TB16, stride, pa, j0, lane_bt, t, lq, el.Lu, el.Ru);
+  #else
+              (void)lq;
+              gather_issue_t(TB16, stride, pa, j0, lane_bt, t);
+  #endif
+            };
             auto pipeline = [&](auto&& proc) {
               uint64_t ma = 0, mb = 0;
-              uint32_t t[2][EBB];
+              uint32_t t[2][EBB], lq[2][EBB];
               xw_ld2(codes + wn, posA_byB + wn, voff_of(wn), cdn, pan);  // S(w+1)
-              gather_issue_t(TB16, stride, pa, 0, lane_bt, t[0]);
+              issue(0, t[0], lq[0]);
   #pragma unroll
               for (int h = 0; h < 64 / EBB; ++h) {
                 uint32_t(&cur)[EBB] = t[h & 1];
                 if (h + 1 < 64 / EBB) {
-                  gather_issue_t(TB16, stride, pa, (h + 1) * EBB, lane_bt, t[(h + 1) & 1]);
+                  issue((h + 1) * EBB, t[(h + 1) & 1], lq[(h + 1) & 1]);
                   gather_wait_n<EBB>(cur);
                   if (h == 0) asm volatile("" : "+v"(cdn), "+v"(pan));  // S(w+1): older than G[0]
                   if constexpr (!LDS) {
@@ -1445,24 +1507,23 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
                 } else {
                   gather_wait_n<0>(cur);
                 }
-                proc(h, cur);
+                proc(h, cur, lq[h & 1]);
               }
             };
+  #if VR_XW_SLO
+            // pair j's window low end (gather_issue_tl: scalar, from its row index)
+            auto recover = [&](uint32_t v, uint32_t lo) -> uint32_t { return est_recover(v, lo); };
+  #else
             // the window low ends of the window's A positions, lane j = pair j (3 VALU ops)
             const uint32_t la = el.Lu + __umulhi(pa << 1, el.Ru);
-            auto recover = [&](uint32_t v, uint32_t j) -> uint32_t {
-  #if VR_XP & 4  // timing probe only: one low end for the whole window (no per-pair readlane)
-              return est_recover(v, readlane_u32(la, 0));
-  #else
-              return est_recover(v, est_lo_b<EST>(el, pa, la, j, lane, v));
+            auto recover = [&](uint32_t v, uint32_t j) -> uint32_t { return est_recover(v, readlane_u32(la, j)); };
   #endif
-            };
             auto fast_proc = [&](uint64_t& a64, uint32_t& c1) {
-              return [&](int h, uint32_t* cur) {
+              return [&](int h, uint32_t* cur, const uint32_t* lo) {
   #pragma unroll
                 for (int q = 0; q < EBB; ++q) {
                   const uint32_t j = h * EBB + q;
-                  const uint32_t y = recover(cur[q], j);
+                  const uint32_t y = recover(cur[q], VR_XW_SLO ? lo[q] : j);
                   const uint32_t mk = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
                   const uint32_t yb = y & mk;
                   if (j < 63) {
@@ -1484,11 +1545,11 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
                 }
               };
             };
-            auto slow_proc = [&](int h, uint32_t* cur) {
+            auto slow_proc = [&](int h, uint32_t* cur, const uint32_t* lo) {
   #pragma unroll
               for (int q = 0; q < EBB; ++q) {
                 const uint32_t j = h * EBB + q;
-                const uint32_t y = recover(cur[q], j);
+                const uint32_t y = recover(cur[q], VR_XW_SLO ? lo[q] : j);
                 if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
                 S += ((x >> j) & 1ull) ? (uint64_t)y : 0ull;
               }
@@ -1717,9 +1778,126 @@ __global__ __launch_bounds__(1024) void k_tail_part(
 // recovery error (a wrong 2^16 window, a corrupted TB row) moves S and sets *viol, so the
 // pass is re-run in the exact form (EST) or the call fails (exact form) -- never a silent
 // wrong score.
+// EST 4 pass (est4_shift): lane 0's shifted-away sums of one unit, sum_p d(posA(p)) and
+// sum_p d(posA(p)) yB(p) over its B positions p, yB(p) = gs + ge + 1 for p's B tie group
+// [gs, ge) (the full set's doubled midrank). Each wave walks a contiguous range of 64-position
+// windows in order: lane j holds position w + j, the window's group-start bits F (two scalar
+// loads) give every lane its group bounds inside the window, and the group open at a window's
+// end is carried into the next (its members' d summed per lane until it ends). Only the
+// range's first and last groups need a search, wave-uniform (a few flag words back or
+// forward, else a binary search over the group starts). A fixed grid of CORR_BLK blocks,
+// each writing its block's sums (sum d, then sum d yB as four 32-bit limb sums) to
+// corr[field][block]; k_tail_top adds them up (exact integers: no order dependence).
+__device__ inline uint32_t group_index(const uint32_t* __restrict__ gstart, uint32_t G, uint32_t p) {
+  uint32_t lo = 0, hi = G;  // gstart[lo] <= p < gstart[hi] (gstart[G] = M)
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    if (sload(gstart + mid) <= p) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+// the last group start < w (w a multiple of 64, > 0): wave-uniform
+__device__ inline uint32_t start_before(const uint32_t* __restrict__ gflag, const uint32_t* __restrict__ gstart,
+                                        uint32_t G, uint32_t w) {
+  for (uint32_t k = w >> 5, i = 0; k > 0 && i < 8; ++i) {
+    const uint32_t v = sload(gflag + (--k));
+    if (v) return (k << 5) + 31u - (uint32_t)__clz(v);
+  }
+  return sload(gstart + group_index(gstart, G, w - 1u));
+}
+// the first group start >= e (a multiple of 64), or M: wave-uniform
+__device__ inline uint32_t start_from(const uint32_t* __restrict__ gflag, const uint32_t* __restrict__ gstart,
+                                      uint32_t G, int64_t M, uint32_t e) {
+  if ((int64_t)e >= M) return (uint32_t)M;
+  const uint32_t kend = (uint32_t)((M + 31) >> 5);
+  for (uint32_t k = e >> 5, i = 0; k < kend && i < 8; ++k, ++i) {
+    const uint32_t v = sload(gflag + k);
+    if (v) {
+      const uint32_t s = (k << 5) + (uint32_t)__ffs(v) - 1u;
+      return (int64_t)s >= M ? (uint32_t)M : s;  // (bits past the last position are padding)
+    }
+  }
+  const uint32_t gi = group_index(gstart, G, e);  // the group holding e (no start in 8 words)
+  return sload(gstart + gi + 1u);
+}
+constexpr int CORR_UNROLL = 4;  // windows per round, their loads issued together
+__global__ __launch_bounds__(256) void k_full_corr(const uint32_t* __restrict__ posA_byB,
+                                                   const uint32_t* __restrict__ gflag,
+                                                   const uint32_t* __restrict__ gstart, uint32_t G, int64_t M,
+                                                   uint32_t Ru, uint64_t* __restrict__ corr) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t nwin = (uint64_t)(M + 63) / 64u;
+  const uint64_t waves = (uint64_t)gridDim.x * 4u;
+  const uint64_t wid = wave_uniform(blockIdx.x * 4u + (uint32_t)wv);
+  // this wave's windows: a contiguous range, walked in order, so the group open at a window's
+  // end is carried into the next one (no search per window)
+  const uint64_t wb = nwin * wid / waves, we = nwin * (wid + 1) / waves;
+  const uint64_t below = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // positions <= lane
+  uint64_t c1 = 0;
+  u128 c2 = 0;
+  uint64_t dopen = 0;  // sum of d over this lane's positions in the group open at the window end
+  uint32_t gsc = 0;    // the last group start before the current window (wave-uniform)
+  if (wb < we && wb > 0 && !(sload(gflag + 2 * wb) & 1u)) gsc = start_before(gflag, gstart, G, (uint32_t)(wb * 64u));
+  for (uint64_t w0 = wb; w0 < we; w0 += CORR_UNROLL) {
+    uint32_t pa[CORR_UNROLL];
+    uint64_t Fs[CORR_UNROLL];
+#pragma unroll
+    for (int i = 0; i < CORR_UNROLL; ++i) {
+      const uint64_t win = w0 + i < we ? w0 + i : w0;
+      const int64_t p = (int64_t)win * 64 + lane;
+      pa[i] = p < M ? posA_byB[p] : 0u;
+      Fs[i] = ((uint64_t)sload(gflag + 2 * win + 1) << 32) | sload(gflag + 2 * win);
+    }
+#pragma unroll
+    for (int i = 0; i < CORR_UNROLL; ++i) {
+      if (w0 + i >= we) break;
+      const uint32_t w = (uint32_t)((w0 + i) * 64u);
+      const int64_t left = M - (int64_t)w;
+      uint64_t F = Fs[i];
+      if (left < 64) F |= ~0ull << left;  // the triangle's end starts a (padding) group
+      if (F) {  // the carried group (if any) ends at the window's first start
+        const uint32_t ge0 = w + (uint32_t)__builtin_ctzll(F);
+        c2 += (u128)dopen * ge0;
+        dopen = 0;
+      }
+      const bool valid = (int64_t)lane < left;
+      const uint32_t d = valid ? est4_shift(Ru, pa[i]) : 0u;
+      const uint64_t lo = F & below, hi = F & ~below;
+      const uint32_t gs = lo ? w + 63u - (uint32_t)__builtin_clzll(lo) : gsc;
+      c1 += d;
+      c2 += (u128)((uint64_t)d * (gs + 1u));  // the gs + 1 part of yB = gs + ge + 1
+      if (hi)
+        c2 += (u128)((uint64_t)d * (w + (uint32_t)__builtin_ctzll(hi)));  // ge inside the window
+      else
+        dopen += d;  // ge lies past the window: added when the group ends
+      if (F) gsc = w + 63u - (uint32_t)__builtin_clzll(F);
+    }
+  }
+  if (wb < we) {  // the group open at the range end ends at the next start (or M)
+    const uint64_t any = __ballot(dopen != 0);
+    if (any) c2 += (u128)dopen * start_from(gflag, gstart, G, M, (uint32_t)(we * 64u));
+  }
+  __shared__ uint64_t red[CORR_F][4];
+  const uint64_t v[CORR_F] = {c1, (uint64_t)(uint32_t)c2, (uint64_t)(uint32_t)(c2 >> 32),
+                              (uint64_t)(uint32_t)(c2 >> 64), (uint64_t)(c2 >> 96)};
+#pragma unroll
+  for (int f = 0; f < CORR_F; ++f) {
+    uint64_t s = v[f];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += shfl_xor64(s, m);
+    if (lane == 0) red[f][wv] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < CORR_F)
+    corr[(size_t)threadIdx.x * CORR_BLK + blockIdx.x] =
+        red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+}
+
+// corr (EST 4 pass, else null): per unit [CORR_F][CORR_BLK] k_full_corr block sums, added to lane 0's
 __global__ void k_tail_top(const uint64_t* __restrict__ fpart0, uint32_t nblk,
                            const uint32_t* __restrict__ totA, int a_nan, uint64_t nan_units, int nl,
-                           double* __restrict__ scores0, int64_t score_ld, uint32_t* __restrict__ viol) {
+                           double* __restrict__ scores0, int64_t score_ld, uint32_t* __restrict__ viol,
+                           const uint64_t* __restrict__ corr) {
   const int lane = threadIdx.x;
   const uint32_t u = blockIdx.x;
   const uint64_t* fpart = fpart0 + (size_t)u * nblk * FP_N * LANES;
@@ -1735,6 +1913,21 @@ __global__ void k_tail_top(const uint64_t* __restrict__ fpart0, uint32_t nblk,
     ab += (((u128)f[5 * LANES] << 64) | f[4 * LANES]) + 2 * (u128)P * f[7 * LANES];
     P += f[6 * LANES];
     Ssum += f[7 * LANES];
+  }
+  if (corr != nullptr) {  // lane 0: the full set's shifted ranks (est4_shift)
+    const uint64_t* c = corr + (size_t)u * CORR_N;
+    uint64_t s[CORR_F] = {0, 0, 0, 0, 0};
+    for (int b = lane; b < CORR_BLK; b += LANES)
+#pragma unroll
+      for (int f = 0; f < CORR_F; ++f) s[f] += c[(size_t)f * CORR_BLK + b];
+#pragma unroll
+    for (int f = 0; f < CORR_F; ++f)
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) s[f] += shfl_xor64(s[f], m);
+    if (lane == 0) {
+      Ssum += s[0];
+      ab += (u128)s[1] + ((u128)s[2] << 32) + ((u128)s[3] << 64) + ((u128)s[4] << 96);
+    }
   }
   const bool forced_nan = a_nan || ((nan_units >> u) & 1ull);
   const bool broken = lane < nl && !forced_nan &&
@@ -1883,7 +2076,7 @@ static int est_predict(const PlanView& A, int64_t n, const EngineWs& E, int lw, 
 // posA_byB (and chunkA_byB: the A chunks in the exact form, EST 3's window low ends)
 template <bool LDS, bool FULL, typename TBT, bool BTB, int EST>
 static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* chunkA_byB, int64_t n,
-                  const EngineWs& E, int lw, int64_t u, const EngineCfg& cfg, hipStream_t st) {
+                  const EngineWs& E, int lw, int64_t u, const EngineCfg& cfg, hipStream_t st, int kt_slot = -1) {
   static bool attr = false;
   if (!attr) {
     VR_TRY(allow_big_lds(k_rankB<LDS, FULL, TBT, BTB, EST>));
@@ -1902,7 +2095,7 @@ static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* c
     if (u >= QSLOTS - QS_RANKB) VR_CHECK_HIP(hipMemsetAsync(q, 0, sizeof(uint32_t), st));
   }
   {
-    KtScope kt(EST == 4 || EST == 6 ? KT_RANKB_FULL : EST ? KT_RANKB_EST : KT_RANKB_EXACT, (double)M, st);
+    KtScope kt(kt_slot >= 0 ? kt_slot : EST == 6 ? KT_RANKB_FULL : EST ? KT_RANKB_EST : KT_RANKB_EXACT, (double)M, st);
     k_rankB<LDS, FULL, TBT, BTB, EST><<<EST ? cfg.est_grid : cfg.grid, ENG_THREADS, EST ? cfg.tab : cfg.lds, st>>>(
         B.codes, B.gstart, B.chunk_g, B.gflag, nch, E.masks, n, static_cast<const TBT*>(E.TB), lw,
         posA_byB, chunkA_byB, E.baseA, E.segB_tot + us, E.segB_part + us * PB_N, nseg, E.ftab,
@@ -1917,7 +2110,7 @@ static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* c
 // sums break the invariants (k_tail_top).
 static int tail_units(const EngineWs& E, int64_t nb, uint32_t nseg, uint32_t ratioA, bool a_nan,
                       const std::vector<char>& nan_b, int nl, double* scores, int64_t score_ld, uint32_t* viol,
-                      hipStream_t st) {
+                      hipStream_t st, const uint64_t* corr = nullptr) {
   const uint32_t nsb = scan_blocks(nseg);
   for (int64_t u0 = 0; u0 < nb; u0 += 64) {  // 64 units per launch (the NaN bitmask)
     const int64_t cnt = std::min<int64_t>(64, nb - u0);
@@ -1929,7 +2122,8 @@ static int tail_units(const EngineWs& E, int64_t nb, uint32_t nseg, uint32_t rat
                                                             E.segB_tot + us, nseg, E.useg, E.fpart, ratioA);
     VR_CHECK_LAUNCH();
     k_tail_top<<<(unsigned)cnt, LANES, 0, st>>>(E.fpart, nsb, E.totA, a_nan ? 1 : 0, nan_units, nl,
-                                                scores + u0 * score_ld, score_ld, viol);
+                                                scores + u0 * score_ld, score_ld, viol,
+                                                corr ? corr + (size_t)u0 * CORR_N : nullptr);
     VR_CHECK_LAUNCH();
   }
   return VR_OK;
@@ -2135,16 +2329,26 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
                                                  (int)std::min<int64_t>(lw, sub));
                 VR_CHECK_LAUNCH();
               }
+              // EST 4: lane 0's ranks are stored shifted (est4_shift), so its B walks are the EST 3
+              // kernel (timed on their own slot) and k_full_corr supplies lane 0's shift sums
+              constexpr int EB = EM == 4 ? 3 : EM;
+              const int kts = EM == 4 ? KT_RANKB_FULL : -1;
               for (int64_t j = 0; j < nb; ++j) {
                 // EST 3/4: A positions and streamed low ends; EST 5/6: neither
                 const uint32_t* pj = EM >= 5 ? nullptr : joins[2 * j];
                 const uint32_t* lj = EM >= 3 && EM <= 4 && lo_join ? joins[2 * j + 1] : nullptr;
                 VR_TRY((h[(size_t)j + 1].max_group >= 65536u
-                            ? walk_b<Tg::lds, Tg::full, uint16_t, true, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)
-                            : walk_b<Tg::lds, Tg::full, uint16_t, false, EM>(Bs[j], pj, lj, n, E, lw, j, cfg, st)));
+                            ? walk_b<Tg::lds, Tg::full, uint16_t, true, EB>(Bs[j], pj, lj, n, E, lw, j, cfg, st, kts)
+                            : walk_b<Tg::lds, Tg::full, uint16_t, false, EB>(Bs[j], pj, lj, n, E, lw, j, cfg, st, kts)));
+                if constexpr (EM == 4) {
+                  KtScope kt(KT_FULL_CORR, (double)M, st);
+                  k_full_corr<<<CORR_BLK, 256, 0, st>>>(pj, Bs[j].gflag, Bs[j].gstart, h[(size_t)j + 1].G, M, e3.y,
+                                                    E.corr + (size_t)j * CORR_N);
+                  VR_CHECK_LAUNCH();
+                }
               }
               return tail_units(E, nb, cfg.est_nseg, cfg.est_ratioA, h[0].has_nan != 0, nan_b, nl, scores + set0,
-                                score_ld, viol, st);
+                                score_ld, viol, st, EM == 4 ? E.corr : nullptr);
             }
           };
           // EST 3 needs every lane to hold k stimuli: the pass holding the full set runs EST 4

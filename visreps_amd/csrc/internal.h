@@ -95,11 +95,12 @@ enum KtKernel : int {
   KT_GRAM_WIDE = 4,   // k_gram3p / k_gram3w (256^2 super-tiles)
   KT_GRAM_TILE = 5,   // k_gram3 / k_gram (128^2 tiles)
   KT_COUNTA = 6,      // k_countA
-  KT_RANKB_FULL = 7,  // k_rankB, EST 4: the pass holding the full stimulus set (point estimates)
+  KT_RANKB_FULL = 7,  // k_rankB on the pass holding the full stimulus set (EST 4 A side: EST 3 B walks)
   KT_KWALK = 8,       // k_kwalk: one Kendall stream walk (inversion level or tie stream) of one pass
   KT_COV = 9,         // k_cov: fp64 MFMA covariance / Gram tiles (PCA covariance, ridge kernel matrix)
   KT_JOIN4 = 10,      // k_join4: shared join of one B plan to up to 4 A plans (units = algorithmic bytes)
-  KT_N = 11
+  KT_FULL_CORR = 11,  // k_full_corr: lane 0's shift sums of an EST 4 pass, per unit (4 B / pair streamed)
+  KT_N = 12
 };
 bool ktimer_on();
 struct KtScope {

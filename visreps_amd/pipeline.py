@@ -705,7 +705,9 @@ def engine_call_bytes(n: int, subsets: int, units: int, joined: bool = False) ->
         j = 0
     M = n * (n - 1) // 2
     passes = -(-subsets // (63 if tri else 64))
-    return float(M) * (passes * (a + units * b) + units * j)
+    # + the full-set pass's lane-0 shift sums (k_full_corr: the A positions again, 4 B per pair
+    # and unit; csrc/engine.hip est4_shift)
+    return float(M) * (passes * (a + units * b) + units * j + (0 if tri else 4 * units))
 
 
 def run_unit(plan_m: R.RankPlan, plan_n: R.RankPlan, idx: Optional[np.ndarray],
