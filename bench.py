@@ -146,11 +146,16 @@ def pmc_traffic(n: int, est: bool):
     return d
 
 
-def kernel_table(kt: dict, steps: int, est: bool, tri: bool = False) -> dict:
+def kernel_table(kt: dict, steps: int, est: bool, tri: bool = False, regions: int = 4) -> dict:
     """Per hot kernel over the timed steps (vr_ktimer): ms and launches per step, average
-    launch time, and for the engine kernels the algorithmic bytes per launch and GB/s."""
+    launch time, and for the engine kernels the algorithmic bytes per launch and GB/s.
+    k_rankB_grid (and the full-set pass's launches, which are grid launches when the grid
+    runs) count pairs x regions: per (pair, region) the A position 4 + TB row 128 and the
+    B codes' 4 shared by the regions."""
     a_b, b_b, j_b = engine_pair_bytes(est, tri)
+    grid_b = (engine_pair_bytes(True, tri)[1] - 4) + 4.0 / regions
     bpp = {"k_rankB_est": engine_pair_bytes(True, tri)[1], "k_rankB_full": engine_pair_bytes(True, tri)[1],
+           "k_rankB_grid": grid_b,
            "k_rankB_exact": engine_pair_bytes(False)[1],
            "k_rankA": 4 + 128, "k_countA": 4, "k_join": j_b,  # k_rankA: codes 4 + TB row write 128
            "k_full_corr": 4,  # the EST 4 pass: posA stream 4 B per pair (flag words ~1 bit)
@@ -724,27 +729,34 @@ def main():
         pmc = pmc_traffic(N, est)
         tri = engine_tri(N, est)
         a_b, b_b, j_b = engine_pair_bytes(est, tri)
-        kernels = kernel_table(kt, args.steps, est, tri)
+        kernels = kernel_table(kt, args.steps, est, tri, regions=len(NSD_ROIS_4))
         # `roofline`: the dominant kernel, k_rankB (the B-side rank walk), priced per launch:
         # its algorithmic bytes (pairs walked x B/pair) / its HIP-event launch time
-        rb = kernels["k_rankB_est" if est else "k_rankB_exact"]
-        rb_pmc = (pmc or {}).get("kernels", {}).get("k_rankB")
+        grid = est and kernels.get("k_rankB_grid", {}).get("launches_per_step", 0) > 0
+        rb = kernels["k_rankB_grid" if grid else "k_rankB_est" if est else "k_rankB_exact"]
+        rb_pmc = (pmc or {}).get("kernels", {}).get("k_rankB_grid" if grid else "k_rankB")
         roof = {"bound": "hbm", "achieved": rb["gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(rb["gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": round(rb_pmc["bytes_per_launch"]) if rb_pmc else None,
-                "kernel": ("k_rankB, " + ("EST 5 form (triangle-order TB)" if tri else "EST 3 form" if est
+                "kernel": (("k_rankB_grid, EST 3 form: B-side rank walk of one model plan for all %d regions "
+                            "(one unit per region) over one pass of 64 bootstrap subsets (the full-set pass 0 and "
+                            "phase-1 launches are k_rankB_full in kernels_per_step)" % len(NSD_ROIS_4)) if grid else
+                           "k_rankB, " + ("EST 5 form (triangle-order TB)" if tri else "EST 3 form" if est
                                           else "exact chunk-base form")
                            + ": B-side rank walk of one unit over one pass of %d bootstrap subsets " % (63 if tri else 64)
                            + "(the full-set pass 0 and phase-1 launches are k_rankB_full in kernels_per_step)"),
                 "algorithmic_bytes_per_launch": round(rb["bytes_per_launch"]),
-                "algorithmic_bytes_model": (f"{b_b} B per pair: codes 4 (stream; the row is the pair's triangle "
+                "algorithmic_bytes_model": ((f"{rb['bytes_per_launch'] / max(rb['units_per_launch'], 1):.0f} B per "
+                                             "pair and region: per region A position 4 (stream) + 128 B TB row gather, "
+                                             "the B codes' 4 B shared by the regions") if grid else
+                                            f"{b_b} B per pair: codes 4 (stream; the row is the pair's triangle "
                                             "index) + 128 B TB row gather (lane 63: the coarse A position)" if tri else
                                             f"{b_b} B per pair: codes 4 + A position 4 (streams"
                                             + (" + window low end 4" if b_b > 136 else "; the window low end is "
                                                "computed from the A position") + ") + 128 B TB row gather" if est else
                                             f"{b_b} B per pair: codes, A position, A chunk 4 each + 128 B TB "
                                             "row gather (the 256-B chunk-base rows are L2-resident)"),
-                "pairs_per_launch": round(rb["units_per_launch"]),
+                "pairs_per_launch": round(rb["units_per_launch"]),  # (grid: pairs x regions)
                 "launches_per_step": rb["launches_per_step"], "avg_launch_us": rb["avg_us"],
                 "timing": "HIP events around every launch on its stream (vr_ktimer), timed steps only",
                 "traffic_source": ((f"{os.path.relpath(PMC_PROFILE, ROOT)}: {pmc['source']}; bytes per "

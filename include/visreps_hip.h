@@ -204,6 +204,20 @@ int vr_bootstrap_spearman_multi_joined(const void* plan_a, const void* const* pl
                                        const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
                                        double* scores, int64_t ld_scores, uint32_t* const* posA, void* ws,
                                        size_t ws_bytes, void* stream);
+/* The units of n_a <= 4 A plans (regions) x n_b B plans (model layers) on the same subsets,
+ * every unit pre-joined: posA[i * n_b + j] = B plan j's pairs in A plan i (vr_engine_join4);
+ * unit (j, i)'s scores at scores + (i * n_b + j) * ld_scores. Equal bit for bit to n_a
+ * vr_bootstrap_spearman_multi_joined calls (evals.py:323-373's region x layer loop, whose
+ * RandomState(42) gives every region the same index sets): the EST passes walk each B plan
+ * once for all regions (their window inclusion bits, group flags and B counts are the same),
+ * the regions' rank tables resident together; anything off that path (exact form, masks
+ * beyond LDS, giant tie groups, a flagged pass) runs the per-region calls. Workspace
+ * vr_bootstrap_grid_joined_workspace(n, n_a, n_b) = n_a x the per-region joined workspace. */
+size_t vr_bootstrap_grid_joined_workspace(int64_t n, int64_t n_a, int64_t n_b);
+int vr_bootstrap_spearman_grid_joined(const void* const* plan_as, int64_t n_a, const void* const* planBs,
+                                      int64_t n_b, int64_t n, const int32_t* idx, int64_t k, int64_t n_sets,
+                                      int full_first, double* scores, int64_t ld_scores, uint32_t* const* posA,
+                                      void* ws, size_t ws_bytes, void* stream);
 
 /* Passes of the bootstrap engines run in a one-gather-per-pair form (absolute ranks kept
  * modulo 2^16 and recovered against a count estimate). A pass whose ranks the estimate

@@ -1,9 +1,10 @@
 """Engine probe on the bench's own RDMs: the 14 CustomCNN points (random init, seed 0) of
 10k synthetic images against the V1 neural RDM, one vr_bootstrap_spearman_multi call
 (14 units x 1001 subsets), timed REPS times. ALT_LIB=path selects another library build.
-JOINED=1: the bench's own engine path instead -- the 4 NSD ROI neural plans, shared joins
-(vr_engine_posmap4 once, vr_engine_join4 per model plan) and one
-vr_bootstrap_spearman_multi_joined call per region (4 x 14 = 56 units)."""
+JOINED=1: the 4 NSD ROI neural plans, shared joins (vr_engine_posmap4 once, vr_engine_join4
+per model plan) and one vr_bootstrap_spearman_multi_joined call per region (4 x 14 = 56
+units); with GRID=1 one region-fused vr_bootstrap_spearman_grid_joined call instead (the
+bench's engine path)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
@@ -43,6 +44,9 @@ def joined_step():
     sj = R.SharedJoins(list(neurals.values()))
     js = [sj.join(pm) for pm in models]  # js[m][region]
     del sj
+    if os.environ.get("GRID", "0") == "1":  # the region-fused call (bootstrap_spearman_grid)
+        g = R.bootstrap_spearman_grid(list(neurals.values()), models, idx, js, full_first=True)
+        return g.reshape(-1, g.shape[-1])
     out = []
     for i, pn in enumerate(neurals.values()):
         out.append(R.bootstrap_spearman_multi(pn, models, idx, joined=[js[m][i] for m in range(len(models))]))

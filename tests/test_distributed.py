@@ -377,6 +377,9 @@ def test_engine_byte_models(monkeypatch):
     assert per == M * (16 * (136 + 14 * 136) + 14 * 12 + 14 * 4)
     assert P.engine_call_bytes(n, 1001, 14, joined=True) == M * (16 * (136 + 14 * 136) + 14 * 4)
     assert P.shared_join_bytes(n, 4, 14) == M * (16 + 16 + 14 * (4 + 16 + 16))
+    # the grid call: per pass each region's A side, per model plan one walk (codes once, per
+    # region the A position and the TB row), + the full-set pass's shift sums per unit
+    assert P.engine_grid_bytes(n, 1001, 4, 14) == M * (16 * (4 * 136 + 14 * (4 + 4 * 132)) + 4 * 4 * 14)
 
 
 @pytest.mark.parametrize("recv", [[[3, 0, 2], [1, 4, 0], [0, 0, 5]], [[2, 2], [0, 3]]])

@@ -276,3 +276,53 @@ def test_est_strong_stimulus_structure_equals_exact_form(dev):
         ref = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
     assert np.array_equal(est, ref)
     assert abs(est[0] - O.compute_rdm_correlation(a, b, "Spearman")) <= 1e-12
+
+
+@pytest.mark.parametrize("na", [2, 3, 4])
+def test_grid_equals_per_region_calls(dev, na):
+    # The region-fused grid call (one B walk per model plan for all regions, k_rankB_grid) is
+    # bit-equal to one joined multi call per region, in every pass form it takes: the full-set
+    # pass (lane 0 shifted, EST 4) and the EST 3 passes, with ties (ReLU features) and a
+    # quantised model RDM whose tie groups take the walk's slow windows
+    from visreps_amd._lib import ktimer_enable, ktimer_read
+
+    n = 1800
+    neurals = [R.RankPlan(_rdm(dev, n, 90 + 10 * i, 60 + i)) for i in range(na)]
+    q = _rdm(dev, n, 40, 77)
+    q = (q * 64).floor() / 64
+    models = [R.RankPlan(_rdm(dev, n, 70, 70, relu=True)), R.RankPlan(_rdm(dev, n, 150, 71)), R.RankPlan(q)]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 130)  # 131 subsets: 3 passes
+    sj = R.SharedJoins(neurals)
+    joins = [sj.join(pm) for pm in models]  # joins[m][a]
+    ktimer_enable(True)
+    got = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    grid_launches = ktimer_read("k_rankB_grid")[1]
+    ktimer_enable(False)
+    assert grid_launches > 0, "the fused walk did not run"
+    for a, pn in enumerate(neurals):
+        ref = R.bootstrap_spearman_multi(pn, models, idx, full_first=True,
+                                         joined=[joins[m][a] for m in range(len(models))]).cpu().numpy()
+        assert np.array_equal(got[a], ref)
+    with exact_engine():  # the exact form runs the per-region calls
+        ex = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    assert np.array_equal(ex, got)
+
+
+def test_grid_falls_back_on_a_structured_region(dev):
+    # A strongly structured neural RDM fails the up-front estimate check: the grid call then
+    # runs every region on its own (exact form where needed) and still equals the per-region calls
+    n = 1500
+    g = torch.Generator(device=dev).manual_seed(91)
+    u = torch.randn(n, device=dev, generator=g).abs() ** 3
+    s = u[:, None] + u[None, :] + 0.01 * torch.rand(n, n, device=dev, generator=g)
+    s = torch.triu(s, 1)
+    s = s + s.T
+    neurals = [R.RankPlan(s), R.RankPlan(_rdm(dev, n, 80, 92))]
+    models = [R.RankPlan(_rdm(dev, n, 60, 93)), R.RankPlan(_rdm(dev, n, 60, 94, relu=True))]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 100)
+    sj = R.SharedJoins(neurals)
+    joins = [sj.join(pm) for pm in models]
+    got = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    for a, pn in enumerate(neurals):
+        ref = R.bootstrap_spearman_multi(pn, models, idx, full_first=True).cpu().numpy()
+        assert np.array_equal(got[a], ref)

@@ -27,6 +27,8 @@ def rankb():
     if not os.path.exists(ENGINE_O):
         pytest.fail("visreps_amd/csrc/build/engine.o missing: run __graft_entry__.build() first")
     res = check_object(ENGINE_O, r"k_rankB")
+    # (k_rankB_grid issues plain compiler-managed loads: no asm gathers to guard)
+    res = {k: v for k, v in res.items() if "k_rankB_grid" not in k}
     assert len(res) >= 40, f"expected every k_rankB instantiation, found {len(res)}"
     return res
 

@@ -108,6 +108,11 @@ _PROTOTYPES = {
         ctypes.c_int,
         [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _vp, _c_sz, _vp],
     ),
+    "vr_bootstrap_grid_joined_workspace": (_c_sz, [_c_i64, _c_i64, _c_i64]),
+    "vr_bootstrap_spearman_grid_joined": (
+        ctypes.c_int,
+        [_vp, _c_i64, _vp, _c_i64, _c_i64, _vp, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _vp, _c_sz, _vp],
+    ),
     "vr_engine_posmap4_bytes": (_c_sz, [_c_i64]),
     "vr_engine_posmap4": (ctypes.c_int, [_vp, _c_i64, _c_i64, _vp, _vp]),
     "vr_engine_join4": (ctypes.c_int, [_vp, _c_i64, _vp, _c_i64, _vp, _vp]),
@@ -287,7 +292,7 @@ workspace = _WorkspacePool()
 KTIMER_KERNELS = {"k_rankB_est": 0, "k_rankB_exact": 1, "k_rankA": 2, "k_join": 3,
                   "k_gram_wide": 4, "k_gram_tile": 5, "k_countA": 6, "k_rankB_full": 7,
                   "k_kwalk": 8, "k_cov": 9, "k_join4": 10,
-                  "k_full_corr": 11}
+                  "k_full_corr": 11, "k_rankB_grid": 12}
 
 
 def ktimer_enable(on: bool = True) -> None:

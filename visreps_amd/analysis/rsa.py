@@ -41,6 +41,7 @@ __all__ = [
     "RankPlan",
     "bootstrap_spearman",
     "bootstrap_spearman_multi",
+    "bootstrap_spearman_grid",
     "bootstrap_kendall",
     "spearman_full",
     "percentile",
@@ -266,6 +267,58 @@ def bootstrap_spearman_multi(
                 ),
                 "vr_bootstrap_spearman_multi_joined",
             )
+    return scores
+
+
+def bootstrap_spearman_grid(
+    plans_a: Sequence[RankPlan],
+    plans_b: Sequence[RankPlan],
+    idx: Optional[np.ndarray | torch.Tensor],
+    joined: Sequence[Sequence[torch.Tensor]],
+    *,
+    full_first: bool = True,
+) -> torch.Tensor:
+    """Spearman of every plan in plans_b against every plan in plans_a (<= 4, the regions a
+    model layer is scored against) on the same subsets: (len(plans_a), len(plans_b), total)
+    float64 scores on the device, [i, j] equal bit for bit to
+    bootstrap_spearman_multi(plans_a[i], plans_b, idx, joined=...)[j]. joined[j][i]: B plan
+    j's pairs joined to A plan i (SharedJoins(plans_a).join(plans_b[j])). The EST passes walk
+    each B plan once for all A plans (vr_bootstrap_spearman_grid_joined)."""
+    plans_a, plans_b = list(plans_a), list(plans_b)
+    if not 1 <= len(plans_a) <= 4:
+        raise ValueError("bootstrap_spearman_grid takes 1 to 4 A plans")
+    pa0 = plans_a[0]
+    for p in plans_a + plans_b:
+        if p.n != pa0.n or p.device != pa0.device:
+            raise ValueError("rank plans must describe RDMs of the same size and device")
+    dev, n = pa0.device, pa0.n
+    idx_t = _idx_tensor(idx, dev)
+    n_sets, k = (int(idx_t.size(0)), int(idx_t.size(1))) if idx_t.numel() else (0, 0)
+    total = n_sets + (1 if full_first else 0)
+    na, nb = len(plans_a), len(plans_b)
+    scores = torch.empty((na, nb, total), dtype=torch.float64, device=dev)
+    if total == 0 or nb == 0:
+        return scores
+    M = n * (n - 1) // 2
+    joined = [list(js) for js in joined]
+    if len(joined) != nb or any(len(js) != na for js in joined) or any(
+            t.dtype != torch.int32 or t.numel() != M or t.device != dev or not t.is_contiguous()
+            for js in joined for t in js):
+        raise ValueError("joined[j][i]: one contiguous int32 tensor of M pairs per (B plan, A plan), on the plans' device")
+    L = lib()
+    ws = workspace.get(dev, L.vr_bootstrap_grid_joined_workspace(n, na, nb), "engine")
+    pa = (ctypes.c_void_p * na)(*[_ptr(p.buf) for p in plans_a])
+    pb = (ctypes.c_void_p * nb)(*[_ptr(p.buf) for p in plans_b])
+    jp = (ctypes.c_void_p * (na * nb))(*[_ptr(joined[j][i]) for i in range(na) for j in range(nb)])
+    with torch.cuda.device(dev):
+        check(
+            L.vr_bootstrap_spearman_grid_joined(
+                ctypes.cast(pa, ctypes.c_void_p), na, ctypes.cast(pb, ctypes.c_void_p), nb, n,
+                _ptr(idx_t) if idx_t.numel() else None, k, n_sets, int(full_first), _ptr(scores), total,
+                ctypes.cast(jp, ctypes.c_void_p), _ptr(ws), ws.numel(), stream_of(dev),
+            ),
+            "vr_bootstrap_spearman_grid_joined",
+        )
     return scores
 
 

@@ -1696,6 +1696,154 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
 }
 
 // ---------------------------------------------------------------------------------
+// Grid B walk: one B plan against R <= 4 A plans in one launch (the regions a model layer
+// is scored against, evals.py:323-373). Every region's call draws the same bootstrap index
+// sets (RandomState(42) is re-created per region, evals.py:356), so for one B plan and one
+// pass the regions' B walks share everything but the A ranks: the pair order, the window
+// inclusion bits x (mask lookups + 64 x 64 transpose), the group-start flags, the included
+// counts c1 and the B tie terms. Per window those are done once; per pair each region adds
+// its own TB row gather, window low end and sums. The regions' TB tables (one A walk each)
+// are resident together. Same exact integer sums as k_rankB EST 3 (the segment partials go
+// to each region's workspace, unit j), so the scores are bit-identical to the per-region
+// calls. Masks in LDS, tie groups < 2^16 (the caller checks).
+// ---------------------------------------------------------------------------------
+struct GridB {
+  const uint16_t* TB[4];     // each region's TB (EST: absolute doubled ranks mod 2^16)
+  const uint32_t* posA[4];   // B position -> A position, per region
+  uint32_t* seg_tot[4];      // unit (j, region) segment partials (k_tail_part's inputs)
+  uint64_t* seg_part[4];
+};
+#ifndef VR_GRID_NB
+#define VR_GRID_NB 4  // pairs per gather batch (x R regions loads in flight, two batches)
+#endif
+#ifndef VR_GRID_MINW
+#define VR_GRID_MINW 4  // waves per SIMD the grid walk is compiled for (4: 128 VGPRs)
+#endif
+template <int R>
+__global__ __launch_bounds__(ENG_THREADS, VR_GRID_MINW) void k_rankB_grid(
+    const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gflag, const uint64_t* __restrict__ gmask,
+    int64_t n, GridB g, uint32_t nseg, const uint2* __restrict__ ftab, const uint32_t* __restrict__ segpos,
+    uint32_t* __restrict__ queue) {
+  constexpr int NB = VR_GRID_NB;
+  static_assert(64 % NB == 0, "batch");
+  extern __shared__ uint64_t smask[];
+  const uint64_t* m = stage_masks<true>(gmask, n, smask);
+  const uint32_t Lu = wave_uniform(sload(&ftab->x)), Ru = wave_uniform(sload(&ftab->y));
+  const int lane = threadIdx.x & 63;
+  const uint32_t lane_off = (uint32_t)lane;
+  for (;;) {
+    const uint32_t sidx = next_segment(queue);
+    if (sidx >= nseg) break;
+    const uint32_t P0 = segpos[sidx], P1 = segpos[sidx + 1];
+    u128 acc[R];
+    uint64_t St[R], S[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0, St[r] = 0, S[r] = 0;
+    uint64_t tie = 0;
+    u128 tie_unused = 0;
+    uint32_t cw = 0, cgs = 0;
+    if (P0 < P1) {
+      auto close = [&](uint32_t ce) {
+        const uint32_t y = cgs + ce + 1u;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          acc[r] += (u128)S[r] * y;
+          St[r] += S[r];
+          S[r] = 0;
+        }
+        tie_add<false>(tie, tie_unused, ce - cgs);
+        cgs = ce;
+      };
+      for (uint32_t w0 = P0 & ~63u; w0 < P1; w0 += 64) {
+        const uint32_t pos = w0 + (uint32_t)lane;
+        const bool valid = pos >= P0 && pos < P1;
+        const uint32_t cd = valid ? codes[pos] : 0u;
+        uint32_t pa[R], la[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          pa[r] = valid ? g.posA[r][pos] : 0u;
+          la[r] = Lu + __umulhi(pa[r] << 1, Ru);
+        }
+        const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, true);
+        const uint64_t F =
+            restrict_flags(((uint64_t)sload(gflag + (w0 >> 5) + 1) << 32) | sload(gflag + (w0 >> 5)), w0, P0, P1);
+        // batch h's TB entries, t[r][q] = region r's row of pair h NB + q, lane's subset
+        auto issue = [&](int h, uint32_t (&t)[R][NB]) {
+#pragma unroll
+          for (int q = 0; q < NB; ++q)
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+              t[r][q] = __builtin_nontemporal_load(g.TB[r] + (size_t)readlane_u32(pa[r], h * NB + q) * LANES + lane_off);
+        };
+        uint32_t tb[2][R][NB];
+        if (F == ~0ull) {  // every position starts a group (k_rankB's per-window form explains)
+          close(cw);
+          uint64_t a64[R];
+#pragma unroll
+          for (int r = 0; r < R; ++r) a64[r] = 0;
+          uint32_t c1 = cw + 1u;
+          issue(0, tb[0]);
+#pragma unroll
+          for (int h = 0; h < 64 / NB; ++h) {
+            if (h + 1 < 64 / NB) issue(h + 1, tb[(h + 1) & 1]);
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+              const uint32_t j = h * NB + q;
+              const uint32_t mk = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
+#pragma unroll
+              for (int r = 0; r < R; ++r) {
+                const uint32_t yb = est_recover(tb[h & 1][r][q], readlane_u32(la[r], j)) & mk;
+                if (j < 63) {
+                  a64[r] += (uint64_t)yb * c1;
+                  St[r] += yb;
+                } else {
+                  S[r] = yb;
+                }
+              }
+              if (j < 63)
+                c1 -= mk;
+              else
+                cgs = c1 - 1u;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r] += (u128)a64[r] * 2u;
+        } else {
+          issue(0, tb[0]);
+#pragma unroll
+          for (int h = 0; h < 64 / NB; ++h) {
+            if (h + 1 < 64 / NB) issue(h + 1, tb[(h + 1) & 1]);
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+              const uint32_t j = h * NB + q;
+              if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
+              const bool in = (x >> j) & 1ull;
+#pragma unroll
+              for (int r = 0; r < R; ++r) {
+                const uint32_t y = est_recover(tb[h & 1][r][q], readlane_u32(la[r], j));
+                S[r] += in ? (uint64_t)y : 0ull;
+              }
+            }
+          }
+        }
+        cw += popc64(x);
+      }
+      if ((P1 & 63u) == 0) close(cw);  // a 64-aligned segment end is in no window
+    }
+    const size_t o = (size_t)sidx * LANES + lane, fs = (size_t)nseg * LANES;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      g.seg_tot[r][o] = cw;
+      g.seg_part[r][PB_ACCL * fs + o] = (uint64_t)acc[r];
+      g.seg_part[r][PB_ACCH * fs + o] = (uint64_t)(acc[r] >> 64);
+      g.seg_part[r][PB_ST * fs + o] = St[r];
+      g.seg_part[r][PB_TIEL * fs + o] = tie;
+      g.seg_part[r][PB_TIEH * fs + o] = 0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // final combination
 // ---------------------------------------------------------------------------------
 __device__ inline double i128_to_f64(i128 x) {
@@ -2402,6 +2550,151 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
   return VR_OK;
 }
 
+// R A plans (regions) x nb B plans (model layers), every unit pre-joined (joins[r][2 j] =
+// unit (j, r)'s A positions): scores of unit (j, r) at scores + (r nb + j) score_ld. The
+// EST passes run region-fused (k_rankB_grid: one B walk per B plan for all regions) when
+// the happy path holds -- EST 3 with its 4 form for the full set, masks in LDS, tie groups
+// < 2^16, every region's estimate passing its up-front check and every pass its flags;
+// otherwise (and for any region whose pass is flagged) each region runs as its own
+// run_engine_multi call, which re-runs flagged passes in the exact form. Es[r]: region r's
+// workspace (multi_layout, prejoined), which keeps its own TB beside the others'.
+static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_t nb, int64_t n, const int32_t* idx,
+                           int64_t k, int64_t n_sets, int full_first, double* scores, int64_t score_ld,
+                           uint32_t* const* const* joins, const EngineWs* Es, const EngineCfg& cfg, hipStream_t st) {
+  const int64_t M = pairs_of(n);
+  const int64_t total = n_sets + (full_first ? 1 : 0);
+  auto per_region = [&](int r) -> int {
+    return run_engine_multi(As[r], Bs, nb, n, idx, k, n_sets, full_first, scores + (size_t)r * nb * score_ld,
+                            score_ld, joins[r], Es[r], LANES, cfg, st);
+  };
+  auto all_per_region = [&]() -> int {
+    for (int r = 0; r < R; ++r) VR_TRY(per_region(r));
+    return VR_OK;
+  };
+  if (total == 0 || nb == 0 || M == 0) return all_per_region();
+  std::vector<PlanHeader> hA((size_t)R), hB((size_t)nb);
+  for (int r = 0; r < R; ++r)
+    VR_CHECK_HIP(hipMemcpyAsync(&hA[(size_t)r], As[r].hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
+  for (int64_t j = 0; j < nb; ++j)
+    VR_CHECK_HIP(hipMemcpyAsync(&hB[(size_t)j], Bs[j].hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
+  VR_CHECK_HIP(hipStreamSynchronize(st));
+  bool fused = engine_est() && cfg.est_mode == 3 && cfg.est_lds && R >= 2 && R <= 4 &&
+               env_int("VISREPS_ENGINE_TRI", 0) == 0 && env_int("VISREPS_ENGINE_LO_JOIN", 0) == 0 &&
+               env_int("VISREPS_ENGINE_GRID", 1) != 0 && g_test_inject.load() < 0;
+  for (int r = 0; r < R && fused; ++r) fused = hA[(size_t)r].max_group < 65536u;
+  for (int64_t j = 0; j < nb && fused; ++j) fused = hB[(size_t)j].max_group < 65536u;
+  if (!fused) return all_per_region();
+  std::vector<char> nan_b((size_t)nb);
+  for (int64_t j = 0; j < nb; ++j) nan_b[(size_t)j] = hB[(size_t)j].has_nan != 0;
+  const uint2 e3 = est3_params(k, M);
+  const uint2 trip = make_uint2(0u, 0u);
+  const uint32_t ns = cfg.est_nseg, nsA = cfg.est_nsegA;
+  // the masks of a pass are built once (region 0's buffer) and read by every region
+  std::vector<EngineWs> E(Es, Es + R);
+  for (int r = 1; r < R; ++r) E[(size_t)r].masks = E[0].masks;
+  for (int r = 0; r < R; ++r) {
+    k_seg_table<<<(nsA + 256) / 256, 256, 0, st>>>(As[r].gstart, As[r].hdr, M, nsA, E[(size_t)r].segposA);
+    VR_CHECK_LAUNCH();
+  }
+  for (int64_t j = 0; j < nb; ++j) {  // B segments depend on the B plan only: region 0's table
+    k_seg_table<<<(ns + 256) / 256, 256, 0, st>>>(Bs[j].gstart, Bs[j].hdr, M, ns, E[0].segposB + E[0].segstride * (size_t)j);
+    VR_CHECK_LAUNCH();
+  }
+  // the up-front estimate check, per region (its counts are its own)
+  if (n_sets > 0 && env_int("VISREPS_ENGINE_EST_PREDICT", 1) != 0) {
+    const int nl0 = (int)std::min<int64_t>(LANES, total);
+    VR_TRY(build_pass_masks(idx, k, 0, nl0, full_first, E[0].masks, n, st));
+    for (int r = 0; r < R; ++r) {
+      bool bad = false;
+      VR_TRY((est_predict<true, true>(As[r], n, E[(size_t)r], LANES, nl0, full_first != 0, cfg, e3, st, bad)));
+      if (bad) return all_per_region();
+    }
+  }
+  static bool attr = false;
+  if (!attr) {
+    VR_TRY(allow_big_lds(k_rankB_grid<2>));
+    VR_TRY(allow_big_lds(k_rankB_grid<3>));
+    VR_TRY(allow_big_lds(k_rankB_grid<4>));
+    attr = true;
+  }
+  const int64_t npass = (total + LANES - 1) / LANES;
+  const unsigned ggrid = (unsigned)num_cus();  // one 16-wave workgroup per CU (4 waves per SIMD)
+  for (int r = 0; r < R; ++r)
+    VR_CHECK_HIP(hipMemsetAsync(E[(size_t)r].viol, 0, (size_t)std::min<int64_t>(npass, EST_MAX_PASSES) * sizeof(uint32_t), st));
+  for (int64_t p = 0; p < npass; ++p) {
+    const int64_t set0 = p * LANES;
+    const int nl = (int)std::min<int64_t>(LANES, total - set0);
+    const bool full0 = full_first && p == 0;
+    const int64_t vslot = p % EST_MAX_PASSES;
+    VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E[0].masks, n, st));
+    for (int r = 0; r < R; ++r) {
+      VR_CHECK_HIP(hipMemsetAsync(E[(size_t)r].queue, 0, sizeof(uint32_t) * (size_t)QS_RANKB, st));
+      uint32_t* viol = E[(size_t)r].viol + vslot;
+      VR_TRY((full0 ? pass_a_est<4, true, true, false>(As[r], n, E[(size_t)r], LANES, nl, cfg, e3, trip, viol, st)
+                    : pass_a_est<3, true, true, false>(As[r], n, E[(size_t)r], LANES, nl, cfg, e3, trip, viol, st)));
+    }
+    VR_CHECK_HIP(hipMemsetAsync(E[0].queue + QS_RANKB, 0,
+                                sizeof(uint32_t) * (size_t)std::min<int64_t>(nb, QSLOTS - QS_RANKB), st));
+    for (int64_t j = 0; j < nb; ++j) {
+      GridB g{};
+      for (int r = 0; r < R; ++r) {
+        const size_t us = E[(size_t)r].useg * (size_t)j;
+        g.TB[r] = static_cast<const uint16_t*>(E[(size_t)r].TB);
+        g.posA[r] = joins[r][2 * j];
+        g.seg_tot[r] = E[(size_t)r].segB_tot + us;
+        g.seg_part[r] = E[(size_t)r].segB_part + us * PB_N;
+      }
+      uint32_t* q = E[0].queue + QS_RANKB + (size_t)j % (size_t)(QSLOTS - QS_RANKB);
+      if (j >= QSLOTS - QS_RANKB) VR_CHECK_HIP(hipMemsetAsync(q, 0, sizeof(uint32_t), st));
+      const uint32_t* segpos = E[0].segposB + E[0].segstride * (size_t)j;
+      KtScope kt(full0 ? KT_RANKB_FULL : KT_RANKB_GRID, (double)M * R, st);
+      if (R == 2)
+        k_rankB_grid<2><<<ggrid, ENG_THREADS, cfg.tab, st>>>(Bs[j].codes, Bs[j].gflag, E[0].masks, n, g, ns, E[0].ftab,
+                                                             segpos, q);
+      else if (R == 3)
+        k_rankB_grid<3><<<ggrid, ENG_THREADS, cfg.tab, st>>>(Bs[j].codes, Bs[j].gflag, E[0].masks, n, g, ns, E[0].ftab,
+                                                             segpos, q);
+      else
+        k_rankB_grid<4><<<ggrid, ENG_THREADS, cfg.tab, st>>>(Bs[j].codes, Bs[j].gflag, E[0].masks, n, g, ns, E[0].ftab,
+                                                             segpos, q);
+      VR_CHECK_LAUNCH();
+    }
+    for (int r = 0; r < R; ++r) {
+      if (full0) {
+        for (int64_t j = 0; j < nb; ++j) {
+          KtScope kt(KT_FULL_CORR, (double)M, st);
+          k_full_corr<<<CORR_BLK, 256, 0, st>>>(joins[r][2 * j], Bs[j].gflag, Bs[j].gstart, hB[(size_t)j].G, M, e3.y,
+                                                E[(size_t)r].corr + (size_t)j * CORR_N);
+          VR_CHECK_LAUNCH();
+        }
+      }
+      VR_TRY(tail_units(E[(size_t)r], nb, ns, cfg.est_ratioA, hA[(size_t)r].has_nan != 0, nan_b, nl,
+                        scores + (size_t)r * nb * score_ld + set0, score_ld, E[(size_t)r].viol + vslot, st,
+                        full0 ? E[(size_t)r].corr : nullptr));
+    }
+    // flags: after the first pass, then every EST_MAX_PASSES passes and at the end
+    if (p == 0 || vslot == EST_MAX_PASSES - 1 || p == npass - 1) {
+      const int64_t cnt = vslot + 1;
+      for (int r = 0; r < R; ++r) {
+        std::vector<uint32_t> flags((size_t)cnt);
+        VR_CHECK_HIP(hipMemcpyAsync(flags.data(), E[(size_t)r].viol, flags.size() * sizeof(uint32_t),
+                                    hipMemcpyDeviceToHost, st));
+        VR_CHECK_HIP(hipStreamSynchronize(st));
+        bool any = false;
+        for (uint32_t f : flags) any = any || f != 0;
+        // a flagged pass (rare: the estimate missed, or a B-side recovery broke the tail
+        // invariants): every region again on its own (EST with exact re-runs of its flagged
+        // passes), which rewrites every score
+        if (any) return all_per_region();
+      }
+      if (vslot == EST_MAX_PASSES - 1 && p + 1 < npass)
+        for (int r = 0; r < R; ++r)
+          VR_CHECK_HIP(hipMemsetAsync(E[(size_t)r].viol, 0, (size_t)EST_MAX_PASSES * sizeof(uint32_t), st));
+    }
+  }
+  return VR_OK;
+}
+
 // Scores for `total` subsets (full set first if full_first), 64 per pass.
 static int run_engine(const PlanView& A, const PlanView& B, int64_t n, const int32_t* idx,
                       int64_t k, int64_t n_sets, int full_first, double* scores,
@@ -2579,6 +2872,52 @@ int vr_bootstrap_spearman_multi_joined(const void* planA, const void* const* pla
   for (int64_t j = 0; j < n_b; ++j) Bs.push_back(plan_layout(const_cast<void*>(planBs[j]), n));
   return run_engine_multi(A, Bs.data(), n_b, n, idx, k, n_sets, full_first, scores, ld_scores,
                           joins.data(), E, LANES, cfg, as_stream(stream));
+}
+
+size_t vr_bootstrap_grid_joined_workspace(int64_t n, int64_t n_a, int64_t n_b) {
+  n = n < 0 ? 0 : n;
+  n_a = n_a < 1 ? 1 : n_a;
+  n_b = n_b < 1 ? 1 : n_b;
+  return (size_t)n_a * multi_layout(nullptr, n, n_b, engine_cfg(n).nwaves, nullptr, nullptr, true);
+}
+
+int vr_bootstrap_spearman_grid_joined(const void* const* planAs, int64_t n_a, const void* const* planBs, int64_t n_b,
+                                      int64_t n, const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
+                                      double* scores, int64_t ld_scores, uint32_t* const* posA, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  const char* fn = "vr_bootstrap_spearman_grid_joined";
+  VR_REQUIRE(n >= 0 && n <= 65535, "%s: n=%lld out of range", fn, (long long)n);
+  VR_REQUIRE(n_a >= 1 && n_a <= 4, "%s: n_a=%lld not in [1, 4]", fn, (long long)n_a);
+  VR_REQUIRE(n_b >= 0, "%s: n_b=%lld", fn, (long long)n_b);
+  VR_REQUIRE(planAs && (n_b == 0 || (planBs && scores && posA)), "%s: null pointer", fn);
+  VR_REQUIRE(k >= 0 && k <= n && n_sets >= 0, "%s: bad k=%lld sets=%lld", fn, (long long)k, (long long)n_sets);
+  VR_REQUIRE(idx != nullptr || n_sets == 0 || k == 0, "%s: null idx", fn);
+  const int64_t total = n_sets + (full_first ? 1 : 0);
+  VR_REQUIRE(ld_scores >= total, "%s: ld_scores %lld < %lld", fn, (long long)ld_scores, (long long)total);
+  for (int64_t i = 0; i < n_a; ++i) VR_REQUIRE(planAs[i] != nullptr, "%s: planAs[%lld] is null", fn, (long long)i);
+  for (int64_t j = 0; j < n_b; ++j) VR_REQUIRE(planBs[j] != nullptr, "%s: planBs[%lld] is null", fn, (long long)j);
+  for (int64_t u = 0; u < n_a * n_b; ++u) VR_REQUIRE(posA[u] != nullptr, "%s: posA[%lld] is null", fn, (long long)u);
+  EngineCfg cfg = engine_cfg(n);
+  cfg.prejoined = true;
+  const size_t one = multi_layout(nullptr, n, n_b, cfg.nwaves, nullptr, nullptr, true);
+  if (ws == nullptr || ws_bytes < one * (size_t)n_a) {
+    set_error("%s: workspace %zu < %zu", fn, ws_bytes, one * (size_t)n_a);
+    return VR_EWORKSPACE;
+  }
+  std::vector<EngineWs> E((size_t)n_a);
+  std::vector<std::vector<uint32_t*>> jv((size_t)n_a);
+  std::vector<uint32_t* const*> joins((size_t)n_a);
+  std::vector<PlanView> As;
+  for (int64_t i = 0; i < n_a; ++i) {
+    multi_layout(static_cast<char*>(ws) + (size_t)i * one, n, n_b, cfg.nwaves, &E[(size_t)i], &jv[(size_t)i], true);
+    for (int64_t j = 0; j < n_b; ++j) jv[(size_t)i][(size_t)(2 * j)] = posA[i * n_b + j];
+    joins[(size_t)i] = jv[(size_t)i].data();
+    As.push_back(plan_layout(const_cast<void*>(planAs[i]), n));
+  }
+  std::vector<PlanView> Bs;
+  for (int64_t j = 0; j < n_b; ++j) Bs.push_back(plan_layout(const_cast<void*>(planBs[j]), n));
+  return run_engine_grid(As.data(), (int)n_a, Bs.data(), n_b, n, idx, k, n_sets, full_first, scores, ld_scores,
+                         joins.data(), E.data(), cfg, as_stream(stream));
 }
 
 size_t vr_engine_posmap4_bytes(int64_t n) { return (size_t)pairs_of(n) * sizeof(uint4); }

@@ -100,7 +100,8 @@ enum KtKernel : int {
   KT_COV = 9,         // k_cov: fp64 MFMA covariance / Gram tiles (PCA covariance, ridge kernel matrix)
   KT_JOIN4 = 10,      // k_join4: shared join of one B plan to up to 4 A plans (units = algorithmic bytes)
   KT_FULL_CORR = 11,  // k_full_corr: lane 0's shift sums of an EST 4 pass, per unit (4 B / pair streamed)
-  KT_N = 12
+  KT_RANKB_GRID = 12,  // k_rankB_grid: one B plan x up to 4 regions, EST 3 (units: pairs x regions)
+  KT_N = 13
 };
 bool ktimer_on();
 struct KtScope {

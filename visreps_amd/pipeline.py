@@ -725,6 +725,39 @@ def run_unit(plan_m: R.RankPlan, plan_n: R.RankPlan, idx: Optional[np.ndarray],
     return scores
 
 
+def engine_grid_bytes(n: int, subsets: int, regions: int, units_per_region: int) -> float:
+    """Algorithmic HBM bytes of one grid call (bootstrap_spearman_grid, every unit joined):
+    per region its A side as engine_call_bytes; per pass and B plan one walk for all regions,
+    the B codes once (4 B per pair) and per region the A position (4) and the TB row (128)."""
+    tri = engine_tri(n)
+    if tri:  # (the grid form has no triangle-order variant: the per-region calls)
+        return regions * engine_call_bytes(n, subsets, units_per_region, joined=True)
+    a, b, _ = engine_pair_bytes(tri=False)
+    M = n * (n - 1) // 2
+    passes = -(-subsets // 64)
+    walk = 4 + regions * (b - 4)  # codes once, then per region A position + TB row
+    return float(M) * (passes * (regions * a + units_per_region * walk) + 4 * regions * units_per_region)
+
+
+def run_grid(plans_n: Sequence[R.RankPlan], plans_m: Sequence[R.RankPlan], idx: Optional[np.ndarray],
+             joined: Sequence[Sequence[torch.Tensor]], times: Optional[StepTimes] = None) -> torch.Tensor:
+    """Units (m, n) for every model plan m against every neural plan n (<= 4 regions) in one
+    engine call: (len(plans_n), len(plans_m), 1 + n_boot) scores, each model plan walked once
+    per pass for all regions (bootstrap_spearman_grid). joined[m][r] from SharedJoins."""
+    ev = None
+    if times is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+    scores = R.bootstrap_spearman_grid(plans_n, plans_m, idx, joined, full_first=True)
+    if times is not None:
+        ev[1].record()
+        nb = 0 if idx is None else len(idx)
+        units = len(plans_n) * len(plans_m)
+        times.record("engine", ev[0], ev[1], engine_grid_bytes(plans_n[0].n, nb + 1, len(plans_n), len(plans_m)),
+                     calls=units, ref=engine_bytes(plans_n[0].n, nb) * units)
+    return scores
+
+
 def shared_join_bytes(n: int, n_a: int, n_b: int) -> float:
     """Algorithmic bytes of SharedJoins over n_a A plans and n_b B plans: the interleave
     (4 B read per A plan, 16 B written per pair) and per B plan its codes 4 + the 16-B record
@@ -961,6 +994,26 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
         if dev.type == "cuda" and need <= 0.25 * torch.cuda.mem_get_info(dev)[0]:
             pns = {r: (plans[("n", r)] if ("n", r) in plans else plan_fn(neural_rdms[r])) for r in by_region}
             joined = shared_joins(pns, by_region, mplans, times)
+    # Regions sharing their point list (all of them on one GPU) run in groups of up to 4 as
+    # one grid call each: every model plan walked once per pass for the group's regions
+    if joined is not None and os.environ.get("VISREPS_ENGINE_GRID", "1") != "0":
+        groups = []
+        for r in by_region:
+            same = [g for g in groups if by_region[g[0]] == by_region[r] and len(g) < 4]
+            if same:
+                same[0].append(r)
+            else:
+                groups.append([r])
+        for grp in [g for g in groups if len(g) >= 2]:
+            pts = by_region[grp[0]]
+            pg_n = [plans[("n", r)] if ("n", r) in plans else pns.pop(r) for r in grp]
+            out = run_grid(pg_n, [mplans[p] for p in pts], idx,
+                           [[joined.pop((p, r)) for r in grp] for p in pts], times)
+            for i, r in enumerate(grp):
+                for j, p in enumerate(pts):
+                    local[(p, r)] = np.asarray(out[i, j].cpu())
+                del by_region[r]
+            del pg_n, out
     for r, pts in by_region.items():
         pn = plans[("n", r)] if ("n", r) in plans else (pns.pop(r) if joined is not None else plan_fn(neural_rdms[r]))
         if joined is not None:
