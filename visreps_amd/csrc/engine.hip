@@ -1716,6 +1716,12 @@ struct GridB {
 #ifndef VR_GRID_NB
 #define VR_GRID_NB 4  // pairs per gather batch (x R regions loads in flight, two batches)
 #endif
+#ifndef VR_GRID_NT
+#define VR_GRID_NT 1  // TB rows read with nontemporal loads (each is read once per pass and region)
+#endif
+#ifndef VR_GRID_MASKMUL
+#define VR_GRID_MASKMUL 0  // 1: mask the shared multipliers instead of each region's rank (A/B)
+#endif
 #ifndef VR_GRID_MINW
 #define VR_GRID_MINW 4  // waves per SIMD the grid walk is compiled for (4: 128 VGPRs)
 #endif
@@ -1773,7 +1779,11 @@ __global__ __launch_bounds__(ENG_THREADS, VR_GRID_MINW) void k_rankB_grid(
           for (int q = 0; q < NB; ++q)
 #pragma unroll
             for (int r = 0; r < R; ++r)
+#if VR_GRID_NT
               t[r][q] = __builtin_nontemporal_load(g.TB[r] + (size_t)readlane_u32(pa[r], h * NB + q) * LANES + lane_off);
+#else
+              t[r][q] = g.TB[r][(size_t)readlane_u32(pa[r], h * NB + q) * LANES + lane_off];
+#endif
         };
         uint32_t tb[2][R][NB];
         if (F == ~0ull) {  // every position starts a group (k_rankB's per-window form explains)
@@ -1790,14 +1800,25 @@ __global__ __launch_bounds__(ENG_THREADS, VR_GRID_MINW) void k_rankB_grid(
             for (int q = 0; q < NB; ++q) {
               const uint32_t j = h * NB + q;
               const uint32_t mk = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
+#if VR_GRID_MASKMUL
+              // the inclusion mask on the shared multipliers: c1 & mk and mk & 1 (two 64-bit
+              // multiply-adds per region, no per-region mask)
+              const uint32_t c1m = c1 & mk, bit = mk & 1u;
+#endif
 #pragma unroll
               for (int r = 0; r < R; ++r) {
-                const uint32_t yb = est_recover(tb[h & 1][r][q], readlane_u32(la[r], j)) & mk;
+                const uint32_t y = est_recover(tb[h & 1][r][q], readlane_u32(la[r], j));
                 if (j < 63) {
+#if VR_GRID_MASKMUL
+                  a64[r] += (uint64_t)y * c1m;
+                  St[r] += (uint64_t)y * bit;
+#else
+                  const uint32_t yb = y & mk;
                   a64[r] += (uint64_t)yb * c1;
                   St[r] += yb;
+#endif
                 } else {
-                  S[r] = yb;
+                  S[r] = y & mk;
                 }
               }
               if (j < 63)
