@@ -122,13 +122,13 @@ def split_mode(n: int, dims: dict) -> bool:
     return mode == "split" or all(float(n) * n * d >= 1e10 for d in dims.values())
 
 
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r5_pmc_engine_joined.json")
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r5_pmc_engine_grid.json")
 
 
 def pmc_traffic(n: int, est: bool):
     """HBM bytes of the engine from the committed rocprofv3 --pmc passes over the bench's own
-    engine path on its RDMs (JOINED=1 scripts/gpu_pmc_engine.sh: shared joins + one joined
-    call per region, 56 units): FETCH_SIZE x 2 (the gfx950
+    engine path on its RDMs (JOINED=1 GRID=1 scripts/gpu_pmc_engine.sh: shared joins + one
+    region-fused grid call, 56 units): FETCH_SIZE x 2 (the gfx950
     correction, MI355X_MICROARCH.md; calibrated for these 128-B row gathers in
     profiles/r2_fetch_calibration.json) + WRITE_SIZE. A PMC pass cannot share this timed
     run, so the figures come from that separate profile -- and only when it was taken on this
@@ -141,7 +141,7 @@ def pmc_traffic(n: int, est: bool):
     except (OSError, ValueError):
         return None
     if (d.get("build_id") != build_id() or int(d.get("n", -1)) != n or bool(d.get("est", True)) != est
-            or not d.get("joined", False)):
+            or not d.get("joined", False) or not d.get("grid", False)):
         return None
     return d
 

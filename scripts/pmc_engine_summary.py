@@ -42,12 +42,15 @@ def main(d, units, n=10000):
                    "bytes_per_launch": (fb + wb) / max(calls, 1)}
         total += fb + wb
     joined = os.environ.get("JOINED", "0") == "1"
+    grid = joined and os.environ.get("GRID", "0") == "1"
     what = (f"the bench's engine path over {units} units (shared joins: vr_engine_posmap4 + vr_engine_join4 "
-            "per model plan, then one vr_bootstrap_spearman_multi_joined call per region)" if joined else
+            "per model plan, then one region-fused vr_bootstrap_spearman_grid_joined call)" if grid else
+            f"{units} units (shared joins: vr_engine_posmap4 + vr_engine_join4 per model plan, then one "
+            "vr_bootstrap_spearman_multi_joined call per region)" if joined else
             f"one {units}-unit vr_bootstrap_spearman_multi call")
     out = {"source": (f"rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE (separate passes) over {what} on the bench "
                       "RDMs (scripts/gpu_pmc_engine.sh); FETCH_SIZE x 2 (gfx950 correction)"),
-           "joined": joined,
+           "joined": joined, "grid": grid,
            "units_per_call": units, "call_bytes": total, "bytes_per_unit": total / units,
            "kernels": kern, "n": n, "est": os.environ.get("VISREPS_ENGINE_EST") != "0",
            "build_id": build_id()}
