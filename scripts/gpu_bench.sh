@@ -10,7 +10,7 @@ mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 480 python bench.py > $out/bench.json 2> $out/bench.err || { echo "bench failed"; tail -20 $out/bench.err; exit 1; }
 cat $out/bench.json
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o p --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-est-probe --no-extra-legs \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o p --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-est-probe --no-extra-legs --no-exact-step \
     > $out/prof.json 2> $out/prof.err || { echo "rocprof failed"; tail -20 $out/prof.err; exit 1; }
 python3 scripts/check_timed_kernels.py $out/prof/p_kernel_trace.csv $out/timed_kernels.json || exit 1
 rm -f $out/prof/p_kernel_trace.csv

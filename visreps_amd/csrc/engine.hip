@@ -2364,7 +2364,10 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
   for (int64_t j = 0; j < nb; ++j) nan_b[(size_t)j] = h[(size_t)j + 1].has_nan != 0;
   const bool bigA = h[0].max_group >= 65536u;
   const bool est = engine_est();
-  const uint2 e3 = est3_params(k, M);
+  // (a point-only call holds the full set alone: its window is the full set's, so lane 0's
+  // EST 4 shift is at most 1 -- with k's window instead a group of > 3 tied pairs could
+  // shift below 1 and flag the pass)
+  const uint2 e3 = est3_params(n_sets > 0 ? k : n, M);
   int second = JOIN_NONE;  // what the joins' second arrays hold
   auto join = [&](int mode) -> int {
     for (int64_t j = 0; j < nb; ++j) {
@@ -2607,7 +2610,10 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
   if (!fused) return all_per_region();
   std::vector<char> nan_b((size_t)nb);
   for (int64_t j = 0; j < nb; ++j) nan_b[(size_t)j] = hB[(size_t)j].has_nan != 0;
-  const uint2 e3 = est3_params(k, M);
+  // (a point-only call holds the full set alone: its window is the full set's, so lane 0's
+  // EST 4 shift is at most 1 -- with k's window instead a group of > 3 tied pairs could
+  // shift below 1 and flag the pass)
+  const uint2 e3 = est3_params(n_sets > 0 ? k : n, M);
   const uint2 trip = make_uint2(0u, 0u);
   const uint32_t ns = cfg.est_nseg, nsA = cfg.est_nsegA;
   // the masks of a pass are built once (region 0's buffer) and read by every region
