@@ -2,7 +2,7 @@
 the bench's synthetic RDM shapes, HIP events around the point-only call and the full
 1001-subset call, per-kernel times from vr_ktimer where available.
 
-  python scripts/probe_kendall.py [n] [n_boot]
+  python scripts/probe_kendall.py [n] [n_boot]      (CASES=unit,point ... to run a subset)
 """
 import json
 import os
@@ -36,6 +36,8 @@ def main():
     for name, a, b, sets in (("point", "model", "neural", None), ("one_pass", "model", "neural", idx[:63]),
                              ("unit", "model", "neural", idx), ("unit_n2_n", "neural2", "neural", idx),
                              ("unit_noise_n", "noise", "neural", idx), ("unit_n_noise", "neural", "noise", idx)):
+        if os.environ.get("CASES") and name not in os.environ["CASES"].split(","):
+            continue
         pa, pb = plans[a], plans[b]
         R.bootstrap_kendall(pa, pb, sets if sets is None else sets[:2], full_first=True)  # warm
         torch.cuda.synchronize()

@@ -608,7 +608,7 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_countA(
       uint32_t w0 = P0 & ~63u;
       uint32_t cd = (w0 + lane >= P0 && w0 + lane < P1) ? codes[w0 + lane] : 0u;
       for (; w0 < P1; w0 += 64) {
-        const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+        const uint64_t x = window_bits<VR_XPOSE_A>(m, cd, w0, P0, P1, lane, active);
         if (w0 + 64 < P1) {
           const uint32_t q = w0 + 64 + lane;
           cd = q < P1 ? codes[q] : 0u;
@@ -831,7 +831,7 @@ __global__ __launch_bounds__(ENG_THREADS, 8) void k_rankA(
   #if VR_PROBE_WBA  // timing probe only (wrong scores): k_rankA without mask lookups / transposes
         const uint64_t x = active ? (0xF7DFBEFDFBF7EFDFull ^ ((uint64_t)(cd & 7u) << 3)) : 0ull;
   #else
-        const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+        const uint64_t x = window_bits<VR_XPOSE_A>(m, cd, w0, P0, P1, lane, active);
   #endif
         uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
         asm volatile("" ::"v"(x) : "memory");
@@ -1438,7 +1438,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
           // inclusion bits of window wv from its two mask words per lane
           auto bits_of = [&](uint32_t wv, uint64_t ma, uint64_t mb) -> uint64_t {
             const uint32_t pos = wv + (uint32_t)lane;
-            const uint64_t v = transpose64((pos >= P0 && pos < P1) ? (ma & mb) : 0ull, lane);
+            const uint64_t v = transpose64<VR_XPOSE_B>((pos >= P0 && pos < P1) ? (ma & mb) : 0ull, lane);
             return active ? v : 0ull;
           };
           uint32_t w = P0 & ~63u;
@@ -1452,7 +1452,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
             asm volatile("s_waitcnt vmcnt(0)" : "+v"(ma), "+v"(mb) : : "memory");
             x = bits_of(w, ma, mb);
           } else {
-            x = window_bits(m, cd, w, P0, P1, lane, active);
+            x = window_bits<VR_XPOSE_B>(m, cd, w, P0, P1, lane, active);
           }
           // group-start flags of the window (scalar loads), fetched one window ahead
           uint32_t f0 = sload(gflag + (w >> 5)), f1 = sload(gflag + (w >> 5) + 1);
@@ -1500,7 +1500,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
                       const uint32_t pn = wn + (uint32_t)lane;
                       xn = (active && pn >= P0 && pn < P1) ? (m[cdn >> 16] & m[cdn & 0xffffu]) : 0ull;
   #else
-                      xn = window_bits(m, cdn, wn, P0, P1, lane, active);
+                      xn = window_bits<VR_XPOSE_B>(m, cdn, wn, P0, P1, lane, active);
   #endif
                     }
                   }
@@ -1607,7 +1607,7 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
   #if VR_PROBE_WB  // timing probe only (wrong scores): no mask lookups, no transpose
         const uint64_t x = active ? (0xF7DFBEFDFBF7EFDFull ^ ((uint64_t)(cd & 7u) << 3)) : 0ull;
   #else
-        const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, active);
+        const uint64_t x = window_bits<VR_XPOSE_B>(m, cd, w0, P0, P1, lane, active);
   #endif
         const uint64_t F = restrict_flags(((uint64_t)f1 << 32) | f0, w0, P0, P1);
         if (w0 + 64 < P1) fetch(w0 + 64, pa, ca, cd, f0, f1);
@@ -1770,7 +1770,7 @@ __global__ __launch_bounds__(ENG_THREADS, VR_GRID_MINW) void k_rankB_grid(
           pa[r] = valid ? g.posA[r][pos] : 0u;
           la[r] = Lu + __umulhi(pa[r] << 1, Ru);
         }
-        const uint64_t x = window_bits(m, cd, w0, P0, P1, lane, true);
+        const uint64_t x = window_bits<VR_XPOSE_B>(m, cd, w0, P0, P1, lane, true);
         const uint64_t F =
             restrict_flags(((uint64_t)sload(gflag + (w0 >> 5) + 1) << 32) | sload(gflag + (w0 >> 5)), w0, P0, P1);
         // batch h's TB entries, t[r][q] = region r's row of pair h NB + q, lane's subset

@@ -313,7 +313,7 @@ __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
       const uint32_t q = pos + 64u;
       cd = q < (uint64_t)M ? codes[q] : 0u;
     }
-    uint64_t x = transpose64(mb, lane);
+    uint64_t x = transpose64<VR_XPOSE_K>(mb, lane);
     if (!active) x = 0ull;
     const uint64_t S = ((uint64_t)sload(sflag + 2 * win + 1) << 32) | sload(sflag + 2 * win);
     const uint64_t X = ((uint64_t)sload(aux + 2 * win + 1) << 32) | sload(aux + 2 * win);

@@ -90,15 +90,68 @@ __device__ inline uint64_t transpose_stage(uint64_t x, int lane) {
   return ((lane >> (5 - ST)) & 1) ? hi : lo;
 }
 
+// Transpose forms (template argument XM of transpose64 / window_bits):
+//   1: the 64-bit stages above;
+//   2: half-word stages (one exchange, one per-lane rotate, one bit select per 32-bit half;
+//      the w = 32 stage one permlane32_swap), per-lane stage constants rebuilt per call;
+//   3: the same with the constants loop-invariant (the compiler keeps them in ~9 VGPRs).
+// Defaults per walk (A side: count and rank walks; B side: the rank walks at their VGPR
+// budget, where 2 measured no faster than 1; Kendall: the stream walks).
+#ifndef VR_XPOSE_A
+#define VR_XPOSE_A 3
+#endif
+#ifndef VR_XPOSE_B
+#define VR_XPOSE_B 1
+#endif
+#ifndef VR_XPOSE_K
+#define VR_XPOSE_K 3
+#endif
+
+// Stage ST >= 1 (w = 32 >> ST <= 16) on one 32-bit half: the stage's bit moves stay inside
+// each half. A lane with lane bit w clear keeps its K bits and takes the partner's K bits
+// shifted up by w; a lane with it set keeps its ~K bits and takes the partner's ~K bits
+// shifted down by w. Rotating the partner's word right by sa = (set ? w : 32 - w) puts both
+// in place (the wrapped bits land on the kept positions of K = ...0000 1111 patterns), and
+// one bit select with Ml = K ^ F (F = all ones on set lanes) merges.
+template <int ST>
+__device__ inline void transpose_stage_h(uint32_t& lo, uint32_t& hi, int lane) {
+  constexpr uint32_t K[6] = {0u, 0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+  constexpr int w = 32 >> ST;
+  const uint32_t F = (uint32_t)__builtin_amdgcn_sbfe(lane, 5 - ST, 1);  // 0 or all ones
+  const uint32_t Ml = K[ST] ^ F;
+  const uint32_t sa = (F & (uint32_t)w) | (~F & (uint32_t)(32 - w));
+  const uint32_t pl = xor_lane<w>(lo, lane), ph = xor_lane<w>(hi, lane);
+  const uint32_t tl = __builtin_amdgcn_alignbit(pl, pl, sa), th = __builtin_amdgcn_alignbit(ph, ph, sa);
+  lo = ((lo ^ tl) & Ml) ^ tl;  // one 3-input bit op per half
+  hi = ((hi ^ th) & Ml) ^ th;
+}
+
 // 64x64 bit-matrix transpose across the wave: on entry bit s of lane j is element (j, s);
 // on exit bit j of lane s is. Recursive block swap, 6 stages of one 64-bit exchange.
+template <int XM>
 __device__ inline uint64_t transpose64(uint64_t x, int lane) {
-  x = transpose_stage<0>(x, lane);
-  x = transpose_stage<1>(x, lane);
-  x = transpose_stage<2>(x, lane);
-  x = transpose_stage<3>(x, lane);
-  x = transpose_stage<4>(x, lane);
-  return transpose_stage<5>(x, lane);
+  static_assert(XM >= 1 && XM <= 3, "transpose form");
+  if constexpr (XM == 1) {
+    x = transpose_stage<0>(x, lane);
+    x = transpose_stage<1>(x, lane);
+    x = transpose_stage<2>(x, lane);
+    x = transpose_stage<3>(x, lane);
+    x = transpose_stage<4>(x, lane);
+    return transpose_stage<5>(x, lane);
+  }
+  if constexpr (XM == 2) asm volatile("" : "+v"(lane));  // opaque per call: not loop-invariant
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  {  // w = 32: lanes 0-31 take lanes 32-63's low words as their high words and vice versa
+    const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+    lo = r[0];
+    hi = r[1];
+  }
+  transpose_stage_h<1>(lo, hi, lane);
+  transpose_stage_h<2>(lo, hi, lane);
+  transpose_stage_h<3>(lo, hi, lane);
+  transpose_stage_h<4>(lo, hi, lane);
+  transpose_stage_h<5>(lo, hi, lane);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // the round-1 form (every exchange a ds_bpermute): kept for reference timing
@@ -123,12 +176,13 @@ __device__ inline uint32_t popc64(uint64_t x) { return (uint32_t)__popcll(x); }
 
 // Inclusion bits of the window for this lane's subset (bit j <-> position w0 + j), from
 // the window's codes (lane j holds pair w0 + j).
+template <int XM>
 __device__ inline uint64_t window_bits(const uint64_t* m, uint32_t code, uint32_t w0, uint32_t P0,
                                        uint32_t P1, int lane, bool active) {
   const uint32_t pos = w0 + (uint32_t)lane;
   uint64_t x = 0;
   if (pos >= P0 && pos < P1) x = m[code >> 16] & m[code & 0xffffu];
-  x = transpose64(x, lane);
+  x = transpose64<XM>(x, lane);
   return active ? x : 0ull;
 }
 
