@@ -70,12 +70,21 @@ struct KSeg {
 
 // One window. TIE: o == z == the included members of multi-element tie groups, and the
 // count is sum over groups of C(k, 2). `seen` (uniform) = a segment start was met.
+// sum over zeros j of the ones before j in the window (segments ignored)
 template <bool TIE>
-VR_HD inline void kseg_window(uint64_t o, uint64_t z, uint64_t S, KSeg& a, bool& seen) {
+VR_HD inline uint64_t kseg_inner(uint64_t o, uint64_t z) {
+  if (TIE) {
+    const uint32_t p = kc_popc64(z);
+    return (uint64_t)p * (p - 1u) / 2u;
+  }
+  return kc_pairs64(o, z);
+}
+
+// One window given its kseg_inner (callers can compute several windows' inner counts first).
+template <bool TIE>
+VR_HD inline void kseg_window_inner(uint64_t o, uint64_t z, uint64_t S, uint64_t inner, KSeg& a, bool& seen) {
   const uint32_t pz = kc_popc64(z);
   const uint32_t po = TIE ? pz : kc_popc64(o);
-  // sum over zeros j of the ones before j in the window (segments ignored)
-  const uint64_t inner = TIE ? (uint64_t)po * (po - 1u) / 2u : kc_pairs64(o, z);
   if (S == 0) {
     a.acc += (uint64_t)a.c * pz + inner;
     if (!seen) a.zlead += pz;
@@ -102,6 +111,11 @@ VR_HD inline void kseg_window(uint64_t o, uint64_t z, uint64_t S, KSeg& a, bool&
   sub += (uint64_t)(pz - Zp) * Pp;
   a.acc -= sub;
   a.c = po - Pp;
+}
+
+template <bool TIE>
+VR_HD inline void kseg_window(uint64_t o, uint64_t z, uint64_t S, KSeg& a, bool& seen) {
+  kseg_window_inner<TIE>(o, z, S, kseg_inner<TIE>(o, z), a, seen);
 }
 
 // Cross-range fix-up, applied to ranges in stream order: range r's lead zeros pair with

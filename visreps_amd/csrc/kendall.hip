@@ -87,7 +87,7 @@ struct KendallWs {
   uint32_t* xj_mem;
   uint32_t* yb_start;  // B order: starts / members of multi-element B groups
   uint32_t* yb_mem;
-  uint64_t* w_acc;     // [grid][64] per-block summaries (KSum s, g, a, b) and included counts
+  uint64_t* w_acc;     // [pass][grid][64] per-block summaries (KSum s, g, a, b) and included counts
   uint64_t* w_g;
   uint64_t* w_a;
   uint32_t* w_b;
@@ -120,11 +120,13 @@ static KendallWs kendall_layout(void* base, int64_t n, int64_t cap_sets, int nwa
   uint32_t** fl[] = {&w.lv_start, &w.lv_bits, &w.xa_start, &w.xa_mem, &w.xj_start, &w.xj_mem,
                      &w.yb_start, &w.yb_mem};
   for (uint32_t** f : fl) *f = c.take<uint32_t>((size_t)FW);
-  w.w_acc = c.take<uint64_t>((size_t)nwaves * LANES);  // sized per wave; grid entries used
-  w.w_g = c.take<uint64_t>((size_t)nwaves * LANES);
-  w.w_a = c.take<uint64_t>((size_t)nwaves * LANES);
-  w.w_b = c.take<uint32_t>((size_t)nwaves * LANES);
-  w.w_incl = c.take<uint32_t>((size_t)nwaves * LANES);
+  // block summaries of every pass of one stream: [pass][block][lane] (grid = nwaves / 16)
+  const size_t wsum = (size_t)std::max<int64_t>(nwaves, std::max<int64_t>(npass, 1) * (nwaves / KW_WAVES)) * LANES;
+  w.w_acc = c.take<uint64_t>(wsum);
+  w.w_g = c.take<uint64_t>(wsum);
+  w.w_a = c.take<uint64_t>(wsum);
+  w.w_b = c.take<uint32_t>(wsum);
+  w.w_incl = c.take<uint32_t>(wsum);
   w.tot = c.take<uint64_t>((size_t)KF_N * (size_t)std::max<int64_t>(cap_sets, 1));
   if (bytes) *bytes = c.bytes();
   return w;
@@ -300,29 +302,58 @@ __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
   KSeg a{0ull, 0u, 0u};
   bool seen = false;
   uint32_t incl = 0;
-  uint32_t cd = 0;
-  if (wb < we) {
-    const uint32_t p0 = wb * 64u + (uint32_t)lane;
-    cd = p0 < (uint64_t)M ? codes[p0] : 0u;
-  }
-  for (uint32_t win = wb; win < we; ++win) {
+#ifndef VR_KW_PAIR
+#define VR_KW_PAIR 1  // 1: two windows per trip (mask lookups, transposes and pair counts of both
+                      // first, straight-line, so their dependency chains interleave)
+#endif
+  auto code_at = [&](uint32_t win) -> uint32_t {
+    const uint32_t q = win * 64u + (uint32_t)lane;
+    return q < (uint64_t)M ? codes[q] : 0u;
+  };
+  auto bits_of = [&](uint32_t cd, uint32_t win) -> uint64_t {
     const uint32_t pos = win * 64u + (uint32_t)lane;
-    const bool valid = pos < (uint64_t)M;
-    uint64_t mb = valid ? (m[cd >> 16] & m[cd & 0xffffu]) : 0ull;
-    if (win + 1 < we) {  // next window's code, one ahead
-      const uint32_t q = pos + 64u;
-      cd = q < (uint64_t)M ? codes[q] : 0u;
+    const uint64_t mb = pos < (uint64_t)M ? (m[cd >> 16] & m[cd & 0xffffu]) : 0ull;
+    const uint64_t x = transpose64<VR_XPOSE_K>(mb, lane);
+    return active ? x : 0ull;
+  };
+  auto plane = [&](const uint32_t* f, uint32_t win) -> uint64_t {
+    return ((uint64_t)sload(f + 2 * win + 1) << 32) | sload(f + 2 * win);
+  };
+  if (VR_KW_PAIR) {
+    uint32_t c0 = 0, c1 = 0;
+    if (wb < we) c0 = code_at(wb);
+    if (wb + 1 < we) c1 = code_at(wb + 1);
+    for (uint32_t win = wb; win < we; win += 2) {
+      const bool two = win + 1 < we;  // wave-uniform
+      const uint32_t d0 = c0, d1 = c1;
+      if (win + 2 < we) c0 = code_at(win + 2);  // the next pair's codes, one trip ahead
+      if (win + 3 < we) c1 = code_at(win + 3);
+      const uint64_t x0 = bits_of(d0, win);
+      const uint64_t x1 = two ? bits_of(d1, win + 1) : 0ull;
+      const uint64_t S0 = plane(sflag, win), X0 = plane(aux, win);
+      const uint64_t S1 = plane(sflag, win + 1), X1 = plane(aux, win + 1);  // in the padded planes
+      const uint64_t o0 = x0 & X0, z0 = TIE ? o0 : (x0 & ~X0);
+      const uint64_t o1 = x1 & X1, z1 = TIE ? o1 : (x1 & ~X1);
+      const uint64_t i0 = kseg_inner<TIE>(o0, z0), i1 = kseg_inner<TIE>(o1, z1);
+      incl += popc64(x0) + popc64(x1);
+      kseg_window_inner<TIE>(o0, z0, S0, i0, a, seen);
+      if (two) kseg_window_inner<TIE>(o1, z1, S1, i1, a, seen);
     }
-    uint64_t x = transpose64<VR_XPOSE_K>(mb, lane);
-    if (!active) x = 0ull;
-    const uint64_t S = ((uint64_t)sload(sflag + 2 * win + 1) << 32) | sload(sflag + 2 * win);
-    const uint64_t X = ((uint64_t)sload(aux + 2 * win + 1) << 32) | sload(aux + 2 * win);
-    incl += popc64(x);
-    if (TIE) {
-      const uint64_t o = x & X;
-      kseg_window<true>(o, o, S, a, seen);
-    } else {
-      kseg_window<false>(x & X, x & ~X, S, a, seen);
+  } else {
+    uint32_t cd = 0;
+    if (wb < we) cd = code_at(wb);
+    for (uint32_t win = wb; win < we; ++win) {
+      const uint32_t d = cd;
+      if (win + 1 < we) cd = code_at(win + 1);  // next window's code, one ahead
+      const uint64_t x = bits_of(d, win);
+      const uint64_t S = plane(sflag, win), X = plane(aux, win);
+      incl += popc64(x);
+      if (TIE) {
+        const uint64_t o = x & X;
+        kseg_window<true>(o, o, S, a, seen);
+      } else {
+        kseg_window<false>(x & X, x & ~X, S, a, seen);
+      }
     }
   }
   // The block's 16 wave ranges are consecutive: compose them here (affine carry maps, see
@@ -354,12 +385,17 @@ __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
 
 // Stream total per lane: the block summaries (k_kwalk) composed in block order with carry 0
 // into the first, added into tot[field][set0 + lane]; optionally the included-pair count into
-// tot[KF_INCL]. 16 groups compose contiguous block ranges, group 0 composes the groups.
+// tot[KF_INCL]. One block per pass (set0 = 64 x pass), all passes of a stream in one launch;
+// 16 groups compose contiguous block ranges, group 0 composes the groups.
 __global__ __launch_bounds__(KW_THREADS) void k_kfix(
     const uint64_t* __restrict__ w_acc, const uint64_t* __restrict__ w_g,
     const uint64_t* __restrict__ w_a, const uint32_t* __restrict__ w_b,
-    const uint32_t* __restrict__ w_incl, uint32_t nblk, int nl, int field, int add_incl,
-    uint64_t* __restrict__ tot, int64_t cap, int64_t set0) {
+    const uint32_t* __restrict__ w_incl, uint32_t nblk, int64_t total, int field, int add_incl,
+    uint64_t* __restrict__ tot, int64_t cap) {
+  const int64_t set0 = (int64_t)blockIdx.x * LANES;
+  const int nl = (int)(total - set0 < LANES ? total - set0 : LANES);
+  const size_t pbase = (size_t)blockIdx.x * nblk * LANES;
+  w_acc += pbase, w_g += pbase, w_a += pbase, w_b += pbase, w_incl += pbase;
   __shared__ uint64_t s_s[KFIX_GROUPS][LANES], s_g[KFIX_GROUPS][LANES], s_a[KFIX_GROUPS][LANES],
       s_inc[KFIX_GROUPS][LANES];
   __shared__ uint32_t s_b[KFIX_GROUPS][LANES];
@@ -445,24 +481,23 @@ static int walk_stream(bool tie, const uint32_t* codes, const uint32_t* sflag, c
                        int64_t M, const KendallWs& W, int64_t n, int64_t total, int field,
                        bool add_incl, int64_t cap, const KCfg& cfg, hipStream_t st) {
   if (cfg.use_lds) VR_TRY(set_kwalk_attr<true>());
-  auto walk = [&](const uint64_t* mk, int nl) {
+  auto walk = [&](const uint64_t* mk, int nl, size_t o) {
     const size_t lds = cfg.use_lds ? cfg.lds : 0;
     auto* k = cfg.use_lds ? (tie ? k_kwalk<true, true> : k_kwalk<true, false>)
                           : (tie ? k_kwalk<false, true> : k_kwalk<false, false>);
-    k<<<cfg.grid, KW_THREADS, lds, st>>>(codes, sflag, aux, M, mk, n, nl, (uint32_t)cfg.nwaves, W.w_acc, W.w_g,
-                                         W.w_a, W.w_b, W.w_incl);
+    k<<<cfg.grid, KW_THREADS, lds, st>>>(codes, sflag, aux, M, mk, n, nl, (uint32_t)cfg.nwaves, W.w_acc + o,
+                                         W.w_g + o, W.w_a + o, W.w_b + o, W.w_incl + o);
   };
-  for (int64_t set0 = 0, p = 0; set0 < total; set0 += LANES, ++p) {
+  int64_t npass = 0;
+  for (int64_t set0 = 0; set0 < total; set0 += LANES, ++npass) {
     const int nl = (int)std::min<int64_t>(LANES, total - set0);
-    {
-      KtScope kt(KT_KWALK, (double)M, st);  // the walk only, not its fix-up
-      walk(W.masks + (size_t)p * (size_t)n, nl);
-      VR_CHECK_LAUNCH();
-    }
-    k_kfix<<<1, KW_THREADS, 0, st>>>(W.w_acc, W.w_g, W.w_a, W.w_b, W.w_incl, (uint32_t)cfg.grid, nl, field,
-                                     add_incl ? 1 : 0, W.tot, cap, set0);
+    KtScope kt(KT_KWALK, (double)M, st);  // the walk only, not the fix-up
+    walk(W.masks + (size_t)npass * (size_t)n, nl, (size_t)npass * (size_t)cfg.grid * LANES);
     VR_CHECK_LAUNCH();
   }
+  k_kfix<<<(unsigned)npass, KW_THREADS, 0, st>>>(W.w_acc, W.w_g, W.w_a, W.w_b, W.w_incl, (uint32_t)cfg.grid,
+                                                 total, field, add_incl ? 1 : 0, W.tot, cap);
+  VR_CHECK_LAUNCH();
   return VR_OK;
 }
 
