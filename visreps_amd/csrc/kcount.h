@@ -99,16 +99,16 @@ VR_HD inline void kseg_window_inner(uint64_t o, uint64_t z, uint64_t S, uint64_t
   a.acc += (uint64_t)a.c * Zp + inner;
   if (!seen) a.zlead += Zp;
   seen = true;
-  uint64_t sub = 0;
+  uint32_t sub = 0;  // <= 64 x 64 inside one window
   for (uint64_t r = S & (S - 1); r; r &= r - 1) {
     mk = kc_lowmask(kc_ctz64(r));
     const uint32_t Zs = kc_popc64(z & mk);
     const uint32_t Ps = TIE ? Zs : kc_popc64(o & mk);
-    sub += (uint64_t)(Zs - Zp) * Pp;
+    sub += (Zs - Zp) * Pp;
     Zp = Zs;
     Pp = Ps;
   }
-  sub += (uint64_t)(pz - Zp) * Pp;
+  sub += (pz - Zp) * Pp;
   a.acc -= sub;
   a.c = po - Pp;
 }

@@ -77,8 +77,6 @@ struct KendallWs {
   uint32_t* scan;
   uint32_t* ecode[2];  // level streams: pair code and y (dense B rank), ping-pong
   uint32_t* ey[2];
-  uint32_t* zflag;
-  uint32_t* zscan;
   uint32_t* lv_start;  // [FW] bucket starts of the current level
   uint32_t* lv_bits;   // [FW] bit b of y
   uint32_t* xa_start;  // [FW] x-lex order: starts / members of multi-element A groups
@@ -115,8 +113,6 @@ static KendallWs kendall_layout(void* base, int64_t n, int64_t cap_sets, int nwa
     w.ecode[i] = c.take<uint32_t>((size_t)M);
     w.ey[i] = c.take<uint32_t>((size_t)M);
   }
-  w.zflag = c.take<uint32_t>((size_t)M);
-  w.zscan = c.take<uint32_t>((size_t)M);
   uint32_t** fl[] = {&w.lv_start, &w.lv_bits, &w.xa_start, &w.xa_mem, &w.xj_start, &w.xj_mem,
                      &w.yb_start, &w.yb_mem};
   for (uint32_t** f : fl) *f = c.take<uint32_t>((size_t)FW);
@@ -225,11 +221,9 @@ __global__ void k_border_flags(const uint32_t* __restrict__ gflag, int64_t M,
   put_plane(yb_mem, p, mem);
 }
 
-// level b planes of the current stream (sorted by y >> (b+1)): bit b of y, bucket starts;
-// zero flags for the split
+// level b planes of the current stream (sorted by y >> (b+1)): bit b of y, bucket starts
 __global__ void k_level_flags(const uint32_t* __restrict__ ey, int64_t M, int b,
-                              uint32_t* __restrict__ lv_start, uint32_t* __restrict__ lv_bits,
-                              uint32_t* __restrict__ zflag) {
+                              uint32_t* __restrict__ lv_start, uint32_t* __restrict__ lv_bits) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool v = p < M;
   bool st = false, bit = false;
@@ -237,7 +231,6 @@ __global__ void k_level_flags(const uint32_t* __restrict__ ey, int64_t M, int b,
     const uint32_t y = ey[p];
     bit = (y >> b) & 1u;
     st = p == 0 || (ey[p - 1] >> (b + 1)) != (y >> (b + 1));
-    zflag[p] = bit ? 0u : 1u;
   }
   put_plane(lv_start, p, st);
   put_plane(lv_bits, p, bit);
@@ -245,16 +238,22 @@ __global__ void k_level_flags(const uint32_t* __restrict__ ey, int64_t M, int b,
 
 // stable split of every bucket by bit b: the stream for level b-1 (sorted by y >> b).
 // gstartB[g] = number of elements with y < g, so the bucket of y >> (b+1) starts at
-// gstartB[(y >> (b+1)) << (b+1)] and its one-half at gstartB[(y >> b) << b].
+// gstartB[(y >> (b+1)) << (b+1)] and its one-half at gstartB[(y >> b) << b]. Zeros before a
+// position come from the level's bit plane: q - (ones in whole words before q, wpre = the
+// exclusive scan of the plane's word popcounts) - (ones below q in its word).
+__device__ inline uint32_t zeros_before(const uint32_t* __restrict__ bits, const uint32_t* __restrict__ wpre,
+                                        uint32_t q) {
+  return q - wpre[q >> 5] - (uint32_t)__popc(bits[q >> 5] & ((1u << (q & 31u)) - 1u));
+}
 __global__ void k_level_split(const uint32_t* __restrict__ ecode, const uint32_t* __restrict__ ey,
-                              const uint32_t* __restrict__ zscan, const uint32_t* __restrict__ gstartB,
-                              int64_t M, int b, uint32_t* __restrict__ ecode_out,
-                              uint32_t* __restrict__ ey_out) {
+                              const uint32_t* __restrict__ bits, const uint32_t* __restrict__ wpre,
+                              const uint32_t* __restrict__ gstartB, int64_t M, int b,
+                              uint32_t* __restrict__ ecode_out, uint32_t* __restrict__ ey_out) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= M) return;
   const uint32_t y = ey[p];
   const uint32_t bs = gstartB[(y >> (b + 1)) << (b + 1)];
-  const uint32_t zb = zscan[bs], zp = zscan[p];
+  const uint32_t zb = zeros_before(bits, wpre, bs), zp = zeros_before(bits, wpre, (uint32_t)p);
   uint32_t np;
   if ((y >> b) & 1u)
     np = gstartB[(y >> b) << b] + ((uint32_t)p - bs) - (zp - zb);
@@ -566,13 +565,16 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
   while (Lb < 32 && ((G - 1u) >> Lb) != 0u) ++Lb;
   int cur = 0;
   for (int b = Lb - 1; b >= 0; --b) {
-    k_level_flags<<<gbW, 256, 0, st>>>(W.ey[cur], M, b, W.lv_start, W.lv_bits, W.zflag);
+    k_level_flags<<<gbW, 256, 0, st>>>(W.ey[cur], M, b, W.lv_start, W.lv_bits);
     VR_CHECK_LAUNCH();
     VR_TRY(walk_stream(false, W.ecode[cur], W.lv_start, W.lv_bits, M, W, n, total, KF_DIS, b == Lb - 1,
                        cap, cfg, st));
     if (b > 0) {
-      VR_TRY(scan_exclusive_u32(W.zflag, W.zscan, M, nullptr, W.scan, st));
-      k_level_split<<<gbM, 256, 0, st>>>(W.ecode[cur], W.ey[cur], W.zscan, B.gstart, M, b,
+      const int64_t words = (M + 31) / 32;
+      k_word_popc<<<blocks_for(words, 256), 256, 0, st>>>(W.lv_bits, words, W.wcnt);
+      VR_CHECK_LAUNCH();
+      VR_TRY(scan_exclusive_u32(W.wcnt, W.wcnt, words, nullptr, W.scan, st));
+      k_level_split<<<gbM, 256, 0, st>>>(W.ecode[cur], W.ey[cur], W.lv_bits, W.wcnt, B.gstart, M, b,
                                          W.ecode[cur ^ 1], W.ey[cur ^ 1]);
       VR_CHECK_LAUNCH();
       cur ^= 1;
