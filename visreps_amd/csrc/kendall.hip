@@ -26,6 +26,7 @@
 // against it); per unit ~14 x M x 4 B of scratch.
 #include <algorithm>
 #include <cmath>
+#include <mutex>
 
 #include "kcount.h"
 #include "window.h"
@@ -77,8 +78,8 @@ struct KendallWs {
   uint32_t* scan;
   uint32_t* ecode[2];  // level streams: pair code and y (dense B rank), ping-pong
   uint32_t* ey[2];
-  uint32_t* lv_start;  // [FW] bucket starts of the current level
-  uint32_t* lv_bits;   // [FW] bit b of y
+  uint32_t* lv_start[2];  // [FW] bucket starts of a level (double-buffered: level b walked while
+  uint32_t* lv_bits[2];   //      level b-1 is prepared); bit b of y
   uint32_t* xa_start;  // [FW] x-lex order: starts / members of multi-element A groups
   uint32_t* xa_mem;
   uint32_t* xj_start;  //               ... of multi-element joint (A, B) groups
@@ -90,6 +91,11 @@ struct KendallWs {
   uint64_t* w_a;
   uint32_t* w_b;
   uint32_t* w_incl;
+  uint64_t* w2_acc;    // the same for the B tie stream, walked on the side stream beside the
+  uint64_t* w2_g;      // x-lex preparation and tie walks
+  uint64_t* w2_a;
+  uint32_t* w2_b;
+  uint32_t* w2_incl;
   uint64_t* tot;       // [KF_N][cap]
 };
 
@@ -113,7 +119,7 @@ static KendallWs kendall_layout(void* base, int64_t n, int64_t cap_sets, int nwa
     w.ecode[i] = c.take<uint32_t>((size_t)M);
     w.ey[i] = c.take<uint32_t>((size_t)M);
   }
-  uint32_t** fl[] = {&w.lv_start, &w.lv_bits, &w.xa_start, &w.xa_mem, &w.xj_start, &w.xj_mem,
+  uint32_t** fl[] = {&w.lv_start[0], &w.lv_bits[0], &w.lv_start[1], &w.lv_bits[1], &w.xa_start, &w.xa_mem, &w.xj_start, &w.xj_mem,
                      &w.yb_start, &w.yb_mem};
   for (uint32_t** f : fl) *f = c.take<uint32_t>((size_t)FW);
   // block summaries of every pass of one stream: [pass][block][lane] (grid = nwaves / 16)
@@ -123,6 +129,11 @@ static KendallWs kendall_layout(void* base, int64_t n, int64_t cap_sets, int nwa
   w.w_a = c.take<uint64_t>(wsum);
   w.w_b = c.take<uint32_t>(wsum);
   w.w_incl = c.take<uint32_t>(wsum);
+  w.w2_acc = c.take<uint64_t>(wsum);
+  w.w2_g = c.take<uint64_t>(wsum);
+  w.w2_a = c.take<uint64_t>(wsum);
+  w.w2_b = c.take<uint32_t>(wsum);
+  w.w2_incl = c.take<uint32_t>(wsum);
   w.tot = c.take<uint64_t>((size_t)KF_N * (size_t)std::max<int64_t>(cap_sets, 1));
   if (bytes) *bytes = c.bytes();
   return w;
@@ -511,6 +522,30 @@ static int group_index(const PlanView& P, int64_t M, const KendallWs& W, uint32_
   return VR_OK;
 }
 
+// The level preparation's side stream and its events, one set per device, created once. The
+// mutex serialises the enqueue of one call's levels (the events are reused across calls).
+struct KSide {
+  hipStream_t sp = nullptr;
+  hipEvent_t masks = nullptr, in = nullptr, prep[2] = {nullptr, nullptr}, walked[2] = {nullptr, nullptr};
+  std::mutex mu;
+};
+static int kendall_side(KSide*& out) {
+  static KSide sides[64];
+  static std::mutex init_mu;
+  int dev = 0;
+  VR_CHECK_HIP(hipGetDevice(&dev));
+  VR_REQUIRE(dev >= 0 && dev < 64, "kendall: device %d out of range", dev);
+  KSide& k = sides[dev];
+  std::lock_guard<std::mutex> g(init_mu);
+  if (!k.sp) {
+    VR_CHECK_HIP(hipStreamCreateWithFlags(&k.sp, hipStreamNonBlocking));
+    hipEvent_t* evs[] = {&k.masks, &k.in, &k.prep[0], &k.prep[1], &k.walked[0], &k.walked[1]};
+    for (hipEvent_t* e : evs) VR_CHECK_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  out = &k;
+  return VR_OK;
+}
+
 static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const int32_t* idx, int64_t k,
                        int64_t n_sets, int full_first, double* scores, const KendallWs& W,
                        int64_t cap, const KCfg& cfg, hipStream_t st) {
@@ -532,6 +567,27 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
   }
   const unsigned gbM = blocks_for(M, 256);
   const unsigned gbW = blocks_for(kwindows(M) * 64, 256);  // whole windows: ballots
+  KSide* side = nullptr;
+  VR_TRY(kendall_side(side));
+  std::unique_lock<std::mutex> side_lock(side->mu);
+  hipStream_t sp = side->sp;
+  // masks of every pass, totals zeroed
+  for (int64_t set0 = 0, p = 0; set0 < total; set0 += LANES, ++p) {
+    const int nl = (int)std::min<int64_t>(LANES, total - set0);
+    VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, W.masks + (size_t)p * (size_t)n, n, st));
+  }
+  VR_CHECK_HIP(hipMemsetAsync(W.tot, 0, sizeof(uint64_t) * (size_t)KF_N * (size_t)cap, st));
+  VR_CHECK_HIP(hipEventRecord(side->masks, st));
+  // B tie stream (B order: needs only the B plan) on the side stream, its own block summaries,
+  // beside the x-lex order's construction below
+  VR_CHECK_HIP(hipStreamWaitEvent(sp, side->masks, 0));
+  if (h[1].max_group > 1) {
+    KendallWs Wy = W;
+    Wy.w_acc = W.w2_acc, Wy.w_g = W.w2_g, Wy.w_a = W.w2_a, Wy.w_b = W.w2_b, Wy.w_incl = W.w2_incl;
+    k_border_flags<<<gbW, 256, 0, sp>>>(B.gflag, M, W.yb_start, W.yb_mem);
+    VR_CHECK_LAUNCH();
+    VR_TRY(walk_stream(true, B.codes, W.yb_start, W.yb_mem, M, Wy, n, total, KF_YTIE, false, cap, cfg, sp));
+  }
   // dense group ranks of both orders
   VR_TRY(group_index(A, M, W, W.gidxA, st));
   VR_TRY(group_index(B, M, W, W.gidxB, st));
@@ -541,45 +597,48 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
   VR_TRY(radix_sort_kv(W.keys, W.vals, W.keys_alt, W.vals_alt, M, W.radix, st));
   k_kendall_elems<<<gbM, 256, 0, st>>>(W.vals, B.codes, W.gidxB, M, W.ecode[0], W.ey[0]);
   VR_CHECK_LAUNCH();
-  // masks of every pass, totals zeroed
-  for (int64_t set0 = 0, p = 0; set0 < total; set0 += LANES, ++p) {
-    const int nl = (int)std::min<int64_t>(LANES, total - set0);
-    VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, W.masks + (size_t)p * (size_t)n, n, st));
-  }
-  VR_CHECK_HIP(hipMemsetAsync(W.tot, 0, sizeof(uint64_t) * (size_t)KF_N * (size_t)cap, st));
-  // tie streams (only when the plans have multi-element groups)
+  VR_CHECK_HIP(hipEventRecord(side->in, st));  // the level-0 stream exists: preparation may start
+  // x-lex tie streams (only when A has multi-element groups)
   if (h[0].max_group > 1) {
     k_xlex_flags<<<gbW, 256, 0, st>>>(W.keys, W.ey[0], M, W.xa_start, W.xa_mem, W.xj_start, W.xj_mem);
     VR_CHECK_LAUNCH();
     VR_TRY(walk_stream(true, W.ecode[0], W.xa_start, W.xa_mem, M, W, n, total, KF_XTIE, false, cap, cfg, st));
     VR_TRY(walk_stream(true, W.ecode[0], W.xj_start, W.xj_mem, M, W, n, total, KF_NTIE, false, cap, cfg, st));
   }
-  if (h[1].max_group > 1) {
-    k_border_flags<<<gbW, 256, 0, st>>>(B.gflag, M, W.yb_start, W.yb_mem);
-    VR_CHECK_LAUNCH();
-    VR_TRY(walk_stream(true, B.codes, W.yb_start, W.yb_mem, M, W, n, total, KF_YTIE, false, cap, cfg, st));
-  }
   // inversion levels, most significant y bit first
   const uint32_t G = h[1].G;
   int Lb = 0;
   while (Lb < 32 && ((G - 1u) >> Lb) != 0u) ++Lb;
-  int cur = 0;
+  // Level b walks stream c = (Lb - 1 - b) & 1 (ecode/ey[c], planes lv_*[c]) on the caller's
+  // stream while the side stream prepares level b - 1 into the other buffers (plane word
+  // scan, stable split, next planes): VALU-bound walks and memory-bound preparation share the
+  // CUs (a walk block holds one 16-wave workgroup per CU). The preparation of b - 1 waits for
+  // the walks of b + 1, the last readers of the buffers it writes.
+  const int64_t words = (M + 31) / 32;
+  VR_CHECK_HIP(hipStreamWaitEvent(sp, side->in, 0));
+  k_level_flags<<<gbW, 256, 0, sp>>>(W.ey[0], M, Lb - 1, W.lv_start[0], W.lv_bits[0]);
+  VR_CHECK_LAUNCH();
+  VR_CHECK_HIP(hipEventRecord(side->prep[0], sp));
   for (int b = Lb - 1; b >= 0; --b) {
-    k_level_flags<<<gbW, 256, 0, st>>>(W.ey[cur], M, b, W.lv_start, W.lv_bits);
-    VR_CHECK_LAUNCH();
-    VR_TRY(walk_stream(false, W.ecode[cur], W.lv_start, W.lv_bits, M, W, n, total, KF_DIS, b == Lb - 1,
-                       cap, cfg, st));
+    const int c = (Lb - 1 - b) & 1;
     if (b > 0) {
-      const int64_t words = (M + 31) / 32;
-      k_word_popc<<<blocks_for(words, 256), 256, 0, st>>>(W.lv_bits, words, W.wcnt);
+      if (b < Lb - 1) VR_CHECK_HIP(hipStreamWaitEvent(sp, side->walked[c ^ 1], 0));
+      k_word_popc<<<blocks_for(words, 256), 256, 0, sp>>>(W.lv_bits[c], words, W.wcnt);
       VR_CHECK_LAUNCH();
-      VR_TRY(scan_exclusive_u32(W.wcnt, W.wcnt, words, nullptr, W.scan, st));
-      k_level_split<<<gbM, 256, 0, st>>>(W.ecode[cur], W.ey[cur], W.lv_bits, W.wcnt, B.gstart, M, b,
-                                         W.ecode[cur ^ 1], W.ey[cur ^ 1]);
+      VR_TRY(scan_exclusive_u32(W.wcnt, W.wcnt, words, nullptr, W.scan, sp));
+      k_level_split<<<gbM, 256, 0, sp>>>(W.ecode[c], W.ey[c], W.lv_bits[c], W.wcnt, B.gstart, M, b,
+                                         W.ecode[c ^ 1], W.ey[c ^ 1]);
       VR_CHECK_LAUNCH();
-      cur ^= 1;
+      k_level_flags<<<gbW, 256, 0, sp>>>(W.ey[c ^ 1], M, b - 1, W.lv_start[c ^ 1], W.lv_bits[c ^ 1]);
+      VR_CHECK_LAUNCH();
+      VR_CHECK_HIP(hipEventRecord(side->prep[c ^ 1], sp));
     }
+    VR_CHECK_HIP(hipStreamWaitEvent(st, side->prep[c], 0));
+    VR_TRY(walk_stream(false, W.ecode[c], W.lv_start[c], W.lv_bits[c], M, W, n, total, KF_DIS, b == Lb - 1,
+                       cap, cfg, st));
+    VR_CHECK_HIP(hipEventRecord(side->walked[c], st));
   }
+  side_lock.unlock();
   k_kfinal<<<blocks_for(total, 256), 256, 0, st>>>(W.tot, cap, total, scores);
   VR_CHECK_LAUNCH();
   return VR_OK;
