@@ -97,6 +97,24 @@ def test_kendall_bootstrap_matches_oracle(dev, n, nb, levels):
     assert abs(lo - rlo) <= 1e-12 and abs(hi - rhi) <= 1e-12
 
 
+@pytest.mark.parametrize("quantize", ["model", "neural", "both"])
+def test_kendall_bootstrap_either_plan_as_y(dev, quantize):
+    # the plan with fewer distinct values is walked as y (fewer levels); each plan's tie total
+    # stays in its own field, so every score equals the oracle's whichever plan that is
+    x = O.synthetic_features(120, [300, 200], seed=7)
+    m_rdm, n_rdm = O.compute_rdm(x[0]), O.compute_rdm(x[1])
+    if quantize in ("model", "both"):
+        m_rdm = (np.floor(m_rdm * 6) / 6).astype(np.float32)
+    if quantize in ("neural", "both"):
+        n_rdm = (np.floor(n_rdm * 11) / 11).astype(np.float32)
+    point, scores, lo, hi = R.bootstrap_rsa(torch.from_numpy(m_rdm).to(dev), torch.from_numpy(n_rdm).to(dev),
+                                            n_bootstrap=70, seed=42, method="kendall")
+    rp, rs, rlo, rhi = O.bootstrap_rsa(m_rdm, n_rdm, n_bootstrap=70, seed=42, method="Kendall")
+    assert point == rp
+    assert np.array_equal(scores, rs)
+    assert lo == rlo and hi == rhi
+
+
 def test_kendall_bootstrap_end_to_end_tolerance(dev):
     n = 200
     feats = O.synthetic_features(n, [4096, 1000], seed=7, relu=[True, False], noise=3.0)

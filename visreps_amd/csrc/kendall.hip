@@ -565,6 +565,19 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
     VR_CHECK_LAUNCH();
     return VR_OK;
   }
+  // Discordance and the joint ties are symmetric in the two plans: the one with fewer distinct
+  // values plays y (its dense-rank bits are the levels walked), and each plan's tie total
+  // still lands in its own field (x = A's, y = B's), so k_kfinal's fp64 order is unchanged.
+  auto levels = [](uint32_t G) {
+    int L = 0;
+    while (L < 32 && ((G - 1u) >> L) != 0u) ++L;
+    return L;
+  };
+  const bool swap = levels(h[0].G) < levels(h[1].G);
+  const PlanView& PA = swap ? B : A;
+  const PlanView& PB = swap ? A : B;
+  const PlanHeader hx = swap ? h[1] : h[0], hy = swap ? h[0] : h[1];
+  const int fx = swap ? KF_YTIE : KF_XTIE, fy = swap ? KF_XTIE : KF_YTIE;
   const unsigned gbM = blocks_for(M, 256);
   const unsigned gbW = blocks_for(kwindows(M) * 64, 256);  // whole windows: ballots
   KSide* side = nullptr;
@@ -581,32 +594,32 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
   // B tie stream (B order: needs only the B plan) on the side stream, its own block summaries,
   // beside the x-lex order's construction below
   VR_CHECK_HIP(hipStreamWaitEvent(sp, side->masks, 0));
-  if (h[1].max_group > 1) {
+  if (hy.max_group > 1) {
     KendallWs Wy = W;
     Wy.w_acc = W.w2_acc, Wy.w_g = W.w2_g, Wy.w_a = W.w2_a, Wy.w_b = W.w2_b, Wy.w_incl = W.w2_incl;
-    k_border_flags<<<gbW, 256, 0, sp>>>(B.gflag, M, W.yb_start, W.yb_mem);
+    k_border_flags<<<gbW, 256, 0, sp>>>(PB.gflag, M, W.yb_start, W.yb_mem);
     VR_CHECK_LAUNCH();
-    VR_TRY(walk_stream(true, B.codes, W.yb_start, W.yb_mem, M, Wy, n, total, KF_YTIE, false, cap, cfg, sp));
+    VR_TRY(walk_stream(true, PB.codes, W.yb_start, W.yb_mem, M, Wy, n, total, fy, false, cap, cfg, sp));
   }
   // dense group ranks of both orders
-  VR_TRY(group_index(A, M, W, W.gidxA, st));
-  VR_TRY(group_index(B, M, W, W.gidxB, st));
+  VR_TRY(group_index(PA, M, W, W.gidxA, st));
+  VR_TRY(group_index(PB, M, W, W.gidxB, st));
   // (x, y)-lexicographic order: stable sort of B order by A group
-  k_kendall_keys<<<gbM, 256, 0, st>>>(B.codes, M, n, A.pos_map, W.gidxA, W.keys, W.vals);
+  k_kendall_keys<<<gbM, 256, 0, st>>>(PB.codes, M, n, PA.pos_map, W.gidxA, W.keys, W.vals);
   VR_CHECK_LAUNCH();
   VR_TRY(radix_sort_kv(W.keys, W.vals, W.keys_alt, W.vals_alt, M, W.radix, st));
-  k_kendall_elems<<<gbM, 256, 0, st>>>(W.vals, B.codes, W.gidxB, M, W.ecode[0], W.ey[0]);
+  k_kendall_elems<<<gbM, 256, 0, st>>>(W.vals, PB.codes, W.gidxB, M, W.ecode[0], W.ey[0]);
   VR_CHECK_LAUNCH();
   VR_CHECK_HIP(hipEventRecord(side->in, st));  // the level-0 stream exists: preparation may start
   // x-lex tie streams (only when A has multi-element groups)
-  if (h[0].max_group > 1) {
+  if (hx.max_group > 1) {
     k_xlex_flags<<<gbW, 256, 0, st>>>(W.keys, W.ey[0], M, W.xa_start, W.xa_mem, W.xj_start, W.xj_mem);
     VR_CHECK_LAUNCH();
-    VR_TRY(walk_stream(true, W.ecode[0], W.xa_start, W.xa_mem, M, W, n, total, KF_XTIE, false, cap, cfg, st));
+    VR_TRY(walk_stream(true, W.ecode[0], W.xa_start, W.xa_mem, M, W, n, total, fx, false, cap, cfg, st));
     VR_TRY(walk_stream(true, W.ecode[0], W.xj_start, W.xj_mem, M, W, n, total, KF_NTIE, false, cap, cfg, st));
   }
   // inversion levels, most significant y bit first
-  const uint32_t G = h[1].G;
+  const uint32_t G = hy.G;
   int Lb = 0;
   while (Lb < 32 && ((G - 1u) >> Lb) != 0u) ++Lb;
   // Level b walks stream c = (Lb - 1 - b) & 1 (ecode/ey[c], planes lv_*[c]) on the caller's
@@ -626,7 +639,7 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
       k_word_popc<<<blocks_for(words, 256), 256, 0, sp>>>(W.lv_bits[c], words, W.wcnt);
       VR_CHECK_LAUNCH();
       VR_TRY(scan_exclusive_u32(W.wcnt, W.wcnt, words, nullptr, W.scan, sp));
-      k_level_split<<<gbM, 256, 0, sp>>>(W.ecode[c], W.ey[c], W.lv_bits[c], W.wcnt, B.gstart, M, b,
+      k_level_split<<<gbM, 256, 0, sp>>>(W.ecode[c], W.ey[c], W.lv_bits[c], W.wcnt, PB.gstart, M, b,
                                          W.ecode[c ^ 1], W.ey[c ^ 1]);
       VR_CHECK_LAUNCH();
       k_level_flags<<<gbW, 256, 0, sp>>>(W.ey[c ^ 1], M, b - 1, W.lv_start[c ^ 1], W.lv_bits[c ^ 1]);
