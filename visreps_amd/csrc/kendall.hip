@@ -26,6 +26,7 @@
 // against it); per unit ~14 x M x 4 B of scratch.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <mutex>
 
 #include "kcount.h"
@@ -96,6 +97,10 @@ struct KendallWs {
   uint64_t* w2_a;
   uint32_t* w2_b;
   uint32_t* w2_incl;
+  uint64_t* w3[3];     // two more sets for the fused top-level walk's tie streams: acc, g, a
+  uint32_t* w3bi[2];   // b, incl
+  uint64_t* w4[3];
+  uint32_t* w4bi[2];
   uint64_t* tot;       // [KF_N][cap]
 };
 
@@ -134,6 +139,8 @@ static KendallWs kendall_layout(void* base, int64_t n, int64_t cap_sets, int nwa
   w.w2_a = c.take<uint64_t>(wsum);
   w.w2_b = c.take<uint32_t>(wsum);
   w.w2_incl = c.take<uint32_t>(wsum);
+  for (int i = 0; i < 3; ++i) w.w3[i] = c.take<uint64_t>(wsum), w.w4[i] = c.take<uint64_t>(wsum);
+  for (int i = 0; i < 2; ++i) w.w3bi[i] = c.take<uint32_t>(wsum), w.w4bi[i] = c.take<uint32_t>(wsum);
   w.tot = c.take<uint64_t>((size_t)KF_N * (size_t)std::max<int64_t>(cap_sets, 1));
   if (bytes) *bytes = c.bytes();
   return w;
@@ -393,6 +400,94 @@ __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
   w_incl[o] = inc;
 }
 
+// The top inversion level fused with the two x-lex tie streams (A ties, joint ties): the same
+// pair codes (the x-lex order), so one walk shares the code loads, mask lookups and
+// transposes; three segment states, three block summaries (one k_kfix each).
+struct KOut {
+  uint64_t *acc, *g, *a;
+  uint32_t *b, *incl;
+};
+__device__ inline void kw_block_summary(const KSeg& a, bool seen, uint32_t incl, const KOut& o, uint64_t* s_acc,
+                                        uint64_t* s_zl, uint32_t* s_c, uint32_t* s_inc, uint32_t* s_seen) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();  // the arrays' previous use is done
+  s_acc[wv * LANES + lane] = a.acc;
+  s_zl[wv * LANES + lane] = a.zlead;
+  s_c[wv * LANES + lane] = a.c;
+  s_seen[wv * LANES + lane] = seen ? 1u : 0u;
+  s_inc[wv * LANES + lane] = incl;
+  __syncthreads();
+  if (wv == 0) {
+    KSum S = ksum_identity();
+    uint32_t inc = 0;
+    for (int w = 0; w < KW_WAVES; ++w) {
+      ksum_push(S, s_acc[w * LANES + lane], s_zl[w * LANES + lane], s_c[w * LANES + lane],
+                s_seen[w * LANES + lane] == 0u);
+      inc += s_inc[w * LANES + lane];
+    }
+    const size_t off = (size_t)blockIdx.x * LANES + lane;
+    o.acc[off] = S.s;
+    o.g[off] = S.g;
+    o.a[off] = S.a;
+    o.b[off] = S.b;
+    o.incl[off] = inc;
+  }
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk_top3(
+    const uint32_t* __restrict__ codes, const uint32_t* __restrict__ s0, const uint32_t* __restrict__ x0p,
+    const uint32_t* __restrict__ s1, const uint32_t* __restrict__ x1p, const uint32_t* __restrict__ s2,
+    const uint32_t* __restrict__ x2p, int64_t M, const uint64_t* __restrict__ gmask, int64_t n, int nl,
+    uint32_t nwaves, KOut o0, KOut o1, KOut o2) {
+  extern __shared__ uint64_t smask[];
+  const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
+  const int lane = threadIdx.x & 63;
+  const bool active = lane < nl;
+  const uint32_t wave = wave_uniform(blockIdx.x * KW_WAVES + (threadIdx.x >> 6));
+  const uint64_t nwin = (uint64_t)kwindows(M);
+  const uint32_t wb = (uint32_t)(nwin * wave / nwaves), we = (uint32_t)(nwin * (wave + 1) / nwaves);
+  KSeg a0{0ull, 0u, 0u}, a1{0ull, 0u, 0u}, a2{0ull, 0u, 0u};
+  bool seen0 = false, seen1 = false, seen2 = false;
+  uint32_t incl = 0;
+  auto code_at = [&](uint32_t win) -> uint32_t {
+    const uint32_t q = win * 64u + (uint32_t)lane;
+    return q < (uint64_t)M ? codes[q] : 0u;
+  };
+  auto bits_of = [&](uint32_t cd, uint32_t win) -> uint64_t {
+    const uint32_t pos = win * 64u + (uint32_t)lane;
+    const uint64_t mb = pos < (uint64_t)M ? (m[cd >> 16] & m[cd & 0xffffu]) : 0ull;
+    const uint64_t x = transpose64<VR_XPOSE_K>(mb, lane);
+    return active ? x : 0ull;
+  };
+  auto plane = [&](const uint32_t* f, uint32_t win) -> uint64_t {
+    return ((uint64_t)sload(f + 2 * win + 1) << 32) | sload(f + 2 * win);
+  };
+  uint32_t cd = 0;
+  if (wb < we) cd = code_at(wb);
+  for (uint32_t win = wb; win < we; ++win) {
+    const uint32_t d = cd;
+    if (win + 1 < we) cd = code_at(win + 1);  // next window's code, one ahead
+    const uint64_t x = bits_of(d, win);
+    incl += popc64(x);
+    {  // the level: ones = bit set, zeros = bit clear
+      const uint64_t X = plane(x0p, win);
+      kseg_window<false>(x & X, x & ~X, plane(s0, win), a0, seen0);
+    }
+    {  // the tie streams: included members of multi-element groups
+      const uint64_t t1 = x & plane(x1p, win);
+      kseg_window<true>(t1, t1, plane(s1, win), a1, seen1);
+      const uint64_t t2 = x & plane(x2p, win);
+      kseg_window<true>(t2, t2, plane(s2, win), a2, seen2);
+    }
+  }
+  __shared__ uint64_t s_acc[KW_WAVES * LANES], s_zl[KW_WAVES * LANES];
+  __shared__ uint32_t s_c[KW_WAVES * LANES], s_inc[KW_WAVES * LANES], s_seen[KW_WAVES * LANES];
+  kw_block_summary(a0, seen0, incl, o0, s_acc, s_zl, s_c, s_inc, s_seen);
+  kw_block_summary(a1, seen1, incl, o1, s_acc, s_zl, s_c, s_inc, s_seen);
+  kw_block_summary(a2, seen2, incl, o2, s_acc, s_zl, s_c, s_inc, s_seen);
+}
+
 // Stream total per lane: the block summaries (k_kwalk) composed in block order with carry 0
 // into the first, added into tot[field][set0 + lane]; optionally the included-pair count into
 // tot[KF_INCL]. One block per pass (set0 = 64 x pass), all passes of a stream in one launch;
@@ -481,6 +576,8 @@ static int set_kwalk_attr() {
                                      hipFuncAttributeMaxDynamicSharedMemorySize, mx));
     VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk<LDS, true>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, mx));
+    VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk_top3<LDS>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, mx));
     done = true;
   }
   return VR_OK;
@@ -508,6 +605,42 @@ static int walk_stream(bool tie, const uint32_t* codes, const uint32_t* sflag, c
   k_kfix<<<(unsigned)npass, KW_THREADS, 0, st>>>(W.w_acc, W.w_g, W.w_a, W.w_b, W.w_incl, (uint32_t)cfg.grid,
                                                  total, field, add_incl ? 1 : 0, W.tot, cap);
   VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+// the fused top level + x-lex tie streams against every pass: totals into tot[KF_DIS] (with the
+// included-pair count), tot[fa] (A ties) and tot[KF_NTIE]
+static int walk_top3(const uint32_t* codes, const uint32_t* lvs, const uint32_t* lvb, const KendallWs& W,
+                     int64_t M, int64_t n, int64_t total, int fa, int64_t cap, const KCfg& cfg, hipStream_t st) {
+  if (cfg.use_lds) VR_TRY(set_kwalk_attr<true>());
+  const KOut o0{W.w_acc, W.w_g, W.w_a, W.w_b, W.w_incl};
+  const KOut o1{W.w3[0], W.w3[1], W.w3[2], W.w3bi[0], W.w3bi[1]};
+  const KOut o2{W.w4[0], W.w4[1], W.w4[2], W.w4bi[0], W.w4bi[1]};
+  auto shift = [&](KOut o, size_t d) { return KOut{o.acc + d, o.g + d, o.a + d, o.b + d, o.incl + d}; };
+  int64_t npass = 0;
+  for (int64_t set0 = 0; set0 < total; set0 += LANES, ++npass) {
+    const int nl = (int)std::min<int64_t>(LANES, total - set0);
+    const size_t d = (size_t)npass * (size_t)cfg.grid * LANES;
+    // bytes: the pair code + six bit planes, in the 4.25-B-per-walk units of k_kwalk
+    KtScope kt(KT_KWALK, (double)M * (4.75 / 4.25), st);
+    const uint64_t* mk = W.masks + (size_t)npass * (size_t)n;
+    if (cfg.use_lds)
+      k_kwalk_top3<true><<<cfg.grid, KW_THREADS, cfg.lds, st>>>(codes, lvs, lvb, W.xa_start, W.xa_mem, W.xj_start,
+                                                               W.xj_mem, M, mk, n, nl, (uint32_t)cfg.nwaves,
+                                                               shift(o0, d), shift(o1, d), shift(o2, d));
+    else
+      k_kwalk_top3<false><<<cfg.grid, KW_THREADS, 0, st>>>(codes, lvs, lvb, W.xa_start, W.xa_mem, W.xj_start,
+                                                          W.xj_mem, M, mk, n, nl, (uint32_t)cfg.nwaves,
+                                                          shift(o0, d), shift(o1, d), shift(o2, d));
+    VR_CHECK_LAUNCH();
+  }
+  const KOut outs[3] = {o0, o1, o2};
+  const int fields[3] = {KF_DIS, fa, KF_NTIE};
+  for (int i = 0; i < 3; ++i) {
+    k_kfix<<<(unsigned)npass, KW_THREADS, 0, st>>>(outs[i].acc, outs[i].g, outs[i].a, outs[i].b, outs[i].incl,
+                                                   (uint32_t)cfg.grid, total, fields[i], i == 0 ? 1 : 0, W.tot, cap);
+    VR_CHECK_LAUNCH();
+  }
   return VR_OK;
 }
 
@@ -612,11 +745,16 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
   VR_CHECK_LAUNCH();
   VR_CHECK_HIP(hipEventRecord(side->in, st));  // the level-0 stream exists: preparation may start
   // x-lex tie streams (only when A has multi-element groups)
-  if (hx.max_group > 1) {
+  // (fused into the top level's walk below unless VISREPS_KENDALL_TOP3=0)
+  static const bool top3 = !(getenv("VISREPS_KENDALL_TOP3") && atoi(getenv("VISREPS_KENDALL_TOP3")) == 0);
+  const bool xties = hx.max_group > 1;
+  if (xties) {
     k_xlex_flags<<<gbW, 256, 0, st>>>(W.keys, W.ey[0], M, W.xa_start, W.xa_mem, W.xj_start, W.xj_mem);
     VR_CHECK_LAUNCH();
-    VR_TRY(walk_stream(true, W.ecode[0], W.xa_start, W.xa_mem, M, W, n, total, fx, false, cap, cfg, st));
-    VR_TRY(walk_stream(true, W.ecode[0], W.xj_start, W.xj_mem, M, W, n, total, KF_NTIE, false, cap, cfg, st));
+    if (!top3) {
+      VR_TRY(walk_stream(true, W.ecode[0], W.xa_start, W.xa_mem, M, W, n, total, fx, false, cap, cfg, st));
+      VR_TRY(walk_stream(true, W.ecode[0], W.xj_start, W.xj_mem, M, W, n, total, KF_NTIE, false, cap, cfg, st));
+    }
   }
   // inversion levels, most significant y bit first
   const uint32_t G = hy.G;
@@ -647,8 +785,11 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
       VR_CHECK_HIP(hipEventRecord(side->prep[c ^ 1], sp));
     }
     VR_CHECK_HIP(hipStreamWaitEvent(st, side->prep[c], 0));
-    VR_TRY(walk_stream(false, W.ecode[c], W.lv_start[c], W.lv_bits[c], M, W, n, total, KF_DIS, b == Lb - 1,
-                       cap, cfg, st));
+    if (b == Lb - 1 && xties && top3)  // level 0's stream is the x-lex order the tie streams walk
+      VR_TRY(walk_top3(W.ecode[c], W.lv_start[c], W.lv_bits[c], W, M, n, total, fx, cap, cfg, st));
+    else
+      VR_TRY(walk_stream(false, W.ecode[c], W.lv_start[c], W.lv_bits[c], M, W, n, total, KF_DIS, b == Lb - 1,
+                         cap, cfg, st));
     VR_CHECK_HIP(hipEventRecord(side->walked[c], st));
   }
   side_lock.unlock();
