@@ -202,14 +202,15 @@ def bench(dev):
     model = CustomCNN(num_classes=1000).to(dev).eval()
     ex = FeatureExtractor(model, LAYERS, extract_pre_and_post=True)
     images = make_images(range(N), device=dev)
-    y = make_responses(images, range(N), {"V1": NSD_ROIS_4["V1"]})["V1"]
+    ys = make_responses(images, range(N), NSD_ROIS_4)  # the bench's 4 regions (V1 first)
+    y = ys["V1"]
     feats = extract(ex, images, 128)
     del images
     neural_split = R.compute_rdm(y)
     neural_64 = rdm_f64(y)
     with gram_mode("fp32"):
         neural_32 = R.compute_rdm(y)
-    return feats, neural_split, neural_64, neural_32, y
+    return feats, neural_split, neural_64, neural_32, y, ys
 
 
 POINTS = [f"{l}_{s}" for l in ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1", "fc2"]
@@ -277,6 +278,67 @@ def test_bench_point_vs_cpu_oracle(dev, bench, point):
                   est_reruns=reruns, est_tail_flags=tail)
     assert tail == 0, "B-side invariant broken on the bench's own RDMs"
     assert dp < SPEARMAN_TOL and db < SPEARMAN_TOL and dl < SPEARMAN_TOL, (point, dp, db, dl)
+
+
+GRID_POINTS = ["conv1_pre", "conv5_post", "fc1_post"]
+
+
+def test_bench_grid_walk_full_size(dev, bench, idx):
+    """the region-fused grid walk (k_rankB_grid, the bench's dominant kernel)
+    at the bench's own size -- N = 10k, the 4 regions' neural RDMs, 1000 RandomState(42)
+    bootstraps, model plans conv1_pre / conv5_post / fc1_post:
+      * all 4 x 3 x 1001 scores bit-equal to one joined per-region multi call per region;
+      * the conv5_post x V1 unit's point, first 5 draws and draws #64/#65/#500/#1000 vs the
+        CPU oracle (numpy RDMs + scipy spearmanr, evals.py:341-373);
+      * pipeline.all_units_rsa (the bench's route into the grid) equal to per-unit
+        bootstrap_rsa for two units, every score and both percentiles."""
+    from visreps_amd._lib import ktimer_enable, ktimer_read, lib
+    from visreps_amd.pipeline import all_units_rsa
+
+    feats, ys = bench[0], bench[5]
+    regions = list(ys)
+    rdms_n = {r: R.compute_rdm(ys[r]) for r in regions}
+    pns = [R.RankPlan(rdms_n[r]) for r in regions]
+    pms = [R.RankPlan(R.compute_rdm(feats[p])) for p in GRID_POINTS]
+    sj = R.SharedJoins(pns)
+    joins = [sj.join(pm) for pm in pms]  # joins[m][a]
+    del sj
+    r0, t0 = int(lib().vr_engine_est_reruns()), int(lib().vr_engine_est_tail_flags())
+    ktimer_enable(True)
+    grid = R.bootstrap_spearman_grid(pns, pms, idx, joins, full_first=True).cpu().numpy()
+    launches = ktimer_read("k_rankB_grid")[1]
+    ktimer_enable(False)
+    assert int(lib().vr_engine_est_reruns()) == r0 and int(lib().vr_engine_est_tail_flags()) == t0
+    assert launches == (NB + 1 + 63) // 64 * len(GRID_POINTS) - len(GRID_POINTS), launches  # pass 0: its own slot
+    assert grid.shape == (len(regions), len(GRID_POINTS), NB + 1) and np.all(np.isfinite(grid))
+    n_equal = 0
+    for a, pn in enumerate(pns):
+        ref = R.bootstrap_spearman_multi(pn, pms, idx, full_first=True,
+                                         joined=[joins[m][a] for m in range(len(pms))]).cpu().numpy()
+        assert np.array_equal(grid[a], ref), regions[a]
+        n_equal += ref.size
+    del joins
+    u = grid[regions.index("V1"), GRID_POINTS.index("conv5_post")]
+    point_o, boot5_o, late_o = _oracle_results(bench)["conv5_post"].result()
+    dp = abs(float(u[0]) - point_o)
+    db = float(np.max(np.abs(u[1:6] - boot5_o)))
+    dl = max(abs(float(u[1 + i]) - late_o[i]) for i in LATE_DRAWS)
+    # the bench's route: all_units_rsa over the 4 regions runs them as one grid call
+    ktimer_enable(True)
+    res = all_units_rsa(lambda p: R.compute_rdm(feats[p]), GRID_POINTS, rdms_n, N, n_boot=NB, seed=42)
+    routed = ktimer_read("k_rankB_grid")[1]
+    ktimer_enable(False)
+    assert routed == launches, "all_units_rsa did not take the grid walk"
+    for p, r in [("conv5_post", "V1"), ("fc1_post", "hV4")]:
+        point, scores, lo, hi = R.bootstrap_rsa(R.compute_rdm(feats[p]), rdms_n[r], n_bootstrap=NB, seed=42)
+        v = res[(p, r)]
+        assert v["score"] == point and v["ci_low"] == lo and v["ci_high"] == hi, (p, r)
+        assert np.array_equal(np.asarray(v["bootstrap_scores"]), scores), (p, r)
+        assert np.array_equal(grid[regions.index(r), GRID_POINTS.index(p)][1:], scores), (p, r)
+    record_margin("bench_grid_full_size", n=N, regions=len(regions), model_plans=len(GRID_POINTS),
+                  scores_bit_equal_per_region=n_equal, grid_launches=launches, dspearman_point=dp,
+                  dspearman_boot5=db, dspearman_late_draws=dl, late_draws=LATE_DRAWS)
+    assert dp < SPEARMAN_TOL and db < SPEARMAN_TOL and dl < SPEARMAN_TOL, (dp, db, dl)
 
 
 class _engine_form:

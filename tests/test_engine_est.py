@@ -326,3 +326,127 @@ def test_grid_falls_back_on_a_structured_region(dev):
     for a, pn in enumerate(neurals):
         ref = R.bootstrap_spearman_multi(pn, models, idx, full_first=True).cpu().numpy()
         assert np.array_equal(got[a], ref)
+
+
+def test_grid_l2_masks_equal_per_region_calls(dev, monkeypatch):
+    # the grid walk's L2-mask form (what n > 20,352 takes; VISREPS_ENGINE_GRID_LDS=0 forces it
+    # here) against the per-region calls, with ties in a quantised model RDM
+    from visreps_amd._lib import ktimer_enable, ktimer_read
+
+    monkeypatch.setenv("VISREPS_ENGINE_GRID_LDS", "0")
+    n = 1800
+    neurals = [R.RankPlan(_rdm(dev, n, 90 + 10 * i, 80 + i)) for i in range(3)]
+    q = (_rdm(dev, n, 40, 87) * 64).floor() / 64
+    models = [R.RankPlan(_rdm(dev, n, 70, 88, relu=True)), R.RankPlan(q)]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 130)
+    sj = R.SharedJoins(neurals)
+    joins = [sj.join(pm) for pm in models]
+    ktimer_enable(True)
+    got = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    assert ktimer_read("k_rankB_grid")[1] > 0, "the fused walk did not run"
+    ktimer_enable(False)
+    for a, pn in enumerate(neurals):
+        ref = R.bootstrap_spearman_multi(pn, models, idx, full_first=True,
+                                         joined=[joins[m][a] for m in range(len(models))]).cpu().numpy()
+        assert np.array_equal(got[a], ref)
+
+
+@pytest.mark.parametrize("inject", [0, 2])
+def test_grid_flagged_region_reruns_alone(dev, inject):
+    # a B-side error injected into the first fused region after its A walk of pass
+    # `inject` (pass 0 is checked at once, pass 2 at the end): the tail invariants flag it, that
+    # region runs again on its own (re-running the flagged pass exact), the other two stay
+    # fused, and every score equals the clean per-region calls
+    from visreps_amd._lib import ktimer_enable, ktimer_read
+
+    n = 1800
+    neurals = [R.RankPlan(_rdm(dev, n, 90 + 10 * i, 100 + i)) for i in range(3)]
+    models = [R.RankPlan(_rdm(dev, n, 70, 110, relu=True)), R.RankPlan(_rdm(dev, n, 150, 111))]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 130)  # 131 subsets: 3 passes
+    sj = R.SharedJoins(neurals)
+    joins = [sj.join(pm) for pm in models]
+    clean = [R.bootstrap_spearman_multi(pn, models, idx, full_first=True,
+                                        joined=[joins[m][a] for m in range(len(models))]).cpu().numpy()
+             for a, pn in enumerate(neurals)]
+    r0, t0 = int(lib().vr_engine_est_reruns()), int(lib().vr_engine_est_tail_flags())
+    lib().vr_test_engine_inject(inject)
+    ktimer_enable(True)
+    try:
+        got = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    finally:
+        lib().vr_test_engine_inject(-1)
+    grid_launches = ktimer_read("k_rankB_grid")[1]
+    ktimer_enable(False)
+    assert int(lib().vr_engine_est_reruns()) - r0 >= 1, "the injected error must flag a pass"
+    assert int(lib().vr_engine_est_tail_flags()) - t0 >= 1
+    assert grid_launches == 2 * len(models), "passes 1-2 stay fused for the other regions"
+    for a in range(len(neurals)):
+        assert np.array_equal(got[a], clean[a]), a
+
+
+def test_grid_structured_region_leaves_the_others_fused(dev):
+    # one region failing the up-front check runs on its own; the other two
+    # still walk each model plan once per pass together
+    from visreps_amd._lib import ktimer_enable, ktimer_read
+
+    n = 5000  # test_structured_rdm_goes_exact_up_front's RDM, which fails the check
+    g = torch.Generator(device=dev).manual_seed(7)
+    u = torch.empty(n, device=dev).exponential_(1.0, generator=g) ** 2
+    s = u[:, None] + u[None, :] + 0.05 * torch.rand(n, n, device=dev, generator=g)
+    s = torch.triu(s, 1)
+    s = s + s.T
+    neurals = [R.RankPlan(_rdm(dev, n, 80, 96)), R.RankPlan(s), R.RankPlan(_rdm(dev, n, 90, 97))]
+    del s
+    models = [R.RankPlan(_rdm(dev, n, 60, 98)), R.RankPlan(_rdm(dev, n, 60, 99, relu=True))]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 100)
+    sj = R.SharedJoins(neurals)
+    joins = [sj.join(pm) for pm in models]
+    p0 = int(lib().vr_engine_est_predicted())
+    ktimer_enable(True)
+    got = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    grid_launches = ktimer_read("k_rankB_grid")[1]
+    ktimer_enable(False)
+    assert grid_launches == 1 * len(models), "the two continuous regions stay fused (pass 1)"
+    assert int(lib().vr_engine_est_predicted()) - p0 == 1, "the structured region goes exact up front"
+    for a, pn in enumerate(neurals):
+        ref = R.bootstrap_spearman_multi(pn, models, idx, full_first=True).cpu().numpy()
+        assert np.array_equal(got[a], ref)
+
+
+@pytest.mark.parametrize("n", [12000, 20500])
+def test_large_n_engine_forms(dev, n):
+    # n above the two-workgroup LDS mask limit (10,176). 12,000 keeps the
+    # grid walk's masks in LDS (one workgroup per CU), 20,500 reads them from L2; the A walks
+    # and the per-region B walks read L2 masks at both. 127 draws (2 passes). The grid call,
+    # the per-region EST calls and the exact form agree bit for bit; the point and draw #100
+    # of one unit equal the CPU oracle (scipy spearmanr on the sub-RDMs).
+    from visreps_amd._lib import ktimer_enable, ktimer_read
+
+    nb = 127
+    neurals = [R.RankPlan(_rdm(dev, n, 64 + 16 * i, 120 + i)) for i in range(2)]
+    m_rdm = _rdm(dev, n, 96, 130, relu=True)
+    models = [R.RankPlan(m_rdm), R.RankPlan(_rdm(dev, n, 48, 131))]
+    idx = bootstrap_indices(42, n, int(0.9 * n), nb)
+    sj = R.SharedJoins(neurals)
+    joins = [sj.join(pm) for pm in models]
+    del sj
+    ktimer_enable(True)
+    grid = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    assert ktimer_read("k_rankB_grid")[1] == len(models), "pass 1 fused"
+    ktimer_enable(False)
+    del joins
+    per = [R.bootstrap_spearman_multi(pn, models, idx, full_first=True).cpu().numpy() for pn in neurals]
+    with exact_engine():
+        ex = R.bootstrap_spearman(models[0], neurals[0], idx, full_first=True).cpu().numpy()
+    for a in range(2):
+        assert np.array_equal(grid[a], per[a]), a
+    assert np.array_equal(per[0][0], ex)
+    if n > 15000:  # (scipy on 2e8 pairs takes minutes of host time: the oracle runs at 12,000)
+        return
+    # the oracle on the same fp32 RDMs (point and draw #100: subsets of 0.9 n stimuli)
+    a_np = m_rdm.cpu().numpy()
+    b_np = _rdm(dev, n, 64, 120).cpu().numpy()
+    assert abs(float(per[0][0][0]) - O.compute_rdm_correlation(a_np, b_np, "Spearman")) <= 1e-12
+    i = np.asarray(idx[99])
+    ref = O.compute_rdm_correlation(a_np[np.ix_(i, i)], b_np[np.ix_(i, i)], "Spearman")
+    assert abs(float(per[0][0][100]) - ref) <= 1e-12

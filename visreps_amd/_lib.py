@@ -278,6 +278,11 @@ class _WorkspacePool:
             self._bufs[key] = buf
         return buf
 
+    def current(self, device: torch.device, tag: str = "ws") -> int:
+        """Bytes of the (device, tag) buffer held now (0 if none)."""
+        buf = self._bufs.get((str(device), tag))
+        return 0 if buf is None else int(buf.numel())
+
     def release(self, tag: str | None = None) -> None:
         if tag is None:
             self._bufs.clear()

@@ -81,3 +81,13 @@ __device__ inline uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {
     int rc_ = (expr);         \
     if (rc_ != VR_OK) return rc_; \
   } while (0)
+
+// One-time setup (hipFuncSetAttribute of a kernel instantiation) run exactly once per
+// process even when host threads enter together: a function-local static is initialised
+// once under the C++11 guarantee, so the library stays thread-safe across distinct streams
+// (SURVEY §8(b)). Every later call returns the first call's status.
+#define VR_ONCE(...)                                                         \
+  do {                                                                       \
+    static const int once_rc_ = [&]() -> int { __VA_ARGS__; return VR_OK; }();\
+    if (once_rc_ != VR_OK) return once_rc_;                                  \
+  } while (0)

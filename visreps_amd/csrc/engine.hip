@@ -29,6 +29,7 @@
 //            S = sum of included yA; segment sums S y'_B, S, tie terms (segment-relative)
 //  k_tail_part + k_tail_top   all units of a pass at once: blockwise prefix products combine
 //            the segments -> rho per lane
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -223,7 +224,11 @@ enum { QS_RANKA = 0, QS_RANKB = 1 };  // queue slots of an EST pass's launches
 
 constexpr int EST_MAX_PASSES = 512;  // passes between two checks of the EST flags
 
-static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t* bytes, int64_t units = 1) {
+// slim: a grid call's region 1.. workspace (run_engine_grid): EST passes only, so the TB is
+// u16 and there are no join arrays (the units arrive joined; flagged or exact-form work of
+// any region runs on region 0's full workspace)
+static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t* bytes, int64_t units = 1,
+                              bool slim = false) {
   const int64_t M = pairs_of(n);
   const size_t nch = plan_nchunks(M);
   // A-side segment partials: up to VR_SEGS_PER_WAVE per wave (EST); B-side: one per wave
@@ -236,9 +241,12 @@ static EngineWs engine_layout(void* base, int64_t n, int lw, int nwaves, size_t*
   e.ftab = c.take<uint2>((size_t)EST_NC * LANES);
   e.viol = c.take<uint32_t>((size_t)EST_MAX_PASSES + 1);  // + the exact form's invariant flag
   e.masks = c.take<uint64_t>((size_t)n);
-  e.posA_byB = c.take<uint32_t>((size_t)M);
-  e.chunkA_byB = c.take<uint32_t>((size_t)M);
-  e.TB = c.take<uint32_t>((size_t)M * (size_t)lw);  // sized for u32
+  e.posA_byB = slim ? nullptr : c.take<uint32_t>((size_t)M);
+  e.chunkA_byB = slim ? nullptr : c.take<uint32_t>((size_t)M);
+  if (slim)
+    e.TB = c.take<uint16_t>((size_t)M * (size_t)lw);
+  else
+    e.TB = c.take<uint32_t>((size_t)M * (size_t)lw);  // sized for u32 (exact form, wide chunk ranks)
   e.lpA = c.take<uint32_t>(nch * LANES);
   e.baseA = c.take<uint32_t>(nch * LANES);
   e.segA_tot = c.take<uint32_t>(nsegmax * LANES);
@@ -1342,6 +1350,9 @@ __device__ inline void gather_window(const TBT* __restrict__ TB, const uint32_t*
 #if VR_PROBE_WT
 __device__ uint64_t g_wt[2 * 16384];
 #endif
+#ifndef VR_XW_L2
+#define VR_XW_L2 0  // 1: the prefetching walk also with masks from L2 (n > 10,176)
+#endif
 #ifndef VR_XWIN
 #define VR_XWIN 1  // EST 3 / 4 B walk: next window's streams and masks fetched inside the window (0: off)
 #endif
@@ -1420,9 +1431,10 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       // EST 3 / 4 (small tie groups): the prefetching walk, which computes the window low
       // ends from the A positions (a join's streamed low ends, VISREPS_ENGINE_LO_JOIN=1, hold
       // the same values and are not read)
-      // (masks in LDS only: with masks from L2 -- n > 10,176 -- the per-window walk below
-      // serves; the prefetching form's L2-mask path faulted when a round-5 test first ran it)
-      constexpr bool XW = VR_XWIN && EST == 3 && !BIGT && LDS;
+      // (masks in LDS only unless VR_XW_L2: with masks from L2 -- n > 10,176 -- the per-window
+      // walk below serves; the prefetching form's L2-mask path faulted when a round-5 test
+      // first ran it)
+      constexpr bool XW = VR_XWIN && EST == 3 && !BIGT && (LDS || VR_XW_L2);
       constexpr bool walked = XW;
       if constexpr (XW) {
         static_assert(EBB == 8, "prefetching batches are 8 pairs");
@@ -1705,7 +1717,9 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
 // its own TB row gather, window low end and sums. The regions' TB tables (one A walk each)
 // are resident together. Same exact integer sums as k_rankB EST 3 (the segment partials go
 // to each region's workspace, unit j), so the scores are bit-identical to the per-region
-// calls. Masks in LDS, tie groups < 2^16 (the caller checks).
+// calls. Tie groups < 2^16 (the caller checks). The launch runs one 16-wave workgroup per
+// CU, so the masks (8 B per stimulus) sit in LDS up to n = 20,352 (LDS = true); larger n
+// read them from L2 (LDS = false: two 8-B plain loads per window lane, compiler-counted).
 // ---------------------------------------------------------------------------------
 struct GridB {
   const uint16_t* TB[4];     // each region's TB (EST: absolute doubled ranks mod 2^16)
@@ -1725,7 +1739,7 @@ struct GridB {
 #ifndef VR_GRID_MINW
 #define VR_GRID_MINW 4  // waves per SIMD the grid walk is compiled for (4: 128 VGPRs)
 #endif
-template <int R>
+template <int R, bool LDS>
 __global__ __launch_bounds__(ENG_THREADS, VR_GRID_MINW) void k_rankB_grid(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gflag, const uint64_t* __restrict__ gmask,
     int64_t n, GridB g, uint32_t nseg, const uint2* __restrict__ ftab, const uint32_t* __restrict__ segpos,
@@ -1733,7 +1747,7 @@ __global__ __launch_bounds__(ENG_THREADS, VR_GRID_MINW) void k_rankB_grid(
   constexpr int NB = VR_GRID_NB;
   static_assert(64 % NB == 0, "batch");
   extern __shared__ uint64_t smask[];
-  const uint64_t* m = stage_masks<true>(gmask, n, smask);
+  const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
   const uint32_t Lu = wave_uniform(sload(&ftab->x)), Ru = wave_uniform(sload(&ftab->y));
   const int lane = threadIdx.x & 63;
   const uint32_t lane_off = (uint32_t)lane;
@@ -2140,11 +2154,7 @@ static int allow_big_lds(K kernel) {
 template <bool LDS, bool FULL, typename TBT, bool BTA>
 static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const EngineCfg& cfg,
                   hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    VR_TRY(allow_big_lds(k_rankA<LDS, FULL, TBT, BTA, false>));
-    attr = true;
-  }
+  VR_ONCE(VR_TRY(allow_big_lds(k_rankA<LDS, FULL, TBT, BTA, false>)));
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = (uint32_t)cfg.nwaves;
@@ -2168,12 +2178,7 @@ static int pass_a(const PlanView& A, int64_t n, const EngineWs& E, int lw, const
 template <int EM, bool CL, bool FULL, bool BTA>
 static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, int nl, const EngineCfg& cfg,
                       uint2 e3, uint2 tri, uint32_t* viol, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    VR_TRY(allow_big_lds(k_countA<CL, FULL>));
-    VR_TRY(allow_big_lds(k_rankA<CL, FULL, uint16_t, BTA, EM>));
-    attr = true;
-  }
+  VR_ONCE(VR_TRY(allow_big_lds(k_countA<CL, FULL>)); VR_TRY(allow_big_lds(k_rankA<CL, FULL, uint16_t, BTA, EM>)));
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = cfg.est_nsegA;
@@ -2212,11 +2217,7 @@ static int pass_a_est(const PlanView& A, int64_t n, const EngineWs& E, int lw, i
 template <bool CL, bool FULL>
 static int est_predict(const PlanView& A, int64_t n, const EngineWs& E, int lw, int nl, bool full0,
                        const EngineCfg& cfg, uint2 e3, hipStream_t st, bool& bad) {
-  static bool attr = false;
-  if (!attr) {
-    VR_TRY(allow_big_lds(k_countA<CL, FULL>));
-    attr = true;
-  }
+  VR_ONCE(VR_TRY(allow_big_lds(k_countA<CL, FULL>)));
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = cfg.est_nsegA;
@@ -2246,11 +2247,7 @@ static int est_predict(const PlanView& A, int64_t n, const EngineWs& E, int lw, 
 template <bool LDS, bool FULL, typename TBT, bool BTB, int EST>
 static int walk_b(const PlanView& B, const uint32_t* posA_byB, const uint32_t* chunkA_byB, int64_t n,
                   const EngineWs& E, int lw, int64_t u, const EngineCfg& cfg, hipStream_t st, int kt_slot = -1) {
-  static bool attr = false;
-  if (!attr) {
-    VR_TRY(allow_big_lds(k_rankB<LDS, FULL, TBT, BTB, EST>));
-    attr = true;
-  }
+  VR_ONCE(VR_TRY(allow_big_lds(k_rankB<LDS, FULL, TBT, BTB, EST>)));
   const int64_t M = pairs_of(n);
   const uint32_t nch = plan_nchunks(M);
   const uint32_t nseg = EST ? cfg.est_nseg : (uint32_t)cfg.nwaves;
@@ -2575,39 +2572,71 @@ static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, i
 }
 
 // R A plans (regions) x nb B plans (model layers), every unit pre-joined (joins[r][2 j] =
-// unit (j, r)'s A positions): scores of unit (j, r) at scores + (r nb + j) score_ld. The
-// EST passes run region-fused (k_rankB_grid: one B walk per B plan for all regions) when
-// the happy path holds -- EST 3 with its 4 form for the full set, masks in LDS, tie groups
-// < 2^16, every region's estimate passing its up-front check and every pass its flags;
-// otherwise (and for any region whose pass is flagged) each region runs as its own
-// run_engine_multi call, which re-runs flagged passes in the exact form. Es[r]: region r's
-// workspace (multi_layout, prejoined), which keeps its own TB beside the others'.
+// unit (j, r)'s A positions; joins[r][2 j + 1] = region 0's second arrays): scores of unit
+// (j, r) at scores + (r nb + j) score_ld. The EST passes run region-fused (k_rankB_grid: one
+// B walk per B plan for all fused regions) on the happy path -- EST 3 with its 4 form for
+// the full set, B tie groups < 2^16 -- for every region with A tie groups < 2^16 whose
+// estimate passes its up-front check; a region failing that, or one whose pass is later
+// flagged, leaves the fused set and runs on its own once the fused passes are done (EST with
+// exact re-runs of its flagged passes, or the exact form), so the other regions stay fused.
+// Es[0]: region 0's full workspace (multi_layout, prejoined), which also holds the shared
+// masks and B segment tables and serves every region run on its own; Es[1..]: slim
+// workspaces (u16 TB, no join arrays) beside it.
+template <bool LDS>
+static int launch_grid(int R, unsigned grid, size_t lds, const PlanView& B, const uint64_t* masks, int64_t n,
+                       const GridB& g, uint32_t ns, const uint2* ftab, const uint32_t* segpos, uint32_t* q,
+                       hipStream_t st) {
+  VR_ONCE(VR_TRY(allow_big_lds(k_rankB_grid<2, LDS>)); VR_TRY(allow_big_lds(k_rankB_grid<3, LDS>));
+          VR_TRY(allow_big_lds(k_rankB_grid<4, LDS>)));
+  if (R == 2)
+    k_rankB_grid<2, LDS><<<grid, ENG_THREADS, lds, st>>>(B.codes, B.gflag, masks, n, g, ns, ftab, segpos, q);
+  else if (R == 3)
+    k_rankB_grid<3, LDS><<<grid, ENG_THREADS, lds, st>>>(B.codes, B.gflag, masks, n, g, ns, ftab, segpos, q);
+  else
+    k_rankB_grid<4, LDS><<<grid, ENG_THREADS, lds, st>>>(B.codes, B.gflag, masks, n, g, ns, ftab, segpos, q);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+// masks of the grid walk in LDS (one 16-wave workgroup per CU: up to 20,352 stimuli);
+// VISREPS_ENGINE_GRID_LDS=0 reads them from L2 at any n (A/B, tests)
+static bool grid_masks_lds(int64_t n) {
+  return (size_t)n * sizeof(uint64_t) <= 160 * 1024 - 1024 && env_int("VISREPS_ENGINE_GRID_LDS", 1) != 0;
+}
+
 static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_t nb, int64_t n, const int32_t* idx,
                            int64_t k, int64_t n_sets, int full_first, double* scores, int64_t score_ld,
                            uint32_t* const* const* joins, const EngineWs* Es, const EngineCfg& cfg, hipStream_t st) {
   const int64_t M = pairs_of(n);
   const int64_t total = n_sets + (full_first ? 1 : 0);
-  auto per_region = [&](int r) -> int {
-    return run_engine_multi(As[r], Bs, nb, n, idx, k, n_sets, full_first, scores + (size_t)r * nb * score_ld,
-                            score_ld, joins[r], Es[r], LANES, cfg, st);
-  };
-  auto all_per_region = [&]() -> int {
-    for (int r = 0; r < R; ++r) VR_TRY(per_region(r));
+  std::vector<int> solo;  // regions run on their own once the fused passes are done
+  auto finish = [&]() -> int {
+    for (int r : solo)
+      VR_TRY(run_engine_multi(As[r], Bs, nb, n, idx, k, n_sets, full_first, scores + (size_t)r * nb * score_ld,
+                              score_ld, joins[r], Es[0], LANES, cfg, st));
     return VR_OK;
   };
-  if (total == 0 || nb == 0 || M == 0) return all_per_region();
+  auto all_solo = [&]() -> int {
+    solo.clear();
+    for (int r = 0; r < R; ++r) solo.push_back(r);
+    return finish();
+  };
+  if (total == 0 || nb == 0 || M == 0) return all_solo();
   std::vector<PlanHeader> hA((size_t)R), hB((size_t)nb);
   for (int r = 0; r < R; ++r)
     VR_CHECK_HIP(hipMemcpyAsync(&hA[(size_t)r], As[r].hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
   for (int64_t j = 0; j < nb; ++j)
     VR_CHECK_HIP(hipMemcpyAsync(&hB[(size_t)j], Bs[j].hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
   VR_CHECK_HIP(hipStreamSynchronize(st));
-  bool fused = engine_est() && cfg.est_mode == 3 && cfg.est_lds && R >= 2 && R <= 4 &&
-               env_int("VISREPS_ENGINE_TRI", 0) == 0 && env_int("VISREPS_ENGINE_LO_JOIN", 0) == 0 &&
-               env_int("VISREPS_ENGINE_GRID", 1) != 0 && g_test_inject.load() < 0;
-  for (int r = 0; r < R && fused; ++r) fused = hA[(size_t)r].max_group < 65536u;
+  bool fused = engine_est() && cfg.est_mode == 3 && R >= 2 && R <= 4 && env_int("VISREPS_ENGINE_TRI", 0) == 0 &&
+               env_int("VISREPS_ENGINE_LO_JOIN", 0) == 0 && env_int("VISREPS_ENGINE_GRID", 1) != 0;
+  // test hook (vr_test_engine_inject): the first fused region's TB gets the B-side error after
+  // its A walk of that pass, so the region must be flagged and re-run on its own
+  const int64_t inject = g_test_inject.load(std::memory_order_relaxed);
   for (int64_t j = 0; j < nb && fused; ++j) fused = hB[(size_t)j].max_group < 65536u;
-  if (!fused) return all_per_region();
+  if (!fused) return all_solo();
+  std::vector<int> act;  // the fused regions
+  for (int r = 0; r < R; ++r) (hA[(size_t)r].max_group < 65536u ? act : solo).push_back(r);
   std::vector<char> nan_b((size_t)nb);
   for (int64_t j = 0; j < nb; ++j) nan_b[(size_t)j] = hB[(size_t)j].has_nan != 0;
   // (a point-only call holds the full set alone: its window is the full set's, so lane 0's
@@ -2619,7 +2648,12 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
   // the masks of a pass are built once (region 0's buffer) and read by every region
   std::vector<EngineWs> E(Es, Es + R);
   for (int r = 1; r < R; ++r) E[(size_t)r].masks = E[0].masks;
-  for (int r = 0; r < R; ++r) {
+  // A-side walks: masks in LDS when two 16-wave workgroups per CU hold them (n <= 10,176),
+  // else from L2 (the per-region calls' choice, engine_cfg)
+  auto est_a = [&](auto&& fn) -> int {
+    return cfg.est_lds ? fn(std::integral_constant<bool, true>{}) : fn(std::integral_constant<bool, false>{});
+  };
+  for (int r : act) {
     k_seg_table<<<(nsA + 256) / 256, 256, 0, st>>>(As[r].gstart, As[r].hdr, M, nsA, E[(size_t)r].segposA);
     VR_CHECK_LAUNCH();
   }
@@ -2631,22 +2665,22 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
   if (n_sets > 0 && env_int("VISREPS_ENGINE_EST_PREDICT", 1) != 0) {
     const int nl0 = (int)std::min<int64_t>(LANES, total);
     VR_TRY(build_pass_masks(idx, k, 0, nl0, full_first, E[0].masks, n, st));
-    for (int r = 0; r < R; ++r) {
+    std::vector<int> keep;
+    for (int r : act) {
       bool bad = false;
-      VR_TRY((est_predict<true, true>(As[r], n, E[(size_t)r], LANES, nl0, full_first != 0, cfg, e3, st, bad)));
-      if (bad) return all_per_region();
+      VR_TRY(est_a([&](auto cl) -> int {
+        return est_predict<decltype(cl)::value, true>(As[r], n, E[(size_t)r], LANES, nl0, full_first != 0, cfg, e3,
+                                                      st, bad);
+      }));
+      (bad ? solo : keep).push_back(r);
     }
+    act.swap(keep);
   }
-  static bool attr = false;
-  if (!attr) {
-    VR_TRY(allow_big_lds(k_rankB_grid<2>));
-    VR_TRY(allow_big_lds(k_rankB_grid<3>));
-    VR_TRY(allow_big_lds(k_rankB_grid<4>));
-    attr = true;
-  }
+  if (act.size() < 2) return all_solo();  // fusing pays with two regions or more
   const int64_t npass = (total + LANES - 1) / LANES;
   const unsigned ggrid = (unsigned)num_cus();  // one 16-wave workgroup per CU (4 waves per SIMD)
-  for (int r = 0; r < R; ++r)
+  const bool glds = grid_masks_lds(n);
+  for (int r : act)
     VR_CHECK_HIP(hipMemsetAsync(E[(size_t)r].viol, 0, (size_t)std::min<int64_t>(npass, EST_MAX_PASSES) * sizeof(uint32_t), st));
   for (int64_t p = 0; p < npass; ++p) {
     const int64_t set0 = p * LANES;
@@ -2654,39 +2688,43 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
     const bool full0 = full_first && p == 0;
     const int64_t vslot = p % EST_MAX_PASSES;
     VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E[0].masks, n, st));
-    for (int r = 0; r < R; ++r) {
+    for (int r : act) {
       VR_CHECK_HIP(hipMemsetAsync(E[(size_t)r].queue, 0, sizeof(uint32_t) * (size_t)QS_RANKB, st));
       uint32_t* viol = E[(size_t)r].viol + vslot;
-      VR_TRY((full0 ? pass_a_est<4, true, true, false>(As[r], n, E[(size_t)r], LANES, nl, cfg, e3, trip, viol, st)
-                    : pass_a_est<3, true, true, false>(As[r], n, E[(size_t)r], LANES, nl, cfg, e3, trip, viol, st)));
+      VR_TRY(est_a([&](auto cl) -> int {
+        constexpr bool CL = decltype(cl)::value;
+        return full0 ? pass_a_est<4, CL, true, false>(As[r], n, E[(size_t)r], LANES, nl, cfg, e3, trip, viol, st)
+                     : pass_a_est<3, CL, true, false>(As[r], n, E[(size_t)r], LANES, nl, cfg, e3, trip, viol, st);
+      }));
+      if (p == inject && r == act[0]) {
+        k_inject_tb<<<1, LANES, 0, st>>>(static_cast<uint16_t*>(E[(size_t)r].TB), (uint32_t)(M / 2), LANES, nl);
+        VR_CHECK_LAUNCH();
+      }
     }
     VR_CHECK_HIP(hipMemsetAsync(E[0].queue + QS_RANKB, 0,
                                 sizeof(uint32_t) * (size_t)std::min<int64_t>(nb, QSLOTS - QS_RANKB), st));
+    const int RA = (int)act.size();
     for (int64_t j = 0; j < nb; ++j) {
       GridB g{};
-      for (int r = 0; r < R; ++r) {
-        const size_t us = E[(size_t)r].useg * (size_t)j;
-        g.TB[r] = static_cast<const uint16_t*>(E[(size_t)r].TB);
-        g.posA[r] = joins[r][2 * j];
-        g.seg_tot[r] = E[(size_t)r].segB_tot + us;
-        g.seg_part[r] = E[(size_t)r].segB_part + us * PB_N;
+      for (int i = 0; i < RA; ++i) {
+        const EngineWs& e = E[(size_t)act[(size_t)i]];
+        const size_t us = e.useg * (size_t)j;
+        g.TB[i] = static_cast<const uint16_t*>(e.TB);
+        g.posA[i] = joins[act[(size_t)i]][2 * j];
+        g.seg_tot[i] = e.segB_tot + us;
+        g.seg_part[i] = e.segB_part + us * PB_N;
       }
       uint32_t* q = E[0].queue + QS_RANKB + (size_t)j % (size_t)(QSLOTS - QS_RANKB);
       if (j >= QSLOTS - QS_RANKB) VR_CHECK_HIP(hipMemsetAsync(q, 0, sizeof(uint32_t), st));
       const uint32_t* segpos = E[0].segposB + E[0].segstride * (size_t)j;
-      KtScope kt(full0 ? KT_RANKB_FULL : KT_RANKB_GRID, (double)M * R, st);
-      if (R == 2)
-        k_rankB_grid<2><<<ggrid, ENG_THREADS, cfg.tab, st>>>(Bs[j].codes, Bs[j].gflag, E[0].masks, n, g, ns, E[0].ftab,
-                                                             segpos, q);
-      else if (R == 3)
-        k_rankB_grid<3><<<ggrid, ENG_THREADS, cfg.tab, st>>>(Bs[j].codes, Bs[j].gflag, E[0].masks, n, g, ns, E[0].ftab,
-                                                             segpos, q);
+      KtScope kt(full0 ? KT_RANKB_FULL : KT_RANKB_GRID, (double)M * RA, st);
+      if (glds)
+        VR_TRY(launch_grid<true>(RA, ggrid, (size_t)n * sizeof(uint64_t), Bs[j], E[0].masks, n, g, ns, E[0].ftab,
+                                 segpos, q, st));
       else
-        k_rankB_grid<4><<<ggrid, ENG_THREADS, cfg.tab, st>>>(Bs[j].codes, Bs[j].gflag, E[0].masks, n, g, ns, E[0].ftab,
-                                                             segpos, q);
-      VR_CHECK_LAUNCH();
+        VR_TRY(launch_grid<false>(RA, ggrid, 0, Bs[j], E[0].masks, n, g, ns, E[0].ftab, segpos, q, st));
     }
-    for (int r = 0; r < R; ++r) {
+    for (int r : act) {
       if (full0) {
         for (int64_t j = 0; j < nb; ++j) {
           KtScope kt(KT_FULL_CORR, (double)M, st);
@@ -2699,27 +2737,35 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
                         scores + (size_t)r * nb * score_ld + set0, score_ld, E[(size_t)r].viol + vslot, st,
                         full0 ? E[(size_t)r].corr : nullptr));
     }
-    // flags: after the first pass, then every EST_MAX_PASSES passes and at the end
+    // flags: after the first pass, then every EST_MAX_PASSES passes and at the end. A region
+    // with a flagged pass (rare: the estimate missed, or a B-side recovery broke the tail
+    // invariants) leaves the fused set and is run on its own at the end, which rewrites all
+    // of its scores; the other regions' sums are their own and stand.
     if (p == 0 || vslot == EST_MAX_PASSES - 1 || p == npass - 1) {
       const int64_t cnt = vslot + 1;
-      for (int r = 0; r < R; ++r) {
+      std::vector<int> keep;
+      for (int r : act) {
         std::vector<uint32_t> flags((size_t)cnt);
         VR_CHECK_HIP(hipMemcpyAsync(flags.data(), E[(size_t)r].viol, flags.size() * sizeof(uint32_t),
                                     hipMemcpyDeviceToHost, st));
         VR_CHECK_HIP(hipStreamSynchronize(st));
         bool any = false;
         for (uint32_t f : flags) any = any || f != 0;
-        // a flagged pass (rare: the estimate missed, or a B-side recovery broke the tail
-        // invariants): every region again on its own (EST with exact re-runs of its flagged
-        // passes), which rewrites every score
-        if (any) return all_per_region();
+        (any ? solo : keep).push_back(r);
+      }
+      act.swap(keep);
+      if (act.size() < 2 && p + 1 < npass) {  // one region left: it runs on its own too
+        for (int r : act) solo.push_back(r);
+        act.clear();
+        break;
       }
       if (vslot == EST_MAX_PASSES - 1 && p + 1 < npass)
-        for (int r = 0; r < R; ++r)
+        for (int r : act)
           VR_CHECK_HIP(hipMemsetAsync(E[(size_t)r].viol, 0, (size_t)EST_MAX_PASSES * sizeof(uint32_t), st));
     }
   }
-  return VR_OK;
+  std::sort(solo.begin(), solo.end());
+  return finish();
 }
 
 // Scores for `total` subsets (full set first if full_first), 64 per pass.
@@ -2901,11 +2947,20 @@ int vr_bootstrap_spearman_multi_joined(const void* planA, const void* const* pla
                           joins.data(), E, LANES, cfg, as_stream(stream));
 }
 
+// A grid call's workspace: region 0's full joined-multi layout, then one slim layout (u16 TB,
+// no join arrays) per further region
+static size_t grid_slim_bytes(int64_t n, int64_t n_b, int nwaves) {
+  size_t b = 0;
+  engine_layout(nullptr, n, LANES, nwaves, &b, n_b, true);
+  return b;
+}
+
 size_t vr_bootstrap_grid_joined_workspace(int64_t n, int64_t n_a, int64_t n_b) {
   n = n < 0 ? 0 : n;
   n_a = n_a < 1 ? 1 : n_a;
   n_b = n_b < 1 ? 1 : n_b;
-  return (size_t)n_a * multi_layout(nullptr, n, n_b, engine_cfg(n).nwaves, nullptr, nullptr, true);
+  const int nw = engine_cfg(n).nwaves;
+  return multi_layout(nullptr, n, n_b, nw, nullptr, nullptr, true) + (size_t)(n_a - 1) * grid_slim_bytes(n, n_b, nw);
 }
 
 int vr_bootstrap_spearman_grid_joined(const void* const* planAs, int64_t n_a, const void* const* planBs, int64_t n_b,
@@ -2926,17 +2981,25 @@ int vr_bootstrap_spearman_grid_joined(const void* const* planAs, int64_t n_a, co
   for (int64_t u = 0; u < n_a * n_b; ++u) VR_REQUIRE(posA[u] != nullptr, "%s: posA[%lld] is null", fn, (long long)u);
   EngineCfg cfg = engine_cfg(n);
   cfg.prejoined = true;
-  const size_t one = multi_layout(nullptr, n, n_b, cfg.nwaves, nullptr, nullptr, true);
-  if (ws == nullptr || ws_bytes < one * (size_t)n_a) {
-    set_error("%s: workspace %zu < %zu", fn, ws_bytes, one * (size_t)n_a);
+  const size_t full = multi_layout(nullptr, n, n_b, cfg.nwaves, nullptr, nullptr, true);
+  const size_t slim = grid_slim_bytes(n, n_b, cfg.nwaves);
+  const size_t need = full + (size_t)(n_a - 1) * slim;
+  if (ws == nullptr || ws_bytes < need) {
+    set_error("%s: workspace %zu < %zu", fn, ws_bytes, need);
     return VR_EWORKSPACE;
   }
   std::vector<EngineWs> E((size_t)n_a);
-  std::vector<std::vector<uint32_t*>> jv((size_t)n_a);
+  std::vector<uint32_t*> j0;
+  multi_layout(ws, n, n_b, cfg.nwaves, &E[0], &j0, true);
+  for (int64_t i = 1; i < n_a; ++i)
+    E[(size_t)i] = engine_layout(static_cast<char*>(ws) + full + (size_t)(i - 1) * slim, n, LANES, cfg.nwaves,
+                                 nullptr, n_b, true);
+  // every region: its own A positions, region 0's second arrays (the exact form's A chunks,
+  // written when a region runs on its own)
+  std::vector<std::vector<uint32_t*>> jv((size_t)n_a, j0);
   std::vector<uint32_t* const*> joins((size_t)n_a);
   std::vector<PlanView> As;
   for (int64_t i = 0; i < n_a; ++i) {
-    multi_layout(static_cast<char*>(ws) + (size_t)i * one, n, n_b, cfg.nwaves, &E[(size_t)i], &jv[(size_t)i], true);
     for (int64_t j = 0; j < n_b; ++j) jv[(size_t)i][(size_t)(2 * j)] = posA[i * n_b + j];
     joins[(size_t)i] = jv[(size_t)i].data();
     As.push_back(plan_layout(const_cast<void*>(planAs[i]), n));

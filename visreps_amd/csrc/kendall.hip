@@ -569,8 +569,8 @@ static unsigned blocks_for(int64_t count, int bs) { return (unsigned)((count + b
 
 template <bool LDS>
 static int set_kwalk_attr() {
-  static bool done = false;
-  if (LDS && !done) {
+  if (!LDS) return VR_OK;
+  VR_ONCE({
     const int mx = 160 * 1024 - (int)KW_STATIC_LDS;
     VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk<LDS, false>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, mx));
@@ -578,8 +578,7 @@ static int set_kwalk_attr() {
                                      hipFuncAttributeMaxDynamicSharedMemorySize, mx));
     VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk_top3<LDS>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, mx));
-    done = true;
-  }
+  });
   return VR_OK;
 }
 

@@ -926,6 +926,17 @@ def summarize(scores: np.ndarray, bootstrap: bool) -> Dict:
     return res
 
 
+def _engine_ws_fits(dev: torch.device, nbytes: int) -> bool:
+    """An engine workspace of nbytes fits the device: free memory + torch's cached blocks +
+    the pool's current engine buffer (which the new one replaces), with 10 % headroom."""
+    if dev.type != "cuda":
+        return True
+    free = torch.cuda.mem_get_info(dev)[0]
+    cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    cur = workspace.current(dev, "engine")
+    return nbytes <= 0.9 * (free + cached + cur)
+
+
 def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[str],
                   neural_rdms: Dict[str, torch.Tensor], n: int, *, n_boot: int = 1000,
                   seed: int = 42, pg=None, times: Optional[StepTimes] = None,
@@ -995,7 +1006,10 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
             pns = {r: (plans[("n", r)] if ("n", r) in plans else plan_fn(neural_rdms[r])) for r in by_region}
             joined = shared_joins(pns, by_region, mplans, times)
     # Regions sharing their point list (all of them on one GPU) run in groups of up to 4 as
-    # one grid call each: every model plan walked once per pass for the group's regions
+    # one grid call each: every model plan walked once per pass for the group's regions. A
+    # group whose grid workspace (region 0's full engine workspace + a slim one per further
+    # region) does not fit the free device memory runs as per-region calls.
+    ran_grid = False
     if joined is not None and os.environ.get("VISREPS_ENGINE_GRID", "1") != "0":
         groups = []
         for r in by_region:
@@ -1006,6 +1020,9 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
                 groups.append([r])
         for grp in [g for g in groups if len(g) >= 2]:
             pts = by_region[grp[0]]
+            if not _engine_ws_fits(dev, int(lib().vr_bootstrap_grid_joined_workspace(n, len(grp), len(pts)))):
+                continue
+            ran_grid = True
             pg_n = [plans[("n", r)] if ("n", r) in plans else pns.pop(r) for r in grp]
             out = run_grid(pg_n, [mplans[p] for p in pts], idx,
                            [[joined.pop((p, r)) for r in grp] for p in pts], times)
@@ -1024,6 +1041,8 @@ def all_units_rsa(model_rdm_fn: Callable[[str], torch.Tensor], points: Sequence[
             local[(p, r)] = np.asarray(torch.as_tensor(out[j]).cpu())
         del pn  # the last reference to a plan built here: freed before the next region's call
     del mplans
+    if ran_grid:  # the pool's grow-only engine buffer goes back to torch's cache
+        workspace.release("engine")
     if world > 1:
         gathered: List[Dict] = [None] * world
         dist.all_gather_object(gathered, local, group=pg)
