@@ -203,13 +203,15 @@ def structured_est_probe(n: int, plan_b, dev) -> dict:
             R.bootstrap_spearman_multi(plan_a, [plan_b], idx, full_first=True)  # warm
             torch.cuda.synchronize()
             r0, q0 = int(L.vr_engine_est_reruns()), int(L.vr_engine_est_predicted())
+            f0 = int(L.vr_engine_est1_fallbacks())
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             sc = R.bootstrap_spearman_multi(plan_a, [plan_b], idx, full_first=True)
             e1.record()
             torch.cuda.synchronize()
             out[form] = {"unit_ms": round(e0.elapsed_time(e1), 2), "reruns": int(L.vr_engine_est_reruns()) - r0,
-                         "predicted_exact": int(L.vr_engine_est_predicted()) - q0, "point": float(sc[0, 0])}
+                         "predicted_off_est3": int(L.vr_engine_est_predicted()) - q0,
+                         "est1_fallback": int(L.vr_engine_est1_fallbacks()) - f0, "point": float(sc[0, 0])}
             all_scores[form] = sc.cpu().numpy()
         finally:
             if old is None:
@@ -222,8 +224,9 @@ def structured_est_probe(n: int, plan_b, dev) -> dict:
     out["scores_compared"] = int(all_scores["est"].size)
     out["note"] = ("neural RDM d_ab = u_a + u_b + 0.05 noise, u ~ Exp(1)^2, vs the V1 neural plan of the bench: "
                    "EST passes the A side flags are re-run exact (est.reruns); a call whose first-pass A counts "
-                   "already break the EST 3 window runs exact from the start (est.predicted_exact, no EST pass "
-                   "spent); exact = VISREPS_ENGINE_EST=0")
+                   "already break the EST 3 window leaves EST 3 before any EST pass (est.predicted_off_est3) and "
+                   "runs EST 1, per-lane count tables (est.est1_fallback), its flagged passes exact; "
+                   "exact = VISREPS_ENGINE_EST=0")
     return out
 
 
@@ -888,7 +891,7 @@ def main():
             "roofline_join4": roof_join4,
             "kernels_per_step": {k: v for k, v in kernels.items() if v["launches_per_step"]},
             "est_reruns": est_reruns,
-            "est_predicted_exact": est_predicted,
+            "est_predicted_off_est3": est_predicted,
             "est_tail_flags": est_tail_flags,
             "est_structured": est_structured,
             "exact_form_step_s": exact_step,

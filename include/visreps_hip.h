@@ -236,9 +236,12 @@ int64_t vr_engine_est_tail_flags(void);
  * see), so the tail invariants and the exact re-run can be tested. -1 (the default) = off. */
 int vr_test_engine_inject(int64_t pass);
 /* Engine calls whose first pass's A counts (a count pre-pass before any EST pass) already
- * put some subset's ranks outside the EST 3 window, so the whole call ran in the exact form
- * without spending a flagged EST pass (VISREPS_ENGINE_EST_PREDICT=0 disables the check). */
+ * put some subset's ranks outside the EST 3 window, so the call left EST 3 without spending
+ * a flagged EST pass (VISREPS_ENGINE_EST_PREDICT=0 disables the check). */
 int64_t vr_engine_est_predicted(void);
+/* Of those, the calls run in EST 1 (per-lane count tables) instead of the exact form
+ * (VISREPS_ENGINE_EST1_FALLBACK=0: exact form). */
+int64_t vr_engine_est1_fallbacks(void);
 
 // Kernel-level HIP-event timing of the hot kernels, for pricing the dominant kernel against
 // its roofline on the stream it runs on (bench.py). Off by default; enabling clears the

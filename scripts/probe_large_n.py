@@ -50,6 +50,8 @@ for n in [int(s) for s in os.environ.get("SIZES", "12000,20500").split(",")]:
     sj = R.SharedJoins(neurals)
     js = [sj.join(pm) for pm in models]  # js[m][region]
     del sj
+    L = _lib.lib()
+    c0 = [int(L.vr_engine_est_reruns()), int(L.vr_engine_est_predicted()), int(L.vr_engine_est1_fallbacks())]
     _lib.ktimer_enable(True)
     grid, t_grid = timed(lambda: R.bootstrap_spearman_grid(neurals, models, idx, js, full_first=True))
     gl = _lib.ktimer_read("k_rankB_grid")
@@ -69,7 +71,9 @@ for n in [int(s) for s in os.environ.get("SIZES", "12000,20500").split(",")]:
     print(f"n={n} M={n * (n - 1) // 2} boots={NB}: grid {t_grid / units:.2f} ms/unit "
           f"(k_rankB_grid {gl[1]} launches, {gl[0] / max(gl[1], 1):.3f} ms each) | per-region {t_reg / units:.2f} ms/unit "
           f"(k_rankB {rb[1]} launches, {rb[0] / max(rb[1], 1):.3f} ms each) | bit-equal {equal} "
-          f"reruns={int(_lib.lib().vr_engine_est_reruns())}", flush=True)
+          f"| calls off EST 3 up front {int(L.vr_engine_est_predicted()) - c0[1]}, in EST 1 "
+          f"{int(L.vr_engine_est1_fallbacks()) - c0[2]}, passes re-run exact {int(L.vr_engine_est_reruns()) - c0[0]}",
+          flush=True)
     del neurals, models, js, grid, outs, idx
     _lib.workspace.release()
     torch.cuda.empty_cache()

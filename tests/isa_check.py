@@ -152,6 +152,55 @@ def check_asm_gathers(code: list[tuple[int, str, int | None]]) -> tuple[int, lis
     return n_gathers, sorted(set(problems))
 
 
+_SREG = re.compile(r"\bs(\d+)\b|\bs\[(\d+):(\d+)\]")
+_SADDR_ANY = re.compile(r"^global_(load|store)\w*\s+.*,\s*(s\[\d+:\d+\])(\s|$)")
+
+
+def _sregs(text: str) -> set[int]:
+    out: set[int] = set()
+    for m in _SREG.finditer(text):
+        if m.group(1) is not None:
+            out.add(int(m.group(1)))
+        else:
+            out.update(range(int(m.group(2)), int(m.group(3)) + 1))
+    return out
+
+
+def check_sgpr_base_hazards(code: list[tuple[int, str, int | None]], wait_states: int = 5) -> list[str]:
+    """A VALU write of an SGPR (v_readlane / v_readfirstlane, or an SGPR spill restored from
+    a VGPR lane) followed within `wait_states` wait states by a vector-memory instruction
+    reading that SGPR as its scalar base: the hardware needs 5 wait states there, hipcc pads
+    its own loads but not the inside of an asm statement (cdna_hip_programming.md §5.7
+    item 2), and the load then forms its address from the SGPR's stale value. Round 5's
+    MEMORY_APERTURE_VIOLATION in k_rankB (masks from L2, the VR_XW_SLO probe build: 32 SGPRs
+    spilled to VGPR lanes) was this: `v_readlane_b32 s1, v62, 7` restoring the mask table's
+    address high word right before the asm `global_load_dwordx2 v[4:5], v0, s[0:1]`.
+    Straight-line look-back (a branch target in the window is treated as a fresh start)."""
+    problems = []
+    targets = {t for _, _, t in code if t is not None}
+    for i, (addr, ins, _) in enumerate(code):
+        m = _SADDR_ANY.match(ins)
+        if not m:
+            continue
+        base = _sregs(m.group(2))
+        ws = 0
+        for k in range(i - 1, -1, -1):
+            a_k, t_k, _ = code[k]
+            op = t_k.split()[0]
+            if op == "s_nop":
+                ws += int(t_k.split()[1], 0) + 1
+            else:
+                dst = t_k.split(None, 1)[1].split(",")[0] if " " in t_k else ""
+                if _sregs(dst) & base:
+                    if op.startswith("v_") and ws < wait_states:
+                        problems.append(f"{addr:#x} `{ins}`: base written by `{t_k}` {ws} wait states before")
+                    break
+                ws += 1
+            if ws >= wait_states or a_k in targets:
+                break
+    return problems
+
+
 def check_object(obj: str, kernel_pattern: str) -> dict[str, dict]:
     """Findings for every kernel whose symbol matches kernel_pattern."""
     with tempfile.TemporaryDirectory() as d:
@@ -164,6 +213,7 @@ def check_object(obj: str, kernel_pattern: str) -> dict[str, dict]:
         if not pat.search(name):
             continue
         n, probs = check_asm_gathers(code.get(name, []))
+        probs = probs + check_sgpr_base_hazards(code.get(name, []))
         out[name] = {"vgpr_spill_count": md.get(".vgpr_spill_count", 0),
                      "sgpr_spill_count": md.get(".sgpr_spill_count", 0),
                      "private_segment_fixed_size": md.get(".private_segment_fixed_size", 0),

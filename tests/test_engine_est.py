@@ -154,12 +154,14 @@ def test_triangle_order_form_equals_exact_form(dev, n, nb, monkeypatch):
     assert np.array_equal(est, ref)
 
 
-def test_structured_rdm_goes_exact_up_front(dev, monkeypatch):
+def test_structured_rdm_leaves_est3_up_front(dev, monkeypatch):
     # n = 5000 with the heavy per-stimulus effects: the first pass's A counts (k_countA at
-    # <= 256 boundaries) are already far outside the EST 3 window, so the call runs exact
-    # from the start -- no EST pass is spent and flagged (vr_engine_est_predicted counts
-    # the call, vr_engine_est_reruns stays) -- and the scores equal the exact form; with the
-    # check off, the first EST pass is flagged and the call gives up there, same scores.
+    # <= 256 boundaries) are already far outside the EST 3 window, so the call leaves EST 3
+    # before spending an EST pass (vr_engine_est_predicted counts it) and runs EST 1, whose
+    # per-lane tables follow each subset's own counts (vr_engine_est1_fallbacks); its scores
+    # equal the exact form, and so do those of the exact-form fallback
+    # (VISREPS_ENGINE_EST1_FALLBACK=0); with the check off, the first EST 3 pass is flagged
+    # and the call gives up there, same scores.
     n = 5000
     g = torch.Generator(device=dev).manual_seed(7)
     u = torch.empty(n, device=dev).exponential_(1.0, generator=g) ** 2
@@ -170,13 +172,19 @@ def test_structured_rdm_goes_exact_up_front(dev, monkeypatch):
     del a
     idx = bootstrap_indices(42, n, int(0.9 * n), 140)
     L = lib()
-    p0, r0 = int(L.vr_engine_est_predicted()), int(L.vr_engine_est_reruns())
+    p0, f0 = int(L.vr_engine_est_predicted()), int(L.vr_engine_est1_fallbacks())
     est = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
     assert int(L.vr_engine_est_predicted()) - p0 == 1
-    assert int(L.vr_engine_est_reruns()) == r0
+    assert int(L.vr_engine_est1_fallbacks()) - f0 == 1
     with exact_engine():
         ref = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
     assert np.array_equal(est, ref)
+    monkeypatch.setenv("VISREPS_ENGINE_EST1_FALLBACK", "0")
+    r0 = int(L.vr_engine_est_reruns())
+    ex_up_front = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
+    assert int(L.vr_engine_est_reruns()) == r0, "the exact form from the start spends no flagged pass"
+    assert np.array_equal(ex_up_front, ref)
+    monkeypatch.delenv("VISREPS_ENGINE_EST1_FALLBACK")
     monkeypatch.setenv("VISREPS_ENGINE_EST_PREDICT", "0")
     late = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
     assert int(L.vr_engine_est_reruns()) - r0 >= 1, "without the check the first EST pass is flagged"
@@ -389,7 +397,7 @@ def test_grid_structured_region_leaves_the_others_fused(dev):
     # still walk each model plan once per pass together
     from visreps_amd._lib import ktimer_enable, ktimer_read
 
-    n = 5000  # test_structured_rdm_goes_exact_up_front's RDM, which fails the check
+    n = 5000  # test_structured_rdm_leaves_est3_up_front's RDM, which fails the check
     g = torch.Generator(device=dev).manual_seed(7)
     u = torch.empty(n, device=dev).exponential_(1.0, generator=g) ** 2
     s = u[:, None] + u[None, :] + 0.05 * torch.rand(n, n, device=dev, generator=g)

@@ -57,6 +57,23 @@ def test_default_forms_have_no_scratch(rankb):
         assert r["private_segment_fixed_size"] == 0, (name, r)
 
 
+def test_checker_flags_sgpr_base_hazard():
+    from isa_check import check_sgpr_base_hazards
+
+    def code(lines):
+        return [(4 * i, s, None) for i, s in enumerate(lines)]
+
+    # round 5's fault: an SGPR spill restored by v_readlane right before an asm load's base
+    bad = code(["v_readlane_b32 s1, v62, 7", "global_load_dwordx2 v[4:5], v0, s[0:1]"])
+    assert check_sgpr_base_hazards(bad)
+    # padded by 5 wait states, or written by the scalar unit: fine
+    assert not check_sgpr_base_hazards(code(["v_readlane_b32 s1, v62, 7", "s_nop 4",
+                                             "global_load_dwordx2 v[4:5], v0, s[0:1]"]))
+    assert not check_sgpr_base_hazards(code(["v_readlane_b32 s40, v33, 17", "s_lshl_b64 s[16:17], s[40:41], 7",
+                                             "s_add_u32 s16, s36, s16", "s_addc_u32 s17, s37, s17",
+                                             "global_load_ushort v53, v31, s[16:17] nt"]))
+
+
 def test_checker_flags_violations():
     def code(lines):
         return [(4 * i, s, None) for i, s in enumerate(lines)]

@@ -120,6 +120,7 @@ _PROTOTYPES = {
     "vr_engine_est_tail_flags": (_c_i64, []),
     "vr_test_engine_inject": (ctypes.c_int, [_c_i64]),
     "vr_engine_est_predicted": (_c_i64, []),
+    "vr_engine_est1_fallbacks": (_c_i64, []),
     "vr_ktimer_enable": (ctypes.c_int, [ctypes.c_int]),
     "vr_trace_mark": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp]),
     "vr_ktimer_read": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_double),

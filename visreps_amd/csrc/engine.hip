@@ -84,15 +84,16 @@ constexpr int EST_STEP_BITS = 12;  // interpolation steps per interval: 2^12
 static std::atomic<int64_t> g_est_reruns{0};      // passes re-run in the exact form (vr_engine_est_reruns)
 static std::atomic<int64_t> g_est_predicted{0};   // calls sent to the exact form before any EST pass (vr_engine_est_predicted)
 static std::atomic<int64_t> g_est_tail_flags{0};  // of those, flagged by the tail invariants alone (vr_engine_est_tail_flags)
+static std::atomic<int64_t> g_est1_fallbacks{0};  // calls run in EST 1 after EST 3's up-front check failed
 
 // log2 of the coarse interval: the smallest b >= 12 (windows of 64 never straddle a
 // boundary; the 4096 steps are whole positions) with ceil(M / 2^b) <= 96, or, for larger
 // triangles, <= EST_NC (a step of 2^(b-12) positions moves lo by <= 2^(b-11): b <= 23
 // keeps that at a few thousand of the 2^15 of slack).
 // maxrows < EST_NC: the table must fit beside the masks in LDS (fewer, longer intervals).
-static int est_bits(int64_t M, uint32_t maxrows = EST_NC) {
+static int est_bits(int64_t M, uint32_t maxrows = EST_NC, uint32_t target = 96) {
   int b = 12;
-  while (((M + ((int64_t)1 << b) - 1) >> b) > 96 && b < 23) ++b;
+  while (((M + ((int64_t)1 << b) - 1) >> b) > (int64_t)target && b < 23) ++b;
   while (((M + ((int64_t)1 << b) - 1) >> b) > (int64_t)maxrows && b < 31) ++b;
   return b;
 }
@@ -145,7 +146,9 @@ static uint32_t est_segments(int64_t M, int est_nwaves) {
   return (uint32_t)std::max<int64_t>(1, std::min<int64_t>(by_len, (int64_t)est_nwaves));
 }
 
-static EngineCfg engine_cfg(int64_t n) {
+// mode: the EST estimate (0: VISREPS_ENGINE_EST_MODE, default 3; 1: the per-lane table, the
+// fallback of a call whose EST 3 estimate fails its up-front check)
+static EngineCfg engine_cfg(int64_t n, int mode = 0) {
   EngineCfg c;
   const int64_t M = pairs_of(n);
   const size_t need = (size_t)n * sizeof(uint64_t);
@@ -164,12 +167,15 @@ static EngineCfg engine_cfg(int64_t n) {
   const size_t per_wg = cap / est_wg;
   c.est_lds = c.use_lds && env_int("VISREPS_ENGINE_EST_LDS", 1) != 0 && per_wg >= need + row;
   // VISREPS_ENGINE_EST_LIN=1: one linear interval (EST 2), no table in LDS
-  c.est_mode = std::max(1, std::min(3, env_int("VISREPS_ENGINE_EST_MODE", 3)));
+  c.est_mode = mode > 0 ? mode : std::max(1, std::min(3, env_int("VISREPS_ENGINE_EST_MODE", 3)));
   if (c.est_mode >= 2) c.est_lds = c.use_lds && env_int("VISREPS_ENGINE_EST_LDS", 1) != 0 && per_wg >= need;
   uint32_t rows_fit =
       c.est_lds ? (uint32_t)std::min<size_t>(EST_NC, (per_wg - need) / row) : (uint32_t)EST_NC;
   if (c.est_mode >= 2) rows_fit = 1;
-  c.est_b = est_bits(M, rows_fit);
+  // EST 1 with masks from L2: the table alone in LDS, up to 144 intervals (72 KB: two
+  // workgroups per CU still fit) -- finer knots for the large structured triangles it serves
+  const uint32_t target = (c.est_mode == 1 && !c.est_lds) ? 144u : 96u;
+  c.est_b = est_bits(M, rows_fit, target);
   c.est_rows = M > 0 ? est_intervals(M, c.est_b) : 0;
   c.est_grid = c.est_lds ? num_cus() * est_wg : c.grid;
   c.est_nwaves = c.est_grid * WAVES_PER_WG;
@@ -1351,7 +1357,7 @@ __device__ inline void gather_window(const TBT* __restrict__ TB, const uint32_t*
 __device__ uint64_t g_wt[2 * 16384];
 #endif
 #ifndef VR_XW_L2
-#define VR_XW_L2 0  // 1: the prefetching walk also with masks from L2 (n > 10,176)
+#define VR_XW_L2 1  // the prefetching walk also with masks from L2 (n > 10,176); 0: the per-window walk there
 #endif
 #ifndef VR_XWIN
 #define VR_XWIN 1  // EST 3 / 4 B walk: next window's streams and masks fetched inside the window (0: off)
@@ -1376,8 +1382,11 @@ __device__ inline void xw_ld2(const uint32_t* a, const uint32_t* b, uint32_t vof
   asm volatile("global_load_dword %0, %1, %2" : "=v"(x) : "v"(voff), "s"(a) : "memory");
   asm volatile("global_load_dword %0, %1, %2" : "=v"(y) : "v"(voff), "s"(b) : "memory");
 }
+// (s_nop 4: five wait states between any VALU write of the base SGPRs -- an SGPR spill
+// restored by v_readlane, round 5's fault -- and the loads reading them; hipcc pads nothing
+// inside an asm statement. tests/test_isa_guard.py checks every asm load for it.)
 __device__ inline void xw_ldm(const uint64_t* m, uint32_t code, uint64_t& a, uint64_t& b) {
-  asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(a) : "v"((code >> 16) * 8u), "s"(m) : "memory");
+  asm volatile("s_nop 4\n\tglobal_load_dwordx2 %0, %1, %2" : "=v"(a) : "v"((code >> 16) * 8u), "s"(m) : "memory");
   asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(b) : "v"((code & 0xffffu) * 8u), "s"(m) : "memory");
 }
 
@@ -1431,9 +1440,9 @@ __global__ __launch_bounds__(ENG_THREADS, EST ? VR_RANKB_EST_MINW : VR_RANKB_MIN
       // EST 3 / 4 (small tie groups): the prefetching walk, which computes the window low
       // ends from the A positions (a join's streamed low ends, VISREPS_ENGINE_LO_JOIN=1, hold
       // the same values and are not read)
-      // (masks in LDS only unless VR_XW_L2: with masks from L2 -- n > 10,176 -- the per-window
-      // walk below serves; the prefetching form's L2-mask path faulted when a round-5 test
-      // first ran it)
+      // (with masks from L2 -- n > 10,176 -- too, VR_XW_L2; round 5 restricted it to LDS masks
+      // after a MEMORY_APERTURE_VIOLATION, whose cause was a probe build's SGPR spill restored
+      // by v_readlane right before the asm mask load that reads it: see xw_ldm)
       constexpr bool XW = VR_XWIN && EST == 3 && !BIGT && (LDS || VR_XW_L2);
       constexpr bool walked = XW;
       if constexpr (XW) {
@@ -2332,10 +2341,13 @@ __global__ void k_inject_tb(uint16_t* __restrict__ TB, uint32_t row, int stride,
   if (lane >= 1 && lane < lanes) TB[(size_t)row * stride + lane] += 1u;
 }
 
+// exact_passes (non-null): run only these passes, in the exact form (a grid call's flagged
+// passes of one region; the rest of its scores stand)
 static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t nb, int64_t n,
                                  const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
                                  double* scores, int64_t score_ld, uint32_t* const* joins,
-                                 const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st) {
+                                 const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st,
+                                 const std::vector<int64_t>* exact_passes = nullptr) {
   const int64_t M = pairs_of(n);
   uint32_t* const xbad = E.viol + EST_MAX_PASSES;  // exact-form passes' invariant flag
   const int64_t inject = g_test_inject.load(std::memory_order_relaxed);
@@ -2422,7 +2434,7 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
   bool predicted_bad = false;
   // (only when some lane holds a bootstrap subset: the full-set lane is exact by
   // construction, and a point-only call -- phase 1's 56 -- would pay a host sync for nothing)
-  if (est && cfg.est_mode == 3 && n_sets > 0 && env_int("VISREPS_ENGINE_EST_PREDICT", 1) != 0) {
+  if (est && cfg.est_mode == 3 && n_sets > 0 && !exact_passes && env_int("VISREPS_ENGINE_EST_PREDICT", 1) != 0) {
     const int64_t sub0 = tri ? LANES - 1 : lw;
     const int nl0 = (int)std::min<int64_t>(sub0, total);
     VR_TRY(build_pass_masks(idx, k, 0, nl0, full_first, E.masks, n, st));
@@ -2433,7 +2445,7 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
   }
   // (pre-joined units already hold their A positions: an EST call reading only those skips
   // the join; an exact-form one rewrites them with the same values beside the A chunks)
-  if (!tri && !predicted_bad && !(cfg.prejoined && est && !lo_join))
+  if (!tri && !predicted_bad && !exact_passes && !(cfg.prejoined && est && !lo_join))
     VR_TRY(join(!est ? JOIN_CHUNK : (lo_join ? JOIN_LO : JOIN_NONE)));
   // the exact chunk-base form of subsets [set0, set0 + nl), nl <= lw
   auto exact_pass = [&](auto tag, int64_t set0, int nl) -> int {
@@ -2461,9 +2473,34 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
       return VR_OK;
     });
   };
+  if (exact_passes) {
+    VR_TRY(join(JOIN_CHUNK));
+    return with_pass_tag(cfg.use_lds, lw == LANES, narrow, [&](auto tag) -> int {
+      for (int64_t p : *exact_passes) {
+        const int64_t set0 = p * lw;
+        if (set0 < total) VR_TRY(exact_pass(tag, set0, (int)std::min<int64_t>(lw, total - set0)));
+      }
+      return VR_OK;
+    });
+  }
   if (!est) return exact_from(0);
   if (predicted_bad) {
     g_est_predicted.fetch_add(1);
+    // The lane-uniform EST 3 window cannot hold these counts (per-stimulus structure moves a
+    // subset's included count further from the line than 2^14 pairs: it grows ~ n^1.5, so
+    // large triangles cross it first). EST 1 follows each lane's own counts (an interpolated
+    // table whose knots are the lane's counts at <= 144 boundaries, one LDS read per pair),
+    // one gather per pair like EST 3; its flagged passes are re-run exact as ever. The exact
+    // form from the start only with VISREPS_ENGINE_EST1_FALLBACK=0 or a point-only call.
+    if (lw == LANES && env_int("VISREPS_ENGINE_EST1_FALLBACK", 1) != 0) {
+      EngineCfg c1 = engine_cfg(n, 1);
+      c1.prejoined = cfg.prejoined;
+      if (c1.nwaves == cfg.nwaves && c1.est_nsegA <= (uint32_t)cfg.nwaves * VR_SEGS_PER_WAVE) {
+        g_est1_fallbacks.fetch_add(1);
+        return run_engine_multi_impl(A, Bs, nb, n, idx, k, n_sets, full_first, scores, score_ld, joins, E, lw, c1,
+                                     st);
+      }
+    }
     return exact_from(0);
   }
   const int64_t sub = tri ? LANES - 1 : lw;  // subsets per EST pass
@@ -2557,10 +2594,12 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
 static int run_engine_multi(const PlanView& A, const PlanView* Bs, int64_t nb, int64_t n,
                             const int32_t* idx, int64_t k, int64_t n_sets, int full_first,
                             double* scores, int64_t score_ld, uint32_t* const* joins,
-                            const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st) {
+                            const EngineWs& E, int lw, const EngineCfg& cfg, hipStream_t st,
+                            const std::vector<int64_t>* exact_passes = nullptr) {
   uint32_t* const xbad = E.viol + EST_MAX_PASSES;
   VR_CHECK_HIP(hipMemsetAsync(xbad, 0, sizeof(uint32_t), st));
-  VR_TRY(run_engine_multi_impl(A, Bs, nb, n, idx, k, n_sets, full_first, scores, score_ld, joins, E, lw, cfg, st));
+  VR_TRY(run_engine_multi_impl(A, Bs, nb, n, idx, k, n_sets, full_first, scores, score_ld, joins, E, lw, cfg, st,
+                               exact_passes));
   uint32_t bad = 0;
   VR_CHECK_HIP(hipMemcpyAsync(&bad, xbad, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VR_CHECK_HIP(hipStreamSynchronize(st));
@@ -2610,10 +2649,15 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
   const int64_t M = pairs_of(n);
   const int64_t total = n_sets + (full_first ? 1 : 0);
   std::vector<int> solo;  // regions run on their own once the fused passes are done
+  std::vector<std::vector<int64_t>> fix((size_t)R);  // fused regions' flagged passes (re-run exact)
   auto finish = [&]() -> int {
     for (int r : solo)
       VR_TRY(run_engine_multi(As[r], Bs, nb, n, idx, k, n_sets, full_first, scores + (size_t)r * nb * score_ld,
                               score_ld, joins[r], Es[0], LANES, cfg, st));
+    for (int r = 0; r < R; ++r)
+      if (!fix[(size_t)r].empty())
+        VR_TRY(run_engine_multi(As[r], Bs, nb, n, idx, k, n_sets, full_first, scores + (size_t)r * nb * score_ld,
+                                score_ld, joins[r], Es[0], LANES, cfg, st, &fix[(size_t)r]));
     return VR_OK;
   };
   auto all_solo = [&]() -> int {
@@ -2738,24 +2782,37 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
                         full0 ? E[(size_t)r].corr : nullptr));
     }
     // flags: after the first pass, then every EST_MAX_PASSES passes and at the end. A region
-    // with a flagged pass (rare: the estimate missed, or a B-side recovery broke the tail
-    // invariants) leaves the fused set and is run on its own at the end, which rewrites all
-    // of its scores; the other regions' sums are their own and stand.
+    // whose first pass is flagged (its estimate is off: structured counts, giant tie groups)
+    // leaves the fused set and runs on its own at the end, which rewrites all of its scores;
+    // a later flagged pass (rare: a B-side recovery broke the tail invariants, or one subset
+    // strayed) is re-run alone in the exact form at the end, the region staying fused. The
+    // other regions' sums are their own and stand.
     if (p == 0 || vslot == EST_MAX_PASSES - 1 || p == npass - 1) {
-      const int64_t cnt = vslot + 1;
+      const int64_t cnt = vslot + 1, pbase = p - vslot;
       std::vector<int> keep;
       for (int r : act) {
         std::vector<uint32_t> flags((size_t)cnt);
         VR_CHECK_HIP(hipMemcpyAsync(flags.data(), E[(size_t)r].viol, flags.size() * sizeof(uint32_t),
                                     hipMemcpyDeviceToHost, st));
         VR_CHECK_HIP(hipStreamSynchronize(st));
-        bool any = false;
-        for (uint32_t f : flags) any = any || f != 0;
-        (any ? solo : keep).push_back(r);
+        if (p == 0 && flags[0]) {
+          solo.push_back(r);
+          continue;
+        }
+        for (int64_t i = 0; i < cnt; ++i) {
+          if (!flags[(size_t)i]) continue;
+          fix[(size_t)r].push_back(pbase + i);
+          g_est_reruns.fetch_add(1);
+          if ((flags[(size_t)i] & 3u) == 2u) g_est_tail_flags.fetch_add(1);
+        }
+        keep.push_back(r);
       }
       act.swap(keep);
       if (act.size() < 2 && p + 1 < npass) {  // one region left: it runs on its own too
-        for (int r : act) solo.push_back(r);
+        for (int r : act) {
+          solo.push_back(r);
+          fix[(size_t)r].clear();
+        }
         act.clear();
         break;
       }
@@ -2830,6 +2887,7 @@ extern "C" {
 int64_t vr_engine_est_reruns(void) { return g_est_reruns.load(); }
 int64_t vr_engine_est_tail_flags(void) { return g_est_tail_flags.load(); }
 int64_t vr_engine_est_predicted(void) { return g_est_predicted.load(); }
+int64_t vr_engine_est1_fallbacks(void) { return g_est1_fallbacks.load(); }
 int vr_test_engine_inject(int64_t pass) {
   g_test_inject.store(pass < 0 ? -1 : pass);
   return VR_OK;
