@@ -285,6 +285,24 @@ size_t vr_kendall_vec_workspace(int64_t m);
 int vr_kendall_tau_a_f64(const double* x, const double* y, int64_t m, double* out, void* ws,
                          size_t ws_bytes, void* stream);
 
+/* The same statistic in O(m log m) for any m < 2^32 (the reference's `_kendall_tau_a` has no
+ * size cap: scipy.stats.kendalltau's merge-sort counting, rsa.py:28): both vectors to dense
+ * ranks (radix sorts), the (x, y)-lexicographic order, then the discordant pairs as the
+ * inversions of the y ranks counted one rank bit per level (kendall_full.hip). Exact integer
+ * counts, so equal bit for bit to vr_kendall_tau_a_f64 where both run. x, y, out [dev]. */
+size_t vr_kendall_full_vec_workspace(int64_t m);
+int vr_kendall_full_vec_f64(const double* x, const double* y, int64_t m, double* out, void* ws,
+                            size_t ws_bytes, void* stream);
+
+/* Kendall tau-a of the strict upper triangles of two RDMs beyond the rank plans' 16-bit
+ * stimulus indices (compute_rdm_correlation(.., "Kendall"), rsa.py:96-129 -> rsa.py:22-40, at
+ * n > 65,535): the kendall_full.hip pipeline on the M = n(n-1)/2 < 2^32 triangle elements
+ * (n <= 92,681; configs[2]'s 73k RDM). A, B [dev] (n, n) row-major fp32, leading dimension
+ * ld; out [dev] one double (NaN for M < 2, NaN input, a constant triangle). */
+size_t vr_kendall_full_workspace(int64_t n);
+int vr_kendall_full_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out, void* ws,
+                        size_t ws_bytes, void* stream);
+
 /* Bootstrapped Kendall RSA on two rank plans: the bootstrap loop of evals.py:355-373 /
  * rsa.py:233-261 with compare_method="kendall". Arguments as
  * vr_bootstrap_spearman_plans; the workspace depends on the number of subsets:

@@ -243,3 +243,103 @@ def test_vec_on_rdm_triangles_equals_triu_path(dev):
     iu = np.triu_indices(120, 1)
     got = R._kendall_tau_a(a[iu], b[iu])[0]
     assert got == R.compute_rdm_correlation(torch.from_numpy(a), torch.from_numpy(b), correlation="Kendall")
+
+
+# ------------------------------------------------ O(m log m) form (kendall_full.hip)
+def _full_vec(x, y):
+    from visreps_amd._lib import check, lib, stream_of, workspace
+
+    L = lib()
+    xd = torch.as_tensor(np.asarray(x, dtype=np.float64)).cuda()
+    yd = torch.as_tensor(np.asarray(y, dtype=np.float64)).cuda()
+    out = torch.empty(1, dtype=torch.float64, device=xd.device)
+    ws = workspace.get(xd.device, L.vr_kendall_full_vec_workspace(xd.numel()), "kendall_full")
+    check(L.vr_kendall_full_vec_f64(xd.data_ptr(), yd.data_ptr(), xd.numel(), out.data_ptr(), ws.data_ptr(),
+                                    ws.numel(), stream_of(xd.device)), "vr_kendall_full_vec_f64")
+    return float(out.item())
+
+
+@pytest.mark.parametrize("m,levels,seed", [(2, None, 0), (3, 2, 1), (4096, None, 2), (4097, 30, 3),
+                                           (20000, 300, 4), (65536, None, 5), (65536, 2000, 6)])
+def test_full_vec_equals_pairwise(dev, m, levels, seed):
+    # the sort-and-inversion form against the pairwise kernel (the same exact counts: bit for
+    # bit) and against scipy + the reference's conversion, ties in x, y and jointly
+    r = np.random.RandomState(seed)
+    x, y = r.randn(m), r.randn(m)
+    if levels:
+        x, y = np.floor(x * levels / 3), np.floor(y * levels / 3)
+    y = 0.4 * x + y
+    full, pair = _full_vec(x, y), R._kendall_tau_a(x, y)[0]
+    assert full == pair or (math.isnan(full) and math.isnan(pair)), (full, pair)
+    assert _close(full, O._kendall_tau_a(x, y)[0], 1e-15)
+
+
+def test_full_vec_edge_cases(dev):
+    assert math.isnan(_full_vec([0.0, 1.0, 2.0], [1.0, 1.0, 1.0]))  # constant y: tot == ytie
+    assert math.isnan(_full_vec([1.0, np.nan, 3.0], [0.0, 1.0, 2.0]))
+    x = np.array([0.0, -0.0, 1.0, 2.0, 2.0, -5e-324, 5e-324, 1e308, -np.inf, np.inf])
+    y = np.array([1.0, 2.0, 2.0, 3.0, 1.0, 0.0, 0.0, -1.0, 4.0, 4.0])
+    assert _full_vec(x, y) == R._kendall_tau_a(x, y)[0]
+    assert _close(_full_vec(x, y), O._kendall_tau_a(x, y)[0], 1e-15)
+
+
+def test_full_vec_beyond_the_pairwise_cap(dev):
+    # the reference's _kendall_tau_a has no length cap (scipy's merge sort): 5,000,000 elements
+    # (> 2^22, the pairwise kernel's old limit) with ties, through rsa._kendall_tau_a, device
+    # tensors kept on the device, vs scipy
+    r = np.random.RandomState(11)
+    x = np.floor(r.randn(5_000_000) * 3000).astype(np.float32)
+    y = (0.3 * x + np.floor(r.randn(x.size) * 2000)).astype(np.float32)
+    got = R._kendall_tau_a(torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev))[0]
+    ref = O._kendall_tau_a(x.astype(np.float64), y.astype(np.float64))[0]
+    assert _close(got, ref, 1e-15), (got, ref)
+
+
+@pytest.mark.parametrize("n,levels", [(3000, None), (3000, 50), (20000, None)])
+def test_full_triangle_equals_plan_path(dev, n, levels):
+    # vr_kendall_full_f32 (the path above 65,535 stimuli) against the rank-plan Kendall on the
+    # same RDMs: both exact integer counts, bit for bit; and the oracle at n = 3000
+    from visreps_amd._lib import check, lib, stream_of, workspace
+
+    g = torch.Generator(device=dev).manual_seed(n + (levels or 0))
+    a = R.compute_rdm(torch.randn(n, 48, device=dev, generator=g))
+    b = R.compute_rdm(torch.relu(torch.randn(n, 64, device=dev, generator=g)))
+    if levels:
+        a = (a * levels).floor() / levels
+    L = lib()
+    out = torch.empty(1, dtype=torch.float64, device=dev)
+    ws = workspace.get(dev, L.vr_kendall_full_workspace(n), "kendall_full")
+    check(L.vr_kendall_full_f32(a.data_ptr(), b.data_ptr(), n, n, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                stream_of(dev)), "vr_kendall_full_f32")
+    full = float(out.item())
+    plan = R.compute_rdm_correlation(a, b, correlation="Kendall")
+    assert full == plan, (full, plan)
+    if n <= 3000:
+        assert _close(full, O.compute_rdm_correlation(a.cpu().numpy(), b.cpu().numpy(), "Kendall"))
+
+
+def test_full_triangle_73k_properties(dev):
+    # configs[2]'s size (73,000 stimuli, 2.66e9 pairs), beyond the rank plans: exact
+    # properties of the statistic (the arithmetic is pinned to the plan path and scipy above):
+    # tau(A, 2A) == tau(A, A) (same order and ties), tau(A, -A) == -tau(A, A) bit for bit
+    # (every untied pair discordant), 0 < tau(A, B) < tau(A, A) for a partly reordered B
+    import time
+
+    n = 73000
+    g = torch.Generator(device=dev).manual_seed(73)
+    z = torch.randn(n, 32, device=dev, generator=g)
+    a = R.compute_rdm(z + 0.5 * torch.randn(n, 32, device=dev, generator=g))
+    t0 = time.perf_counter()
+    taa = R.compute_rdm_correlation(a, a, correlation="Kendall")
+    dt = time.perf_counter() - t0
+    assert 0.99 < taa <= 1.0
+    assert R.compute_rdm_correlation(a, a * 2, correlation="Kendall") == taa
+    neg = -a
+    assert R.compute_rdm_correlation(a, neg, correlation="Kendall") == -taa
+    del neg
+    b = R.compute_rdm(z + 0.5 * torch.randn(n, 32, device=dev, generator=g))
+    del z
+    tab = R.compute_rdm_correlation(a, b, correlation="Kendall")
+    assert 0.0 < tab < taa
+    from conftest import record_margin
+    record_margin("kendall_full_73k", n=n, pairs=n * (n - 1) // 2, tau_aa=taa, tau_ab=tab, seconds_first_call=dt)

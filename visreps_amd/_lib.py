@@ -137,6 +137,10 @@ _PROTOTYPES = {
     ),
     "vr_kendall_vec_workspace": (_c_sz, [_c_i64]),
     "vr_kendall_tau_a_f64": (ctypes.c_int, [_vp, _vp, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "vr_kendall_full_vec_workspace": (_c_sz, [_c_i64]),
+    "vr_kendall_full_vec_f64": (ctypes.c_int, [_vp, _vp, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "vr_kendall_full_workspace": (_c_sz, [_c_i64]),
+    "vr_kendall_full_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
     "vr_bootstrap_kendall_workspace": (_c_sz, [_c_i64, _c_i64]),
     "vr_bootstrap_kendall_plans": (
         ctypes.c_int,

@@ -411,31 +411,46 @@ def percentile(scores: np.ndarray, q: float) -> float:
 # -----------------------------------------------------------------------------
 # RDM comparison
 # -----------------------------------------------------------------------------
+_KENDALL_PAIRWISE_MAX = 1 << 16  # longer vectors: the O(m log m) sort path
+
+
+def _vec_f64(v, dev: torch.device) -> torch.Tensor:
+    if isinstance(v, torch.Tensor):
+        return v.detach().reshape(-1).to(device=dev, dtype=torch.float64).contiguous()
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel())).to(dev)
+
+
 def _kendall_tau_a(x, y) -> tuple:
     """Kendall tau-a of two 1-D arrays, returned as (tau_a, nan) (rsa.py:22-40).
 
     The reference takes scipy's tau-b and rescales it by sqrt((n0 - t_x)(n0 - t_y)) / n0.
-    Here vr_kendall_tau_a_f64 compares every pair in fp64 with exact integer discordant and
-    tie counts, then applies the same fp64 conversion. The result is NaN for fewer than two
-    elements, for any NaN element and for a constant input. Arrays of unequal length raise
-    ValueError, as scipy.stats.kendalltau does."""
-    xa = np.asarray(x.detach().cpu() if isinstance(x, torch.Tensor) else x, dtype=np.float64).ravel()
-    ya = np.asarray(y.detach().cpu() if isinstance(y, torch.Tensor) else y, dtype=np.float64).ravel()
-    if xa.size != ya.size:
-        raise ValueError("All inputs to `kendalltau` must be of the same size, found x-size %d and y-size %d"
-                         % (xa.size, ya.size))
-    m = int(xa.size)
-    if m < 2:
+    Here the discordant and tie counts are exact integers -- every pair compared in fp64 up to
+    2^16 elements (vr_kendall_tau_a_f64), beyond that the O(m log m) sort-and-inversion form
+    (vr_kendall_full_vec_f64, any length < 2^32; both give the same bits) -- then the same fp64
+    conversion. NaN for fewer than two elements, any NaN element or a constant input; arrays of
+    unequal length raise ValueError, as scipy.stats.kendalltau does. Tensors already on a HIP
+    device are used there; host arrays go to the current device."""
+    nx = int(x.numel()) if isinstance(x, torch.Tensor) else int(np.size(x))
+    ny = int(y.numel()) if isinstance(y, torch.Tensor) else int(np.size(y))
+    if nx < 2:  # rsa.py:24-26 checks len(x) before scipy sees y
         return (float("nan"), float("nan"))
-    dev = _device_for()
-    xd = torch.from_numpy(np.ascontiguousarray(xa)).to(dev)
-    yd = torch.from_numpy(np.ascontiguousarray(ya)).to(dev)
+    if nx != ny:
+        raise ValueError("All inputs to `kendalltau` must be of the same size, found x-size %d and y-size %d"
+                         % (nx, ny))
+    m = nx
+    dev = _device_for(x, y)
+    xd, yd = _vec_f64(x, dev), _vec_f64(y, dev)
     out = torch.empty(1, dtype=torch.float64, device=dev)
     L = lib()
-    ws = workspace.get(dev, L.vr_kendall_vec_workspace(m), "kendall_vec")
     with torch.cuda.device(dev):
-        check(L.vr_kendall_tau_a_f64(_ptr(xd), _ptr(yd), m, _ptr(out), _ptr(ws), ws.numel(), stream_of(dev)),
-              "vr_kendall_tau_a_f64")
+        if m <= _KENDALL_PAIRWISE_MAX:
+            ws = workspace.get(dev, L.vr_kendall_vec_workspace(m), "kendall_vec")
+            check(L.vr_kendall_tau_a_f64(_ptr(xd), _ptr(yd), m, _ptr(out), _ptr(ws), ws.numel(), stream_of(dev)),
+                  "vr_kendall_tau_a_f64")
+        else:
+            ws = workspace.get(dev, L.vr_kendall_full_vec_workspace(m), "kendall_full")
+            check(L.vr_kendall_full_vec_f64(_ptr(xd), _ptr(yd), m, _ptr(out), _ptr(ws), ws.numel(),
+                                            stream_of(dev)), "vr_kendall_full_vec_f64")
     return (float(out.item()), float("nan"))
 
 
@@ -477,6 +492,13 @@ def compute_rdm_correlation(
                 L.vr_spearman_triu_f32(_ptr(a), _ptr(b), n, a.stride(0), _ptr(out),
                                        _ptr(ws), ws.numel(), stream_of(dev)),
                 "vr_spearman_triu_f32",
+            )
+        elif corr == "kendall" and n > 65535:  # beyond the rank plans: the sort-and-inversion path
+            ws = workspace.get(dev, L.vr_kendall_full_workspace(n), "kendall_full")
+            check(
+                L.vr_kendall_full_f32(_ptr(a), _ptr(b), n, a.stride(0), _ptr(out),
+                                      _ptr(ws), ws.numel(), stream_of(dev)),
+                "vr_kendall_full_f32",
             )
         elif corr == "kendall":
             ws = workspace.get(dev, L.vr_kendall_triu_workspace(n), "kendall_triu")

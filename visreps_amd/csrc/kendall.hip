@@ -659,7 +659,25 @@ static int group_index(const PlanView& P, int64_t M, const KendallWs& W, uint32_
 struct KSide {
   hipStream_t sp = nullptr;
   hipEvent_t masks = nullptr, in = nullptr, prep[2] = {nullptr, nullptr}, walked[2] = {nullptr, nullptr};
+  hipEvent_t done = nullptr;
   std::mutex mu;
+};
+
+// The caller's stream waits for everything enqueued on the side stream, on every way out of
+// run_kendall -- an error return included -- so no side-stream kernel can still be writing
+// the caller's workspace when the next call on it starts.
+struct KSideJoin {
+  hipStream_t sp, st;
+  hipEvent_t ev;
+  bool armed = true;
+  int join() {
+    if (!armed) return VR_OK;
+    armed = false;
+    VR_CHECK_HIP(hipEventRecord(ev, sp));
+    VR_CHECK_HIP(hipStreamWaitEvent(st, ev, 0));
+    return VR_OK;
+  }
+  ~KSideJoin() { (void)join(); }
 };
 static int kendall_side(KSide*& out) {
   static KSide sides[64];
@@ -671,7 +689,7 @@ static int kendall_side(KSide*& out) {
   std::lock_guard<std::mutex> g(init_mu);
   if (!k.sp) {
     VR_CHECK_HIP(hipStreamCreateWithFlags(&k.sp, hipStreamNonBlocking));
-    hipEvent_t* evs[] = {&k.masks, &k.in, &k.prep[0], &k.prep[1], &k.walked[0], &k.walked[1]};
+    hipEvent_t* evs[] = {&k.masks, &k.in, &k.prep[0], &k.prep[1], &k.walked[0], &k.walked[1], &k.done};
     for (hipEvent_t* e : evs) VR_CHECK_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   out = &k;
@@ -716,6 +734,7 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
   VR_TRY(kendall_side(side));
   std::unique_lock<std::mutex> side_lock(side->mu);
   hipStream_t sp = side->sp;
+  KSideJoin side_join{sp, st, side->done};  // (destroyed before side_lock: still under the lock)
   // masks of every pass, totals zeroed
   for (int64_t set0 = 0, p = 0; set0 < total; set0 += LANES, ++p) {
     const int nl = (int)std::min<int64_t>(LANES, total - set0);
@@ -791,6 +810,7 @@ static int run_kendall(const PlanView& A, const PlanView& B, int64_t n, const in
                          cap, cfg, st));
     VR_CHECK_HIP(hipEventRecord(side->walked[c], st));
   }
+  VR_TRY(side_join.join());
   side_lock.unlock();
   k_kfinal<<<blocks_for(total, 256), 256, 0, st>>>(W.tot, cap, total, scores);
   VR_CHECK_LAUNCH();
