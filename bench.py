@@ -383,9 +383,9 @@ def _rdm_timed(x, reps: int = 1):
     return rdm, e0.elapsed_time(e1) / reps, (wide_ms + tile_ms) / reps, (wide_n + tile_n) / reps
 
 
-def _gram_roof(n: int, d: int, call_ms: float, gram_ms: float) -> dict:
+def _gram_roof(n: int, d: int, call_ms: float, gram_ms: float, products: int = 3) -> dict:
     flops = float(n) * (n + 1) * d
-    split_peak = BF16_MFMA_PEAK_TF / 3
+    split_peak = BF16_MFMA_PEAK_TF / products
     tf_call = flops / (call_ms / 1e3) / 1e12
     tf_gram = flops / (gram_ms / 1e3) / 1e12 if gram_ms else 0.0
     return {"bound": "mfma", "achieved": round(tf_call, 2), "peak": round(split_peak, 1), "unit": "TFLOP/s",
@@ -396,7 +396,9 @@ def _gram_roof(n: int, d: int, call_ms: float, gram_ms: float) -> dict:
             "peak_note": ("split ceiling = bf16 dense peak 2516.6 / 3: every k-step is 3 bf16 MFMA products "
                           "(hi hi + hi lo + lo hi of the centred fp32 values, as the reference centres in fp32 "
                           "before its matmul, rsa.py:76-90); frac_of_bf16_dense_peak = algorithmic FLOPs / the bf16 dense "
-                          "peak itself (MFMA busy = 3 x that)")}
+                          "peak itself (MFMA busy = 3 x that)") if products == 3 else
+                         ("one product per k (bf16 features: x_i x_j exact in fp32, the centring a rank-1 "
+                          "correction in the epilogue): peak = the bf16 dense peak 2516.6")}
 
 
 def configs4_leg(dev) -> dict:
@@ -413,18 +415,30 @@ def configs4_leg(dev) -> dict:
     for name, d, reps in (("vit_b16_block", 151296, 1), ("clip_vit_l14", 768, 5)):
         _free_device(dev)
         x = _latent_features(dev, n, d, seed=d, dtype=torch.bfloat16, relu=False)
-        rdm, call_ms, gram_ms, launches = _rdm_timed(x, reps)
+        rows = torch.randperm(n, device=dev, generator=torch.Generator(device=dev).manual_seed(3))[:64]
+        rdm, call_ms, gram_ms, launches = _rdm_timed(x, reps)  # default: one product per k
         ok = bool(torch.all(torch.diagonal(rdm) == 0)) and bool(torch.isfinite(rdm[:64]).all())
-        del rdm, x
-        e = {"n": n, "d": d, "dtype": "bf16 features (rsa.py:76 widens to fp32; split-Gram kernels)",
+        sample = rdm[rows].clone()
+        del rdm
+        os.environ["VISREPS_GRAM_ONE"] = "0"  # the split (hi/lo, 3 products) form, for comparison
+        try:
+            rdm3, call3_ms, gram3_ms, _ = _rdm_timed(x, reps)
+        finally:
+            os.environ.pop("VISREPS_GRAM_ONE", None)
+        diff = float((rdm3[rows] - sample).abs().max())
+        del rdm3, x
+        e = {"n": n, "d": d, "dtype": "bf16 features (rsa.py:76 widens to fp32): one bf16 product per k, centring "
+                                      "as a rank-1 correction in the epilogue",
              "rdm_ms": round(call_ms, 2), "gram_ms": round(gram_ms, 2), "gram_launches": launches,
-             "sane": ok}
-        e["roofline"] = _gram_roof(n, d, call_ms, gram_ms)
+             "sane": ok, "split_form": {"rdm_ms": round(call3_ms, 2), "gram_ms": round(gram3_ms, 2),
+                                        "roofline": _gram_roof(n, d, call3_ms, gram3_ms, 3),
+                                        "max_abs_rdm_diff_vs_one_product_64_rows": diff}}
+        e["roofline"] = _gram_roof(n, d, call_ms, gram_ms, 1)
         out[name] = e
     _free_device(dev)
     out["note"] = ("one RDM per shape after a warm call; rdm_ms = HIP events around compute_rdm (row statistics "
-                   "+ split prepass + Gram + epilogue), gram_ms = the Gram kernels alone (vr_ktimer); outside "
-                   "the timed steps")
+                   "+ prepass + Gram + epilogue), gram_ms = the Gram kernels alone (vr_ktimer); split_form = the "
+                   "same RDM with VISREPS_GRAM_ONE=0 (the round-5 hi/lo kernel); outside the timed steps")
     return out
 
 

@@ -302,6 +302,11 @@ int vr_kendall_full_vec_f64(const double* x, const double* y, int64_t m, double*
 size_t vr_kendall_full_workspace(int64_t n);
 int vr_kendall_full_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out, void* ws,
                         size_t ws_bytes, void* stream);
+/* ... of the sub-RDMs A[idx][:, idx], B[idx][:, idx] (k rows idx [dev] int32 into the n x n
+ * RDMs, never materialised): one bootstrap draw of evals.py:361-369 with compare_method=kendall
+ * beyond the rank plans. Workspace: vr_kendall_full_workspace(k). */
+int vr_kendall_full_subset_f32(const float* A, const float* B, int64_t n, int64_t ld, const int32_t* idx,
+                               int64_t k, double* out, void* ws, size_t ws_bytes, void* stream);
 
 /* Bootstrapped Kendall RSA on two rank plans: the bootstrap loop of evals.py:355-373 /
  * rsa.py:233-261 with compare_method="kendall". Arguments as
@@ -334,6 +339,12 @@ int vr_srp_csr_f32(const int32_t* indptr, const int32_t* indices, const float* v
 size_t vr_spearman_full_workspace(int64_t n);
 int vr_spearman_full_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out,
                          void* ws, size_t ws_bytes, void* stream);
+/* ... of the sub-RDMs A[idx][:, idx], B[idx][:, idx] (k rows idx [dev] int32, never
+ * materialised): one bootstrap draw of evals.py:361-369 beyond the rank plans' n <= 65,535
+ * (the bootstrap engine's per-pass TB rows would need 128 B per pair: 341 GB at 73k).
+ * Workspace: vr_spearman_full_workspace(k). */
+int vr_spearman_full_subset_f32(const float* A, const float* B, int64_t n, int64_t ld, const int32_t* idx,
+                                int64_t k, double* out, void* ws, size_t ws_bytes, void* stream);
 /* Local pieces of the distributed global rank (sample sort over ranks,
  * visreps_amd/analysis/distributed_spearman.py): sortable keys of fp32 values, an in-place
  * (key, value) radix sort, doubled midranks (+ 2 base) of a sorted key run with its tie

@@ -496,3 +496,90 @@ def test_sort_pairs_stable_vs_numpy(dev, m, dist):
     order = np.argsort(k, kind="stable")
     np.testing.assert_array_equal(ks.cpu().numpy().view(np.uint32), k[order])
     np.testing.assert_array_equal(vs.cpu().numpy().view(np.uint32), v[order])
+
+
+# ------------------------------------------------- bootstrap beyond the rank plans (n > 65,535)
+def test_bootstrap_full_equals_engine(dev):
+    # the plan-free per-draw path (bootstrap_full: sub-RDMs read in place) against the rank-plan
+    # engines on the same RDMs and RandomState(42) draws: exact integer statistics, bit for bit,
+    # Spearman and Kendall
+    from visreps_amd.analysis._random import bootstrap_indices
+
+    n = 2500
+    g = torch.Generator(device=dev).manual_seed(5)
+    z = torch.randn(n, 16, device=dev, generator=g)
+    a = R.compute_rdm(torch.relu(z @ torch.randn(16, 80, device=dev, generator=g) + torch.randn(n, 80, device=dev,
+                                                                                            generator=g)))
+    b = R.compute_rdm(z + torch.randn(n, 16, device=dev, generator=g))
+    idx = bootstrap_indices(42, n, int(0.9 * n), 12)
+    for method in ("spearman", "kendall"):
+        full = R.bootstrap_full(a, b, idx, method=method).cpu().numpy()
+        eng = R._ENGINES[method](R.RankPlan(a), R.RankPlan(b), idx, full_first=True).cpu().numpy()
+        assert np.array_equal(full, eng), method
+
+
+def test_bootstrap_rsa_beyond_rank_plans(dev):
+    # n = 70,000 (> 65,535): bootstrap_rsa runs the per-draw plan-free path; a draw's score equals
+    # spearman_full on the explicitly materialised sub-RDMs A[idx][:, idx] (the reference's
+    # evals.py:362-364 indexing), the point equals spearman_full on the whole RDMs
+    from visreps_amd.analysis._random import bootstrap_indices
+
+    n = 70000
+    g = torch.Generator(device=dev).manual_seed(70)
+    z = torch.randn(n, 24, device=dev, generator=g)
+    a = R.compute_rdm(z + 0.7 * torch.randn(n, 24, device=dev, generator=g))
+    b = R.compute_rdm(z + 0.7 * torch.randn(n, 24, device=dev, generator=g))
+    del z
+    idx = bootstrap_indices(42, n, int(0.9 * n), 2)
+    point, scores, lo, hi = R.bootstrap_rsa(a, b, idx=idx)
+    assert point == R.spearman_full(a, b)
+    i = torch.as_tensor(idx[1], dtype=torch.long, device=dev)
+    sa = a[i][:, i]
+    sb = b[i][:, i]
+    assert scores[1] == R.spearman_full(sa, sb)
+    assert lo <= hi and 0.0 < point < 1.0
+
+
+# ------------------------------------------- bf16 features: one MFMA product per k (configs[4])
+def _rdm_rows_f64(x, rows):
+    xd = x.double()
+    xd = xd - xd.mean(1, keepdim=True)
+    s = torch.sqrt((xd * xd).mean(1) + 1e-12)
+    g = xd[rows] @ xd.T / x.size(1)
+    out = 1.0 - (g / (s[rows, None] * s[None, :] + 1e-12)).clamp(-1, 1)
+    out[torch.arange(len(rows), device=x.device), rows] = 0.0
+    return out
+
+
+@pytest.mark.parametrize("n,d", [(3000, 4128), (700, 768), (1300, 50000)])
+def test_bf16_one_product_rdm(dev, n, d, monkeypatch):
+    # bf16 rows: sum x_i x_j on one bf16 MFMA product per k (exact products, fp32 accumulation)
+    # and the centring as the epilogue's rank-1 correction; against fp64 rows it must do no
+    # worse than the split (hi/lo, 3 products) kernel or the exact-fp32 kernel (the parity bar of
+    # tests/test_benchsize.py::test_cfg5_*); exact symmetry and zero diagonal; rows whose mean is
+    # large against their spread (mean^2 > 4 var) send the call to the split records, bit-equal
+    # to VISREPS_GRAM_ONE=0
+    g = torch.Generator(device=dev).manual_seed(n + d)
+    z = torch.randn(n, 32, device=dev, generator=g)
+    x = (z @ torch.randn(32, d, device=dev, generator=g) / 4 + torch.randn(n, d, device=dev, generator=g)).to(
+        torch.bfloat16)
+    rows = torch.randperm(n, device=dev, generator=g)[:48]
+    ref = _rdm_rows_f64(x.float(), rows)
+    one = R.compute_rdm(x)
+    monkeypatch.setenv("VISREPS_GRAM_ONE", "0")
+    split = R.compute_rdm(x)
+    monkeypatch.setenv("VISREPS_GRAM", "fp32")
+    fp32 = R.compute_rdm(x.float())
+    monkeypatch.delenv("VISREPS_GRAM")
+    e1 = float((one[rows].double() - ref).abs().max())
+    e3 = float((split[rows].double() - ref).abs().max())
+    e32 = float((fp32[rows].double() - ref).abs().max())
+    from conftest import record_margin
+    record_margin("bf16_one_product_rdm", n=n, d=d, err_one=e1, err_split=e3, err_fp32=e32)
+    assert e1 <= max(5e-6, e3, e32), (e1, e3, e32)
+    assert torch.all(torch.diagonal(one) == 0) and torch.equal(one, one.T)
+    # large means: the split records (flag), the same bits as forcing them
+    xm = (x.float() + 8.0).to(torch.bfloat16)
+    forced = R.compute_rdm(xm)
+    monkeypatch.delenv("VISREPS_GRAM_ONE")
+    assert torch.equal(R.compute_rdm(xm), forced)

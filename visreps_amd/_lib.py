@@ -163,6 +163,8 @@ _PROTOTYPES = {
     "vr_gram64_f32": (ctypes.c_int, [_vp, _c_i64, _c_i64, _c_i64, ctypes.c_int, _vp, _c_i64, _vp, _c_sz, _vp]),
     "vr_spearman_full_workspace": (_c_sz, [_c_i64]),
     "vr_spearman_full_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "vr_spearman_full_subset_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _c_sz, _vp]),
+    "vr_kendall_full_subset_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _c_sz, _vp]),
     "vr_f32_sort_keys": (ctypes.c_int, [_vp, _c_i64, _vp, _vp]),
     "vr_sort_pairs_workspace": (_c_sz, [_c_i64]),
     "vr_sort_pairs_u32": (ctypes.c_int, [_vp, _vp, _c_i64, _vp, _c_sz, _vp]),

@@ -43,6 +43,7 @@ __all__ = [
     "bootstrap_spearman_multi",
     "bootstrap_spearman_grid",
     "bootstrap_kendall",
+    "bootstrap_full",
     "spearman_full",
     "percentile",
     "_rank",
@@ -400,6 +401,52 @@ def bootstrap_kendall(
 
 
 _ENGINES = {"spearman": bootstrap_spearman, "kendall": bootstrap_kendall}
+PLAN_MAX_N = 65535  # rank plans (and the bootstrap engines on them) use 16-bit stimulus indices
+
+
+def bootstrap_full(
+    model_rdm: torch.Tensor,
+    neural_rdm: torch.Tensor,
+    idx: Optional[np.ndarray | torch.Tensor],
+    *,
+    method: str = "spearman",
+    full_first: bool = True,
+) -> torch.Tensor:
+    """The bootstrap of evals.py:355-373 for RDMs beyond the rank plans (n > 65,535, where the
+    engines' 128-B rank rows would need 341 GB at 73k): per draw one plan-free call on the
+    sub-RDMs A[idx][:, idx], B[idx][:, idx], read in place (vr_spearman_full_subset_f32 /
+    vr_kendall_full_subset_f32: radix sorts, exact integer statistics, so every score equals
+    the rank-plan engines' where both run). float64 scores on the device, the full set first
+    when full_first. Works at any n with n(n-1)/2 < 2^32."""
+    method = method.lower()
+    if method not in _ENGINES:
+        raise ValueError(f"bootstrap engine for compare_method={method!r}: spearman or kendall")
+    dev = _device_for(model_rdm, neural_rdm)
+    a, b = _as_device_f32(model_rdm, dev), _as_device_f32(neural_rdm, dev)
+    if a.shape != b.shape or a.ndim != 2 or a.size(0) != a.size(1):
+        raise ValueError("RDMs must share the same square 2-D shape")
+    if a.stride(0) != b.stride(0):
+        a, b = a.contiguous(), b.contiguous()
+    n = a.size(0)
+    idx_t = _idx_tensor(idx, dev)
+    n_sets, k = (int(idx_t.size(0)), int(idx_t.size(1))) if idx_t.numel() else (0, 0)
+    total = n_sets + (1 if full_first else 0)
+    scores = torch.empty(total, dtype=torch.float64, device=dev)
+    L = lib()
+    spear = method == "spearman"
+    ws = workspace.get(dev, (L.vr_spearman_full_workspace if spear else L.vr_kendall_full_workspace)(n),
+                       "spearman_full" if spear else "kendall_full")
+    st = stream_of(dev)
+    with torch.cuda.device(dev):
+        if full_first:
+            fn = L.vr_spearman_full_f32 if spear else L.vr_kendall_full_f32
+            check(fn(_ptr(a), _ptr(b), n, a.stride(0), _ptr(scores), _ptr(ws), ws.numel(), st), fn.__name__)
+        sub = L.vr_spearman_full_subset_f32 if spear else L.vr_kendall_full_subset_f32
+        off = 1 if full_first else 0
+        for i in range(n_sets):
+            check(sub(_ptr(a), _ptr(b), n, a.stride(0), _ptr(idx_t[i]), k, _ptr(scores[off + i:]), _ptr(ws),
+                      ws.numel(), st), sub.__name__)
+    return scores
 
 
 def percentile(scores: np.ndarray, q: float) -> float:
@@ -565,12 +612,15 @@ def bootstrap_rsa(
     engine = _ENGINES.get(method.lower())
     if engine is None:
         raise ValueError(f"bootstrap engine for compare_method={method!r}: spearman or kendall")
-    pa = model_rdm if isinstance(model_rdm, RankPlan) else RankPlan(model_rdm)
-    pb = neural_rdm if isinstance(neural_rdm, RankPlan) else RankPlan(neural_rdm)
-    n = pa.n
+    n = model_rdm.n if isinstance(model_rdm, RankPlan) else int(model_rdm.shape[0])
     if idx is None:
         idx = bootstrap_indices(seed, n, int(n * 0.9), int(n_bootstrap)) if n_bootstrap else None
-    scores = engine(pa, pb, idx, full_first=True).cpu().numpy()
+    if n > PLAN_MAX_N and not isinstance(model_rdm, RankPlan):  # beyond the rank plans
+        scores = bootstrap_full(model_rdm, neural_rdm, idx, method=method, full_first=True).cpu().numpy()
+    else:
+        pa = model_rdm if isinstance(model_rdm, RankPlan) else RankPlan(model_rdm)
+        pb = neural_rdm if isinstance(neural_rdm, RankPlan) else RankPlan(neural_rdm)
+        scores = engine(pa, pb, idx, full_first=True).cpu().numpy()
     point, boot = float(scores[0]), scores[1:].copy()
     if boot.size == 0:
         return point, boot, float("nan"), float("nan")
@@ -622,7 +672,7 @@ def compute_rsa(
 
     neural_rdm_sel = compute_rdm(_index_rows(selection.neural, sel_idx))
     engine = _ENGINES.get(method)
-    sel_plan = RankPlan(neural_rdm_sel) if engine is not None and n_sel > 1 else None
+    sel_plan = RankPlan(neural_rdm_sel) if engine is not None and 1 < n_sel <= PLAN_MAX_N else None
 
     selection_scores = []
     best_layer, best_score = None, -float("inf")
@@ -659,13 +709,16 @@ def compute_rsa(
     ci_low, ci_high = None, None
     bootstrap_scores_list = None
     if engine is not None and n_test > 1:
-        plan_m, plan_n = RankPlan(test_model_rdm), RankPlan(test_neural_rdm)
         boot_idx = None
         if bootstrap and n_bootstrap > 0:
             k = int(n_test * 0.9)
             boot_idx = np.stack([rng.choice(n_test, size=k, replace=False)
                                  for _ in range(n_bootstrap)]).astype(np.int32)
-        scores = engine(plan_m, plan_n, boot_idx, full_first=True).cpu().numpy()
+        if n_test > PLAN_MAX_N:  # beyond the rank plans: one plan-free call per draw
+            scores = bootstrap_full(test_model_rdm, test_neural_rdm, boot_idx, method=method).cpu().numpy()
+        else:
+            plan_m, plan_n = RankPlan(test_model_rdm), RankPlan(test_neural_rdm)
+            scores = engine(plan_m, plan_n, boot_idx, full_first=True).cpu().numpy()
         point_estimate = float(scores[0])
         if math.isnan(point_estimate):
             logger.warning("NaN returned for %s correlation", method.capitalize())

@@ -82,6 +82,23 @@ __global__ void k_kf_tri_keys(const float* __restrict__ A, const float* __restri
   }
 }
 
+// the same for the sub-RDMs A[idx][:, idx], B[idx][:, idx] (a bootstrap draw, never materialised)
+__global__ void k_kf_tri_keys_sub(const float* __restrict__ A, const float* __restrict__ B,
+                                  const int32_t* __restrict__ idx, int64_t k, int64_t ld, uint32_t* __restrict__ kx,
+                                  uint32_t* __restrict__ ky, uint32_t* __restrict__ nan) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= k) return;
+  const int64_t cb = idx[b];
+  for (int64_t a = blockIdx.y; a < b; a += gridDim.y) {
+    const int64_t o = (int64_t)idx[a] * ld + cb;
+    const float x = A[o], y = B[o];
+    if (x != x || y != y) *nan = 1u;
+    const uint64_t t = tri_index((uint64_t)a, (uint64_t)b, (uint64_t)k);
+    kx[t] = f32_sort_key(x);
+    ky[t] = f32_sort_key(y);
+  }
+}
+
 // f64 -> ascending-order u64 split in (hi, lo); -0.0 as +0.0 (they tie in scipy)
 __global__ void k_kf_keys64(const double* __restrict__ v, int64_t m, uint32_t* __restrict__ hi,
                             uint32_t* __restrict__ lo, uint32_t* __restrict__ nan) {
@@ -391,6 +408,9 @@ static int kf_nan_out(double* out, hipStream_t st) {
 
 using namespace vr;
 
+static int kendall_full_impl(const float* A, const float* B, int64_t n, int64_t ld, const int32_t* idx, double* out,
+                             void* ws, size_t ws_bytes, hipStream_t st);
+
 extern "C" {
 
 size_t vr_kendall_full_vec_workspace(int64_t m) {
@@ -427,8 +447,22 @@ size_t vr_kendall_full_workspace(int64_t n) {
 int vr_kendall_full_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out, void* ws,
                         size_t ws_bytes, void* stream) {
   VR_REQUIRE(n >= 0 && ld >= n && out, "vr_kendall_full_f32: bad shape n=%lld ld=%lld", (long long)n, (long long)ld);
+  return kendall_full_impl(A, B, n, ld, nullptr, out, ws, ws_bytes, as_stream(stream));
+}
+
+int vr_kendall_full_subset_f32(const float* A, const float* B, int64_t n, int64_t ld, const int32_t* idx, int64_t k,
+                               double* out, void* ws, size_t ws_bytes, void* stream) {
+  VR_REQUIRE(n >= 0 && ld >= n && k >= 0 && k <= n && out, "vr_kendall_full_subset_f32: bad shape n=%lld ld=%lld "
+             "k=%lld", (long long)n, (long long)ld, (long long)k);
+  VR_REQUIRE(idx != nullptr || k == 0, "vr_kendall_full_subset_f32: null idx");
+  return kendall_full_impl(A, B, k, ld, idx, out, ws, ws_bytes, as_stream(stream));
+}
+
+}  // extern "C"
+
+static int kendall_full_impl(const float* A, const float* B, int64_t n, int64_t ld, const int32_t* idx, double* out,
+                             void* ws, size_t ws_bytes, hipStream_t st) {
   VR_REQUIRE(pairs_of(n) < ((int64_t)1 << 32), "vr_kendall_full_f32: n=%lld has 2^32 or more pairs", (long long)n);
-  hipStream_t st = as_stream(stream);
   const int64_t M = pairs_of(n);
   if (M < 2) return kf_nan_out(out, st);
   VR_REQUIRE(A && B, "vr_kendall_full_f32: null pointer");
@@ -440,9 +474,10 @@ int vr_kendall_full_f32(const float* A, const float* B, int64_t n, int64_t ld, d
   }
   VR_CHECK_HIP(hipMemsetAsync(w.nan, 0, sizeof(uint32_t), st));
   const dim3 grid((unsigned)((n + 255) / 256), (unsigned)std::min<int64_t>(n, 16384));
-  k_kf_tri_keys<<<grid, 256, 0, st>>>(A, B, n, ld, w.kx, w.ky, w.nan);
+  if (idx)
+    k_kf_tri_keys_sub<<<grid, 256, 0, st>>>(A, B, idx, n, ld, w.kx, w.ky, w.nan);
+  else
+    k_kf_tri_keys<<<grid, 256, 0, st>>>(A, B, n, ld, w.kx, w.ky, w.nan);
   VR_CHECK_LAUNCH();
   return kf_run(M, w, out, st);
 }
-
-}  // extern "C"

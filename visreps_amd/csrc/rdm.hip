@@ -132,6 +132,8 @@ struct GramParams {
   int raw;                 // 1: plain Gram X X^T (no centring, no correlation epilogue)
   int flush;               // k stages between accumulator flushes (0: none), see gram_flush
   float* fbuf;             // flush buffer: one tile of fp32 per block of a launch
+  int one;                 // bf16 input, one product: records hold raw x (64 k per stage), centring in the epilogue
+  int64_t dk;              // k extent in 32-k units the split-K geometry covers (d; 32 nstage when one)
 };
 
 // Accumulation error. Every MFMA rounds its output to fp32, so an accumulator that runs over
@@ -307,14 +309,25 @@ __device__ inline void store_panel(const GramParams& P, float* lds, int64_t row0
 
 // Epilogue for one element: rdm = 1 - clamp(G/d / (s_i s_j + c)), exactly the
 // reference's fp32 operation order; NaN propagates like torch.clamp.
-__device__ inline float rdm_value(float g, int64_t i, int64_t j, const GramParams& P,
-                                  float si, float sj) {
+// ONE (one product, bf16 input): g = sum x_i x_j of the raw values; the centring is the
+// rank-1 correction cov = g/d - mean_i mean_j, in fp64, rounded once (then the reference's order)
+template <bool ONE>
+__device__ inline float rdm_value_t(float g, int64_t i, int64_t j, const GramParams& P,
+                                    float si, float sj) {
   if (P.raw) return g;  // vr_gram_f32
-  float cov = g / (float)P.d;
+  float cov;
+  if constexpr (ONE)
+    cov = (float)((double)g / (double)P.d -
+                  (double)(i < P.n ? P.mean[i] : 0.f) * (double)(j < P.n ? P.mean[j] : 0.f));
+  else
+    cov = g / (float)P.d;
   float c = cov / (si * sj + P.correction);
   c = (c < -1.f) ? -1.f : ((c > 1.f) ? 1.f : c);
   if (i == j) c = 1.f;
   return 1.f - c;
+}
+__device__ inline float rdm_value(float g, int64_t i, int64_t j, const GramParams& P, float si, float sj) {
+  return P.one ? rdm_value_t<true>(g, i, j, P, si, sj) : rdm_value_t<false>(g, i, j, P, si, sj);
 }
 
 // Tile epilogue (one 2x2 grid of 32x32 accumulators per wave). C/D map of the 32x32 MFMAs
@@ -605,6 +618,50 @@ __global__ __launch_bounds__(RSTAT_BS) void k_stats_split_multi(SplitMulti S, in
                          S.stdv[p], S.planes[p], blockIdx.x, lds);
 }
 
+// One-product prepass (bf16 input, vr_rdm_pearson_bf16): the row statistics as
+// stats_split_row computes them (fp64 sum -> fp32 mean; fp64 sum of squares of the
+// fp32-centred values -> std with the zero-variance guard) and raw stage records: record st
+// of a row holds its bf16 values k 64 st .. 64 st + 63 (exact zeros past d; rows >= n zero).
+// bf16 x bf16 products are exact in fp32, so one MFMA product per k gives sum x_i x_j; the
+// centring is the epilogue's rank-1 correction (rdm_value). That subtraction cancels digits
+// when a row's mean is large against its spread: *flag is set when mean^2 > 4 var for some
+// row, and the call then takes the split (centred hi/lo) records instead.
+__global__ __launch_bounds__(RSTAT_BS) void k_stats_one(const uint16_t* __restrict__ X, int64_t n, int64_t d,
+                                                        int64_t ldx, int64_t nstage1, float correction,
+                                                        float* __restrict__ mean, float* __restrict__ stdv,
+                                                        uint16_t* __restrict__ planes, uint32_t* __restrict__ flag) {
+  __shared__ double lds[RSTAT_BS / 64 + 1];
+  const int64_t r = blockIdx.x, kp = nstage1 * 64;
+  uint16_t* prow = planes + r * kp;
+  if (r >= n) {
+    for (int64_t k = threadIdx.x; k < kp; k += RSTAT_BS) prow[k] = 0;
+    return;
+  }
+  const uint16_t* row = X + r * ldx;
+  double s = 0;
+  for (int64_t k = threadIdx.x; k < kp; k += RSTAT_BS) {
+    const uint16_t v = k < d ? row[k] : (uint16_t)0;
+    prow[k] = v;
+    if (k < d) s += (double)in_f32(v);
+  }
+  s = block_sum_f64(s, lds);
+  const float m = (float)(s / (double)d);
+  double q = 0;
+  for (int64_t k = threadIdx.x; k < d; k += RSTAT_BS) {
+    const float a = in_f32(row[k]) - m;
+    q += (double)(a * a);
+  }
+  q = block_sum_f64(q, lds);
+  if (threadIdx.x == 0) {
+    const float var = (float)(q / (double)d);
+    float sd = sqrtf(var + correction);
+    if (sd < correction * 10.0f) sd = 1.0f;  // rsa.py:84-87 zero-variance guard
+    mean[r] = m;
+    stdv[r] = sd;
+    if ((double)m * (double)m > 4.0 * (double)var) *flag = 1u;  // benign race: every writer stores 1
+  }
+}
+
 template <typename T>
 static int stats_split(const T* X, int64_t n, int64_t rows, int64_t d, int64_t ldx, float correction,
                        float* mean, float* stdv, uint16_t* planes, hipStream_t st) {
@@ -634,6 +691,7 @@ __device__ inline void store_rec(uint16_t* lds, const u32x4 v[4]) {
   }
 }
 
+template <bool ONE>
 __global__ __launch_bounds__(G_THREADS, 2) void k_gram3(GramParams P) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * S_STAGE];  // [buf][A/B]
   const int nwg = gridDim.x;
@@ -644,7 +702,7 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram3(GramParams P) {
   const bool diag = (bi == bj);
   const int64_t row0 = (int64_t)bi * GT, col0 = (int64_t)bj * GT;
   const int64_t k0 = (int64_t)split * P.kslice;
-  const int64_t k1 = min(P.d, k0 + P.kslice);
+  const int64_t k1 = min(P.dk, k0 + P.kslice);
   const int64_t st0 = k0 / GK;
   const int ns = (int)((k1 - k0 + GK - 1) / GK);
 
@@ -694,16 +752,24 @@ __global__ __launch_bounds__(G_THREADS, 2) void k_gram3(GramParams P) {
 #pragma unroll
         for (int nn = 0; nn < 2; ++nn)
           acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[m], bH[nn], acc[m][nn], 0, 0, 0);
+      if constexpr (ONE) {  // the record's second half is k 32..63 of the raw row: one product more
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+        for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int nn = 0; nn < 2; ++nn)
-          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[m], bL[nn], acc[m][nn], 0, 0, 0);
+          for (int nn = 0; nn < 2; ++nn)
+            acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL[m], bL[nn], acc[m][nn], 0, 0, 0);
+      } else {
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+        for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int nn = 0; nn < 2; ++nn)
-          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL[m], bH[nn], acc[m][nn], 0, 0, 0);
+          for (int nn = 0; nn < 2; ++nn)
+            acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aH[m], bL[nn], acc[m][nn], 0, 0, 0);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int nn = 0; nn < 2; ++nn)
+            acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aL[m], bH[nn], acc[m][nn], 0, 0, 0);
+      }
     }
     if (more) {
       uint16_t* nxt = lds + (cur ^ 1) * 2 * S_STAGE;
@@ -1293,7 +1359,8 @@ __device__ inline void e_read_b(const char* half, int r0, const ELane& o, EFragB
 #define VR_E_PRIO 0  // 1: s_setprio(1) over each phase's MFMAs (A/B)
 #endif
 // quadrant (MA, NB) of the wave's block: 4 x 2 tiles of 16 x 16, hh, hl, lh products
-template <int MA, int NB>
+// ONE (bf16 input, raw records of 64 k): hi = k 0..31, lo = k 32..63 of the stage, 2 products
+template <int MA, int NB, bool ONE>
 __device__ inline void e_mfma(const EFragA& a, const EFragB& b, f32x4 (&acc)[8][4]) {
 #if VR_E_PRIO
   __builtin_amdgcn_s_setprio(1);
@@ -1304,6 +1371,18 @@ __device__ inline void e_mfma(const EFragA& a, const EFragB& b, f32x4 (&acc)[8][
     for (int n = 0; n < 2; ++n)
       acc[MA * 4 + m][NB * 2 + n] =
           __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi[m], b.hi[n], acc[MA * 4 + m][NB * 2 + n], 0, 0, 0);
+  if constexpr (ONE) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        acc[MA * 4 + m][NB * 2 + n] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo[m], b.lo[n], acc[MA * 4 + m][NB * 2 + n], 0, 0, 0);
+#if VR_E_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -1354,6 +1433,7 @@ __device__ inline void e_unflush(f32x4 (&acc)[8][4], const float* buf) {
 
 // Epilogue of the wave's 128 x 64 block (8 x 4 tiles of 16 x 16), as gram_store_w: a
 // diagonal super-tile writes each i < j entry from its (i, j) accumulator to both places.
+template <bool ONE>
 __device__ inline void e_store(const GramParams& P, f32x4 (&acc)[8][4], int64_t row0, int64_t col0, bool diag) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wr = wid >> 2, wc = wid & 3, g = lane >> 4, l16 = lane & 15;
@@ -1369,7 +1449,7 @@ __device__ inline void e_store(const GramParams& P, f32x4 (&acc)[8][4], int64_t 
       for (int e = 0; e < 4; ++e) {
         const int64_t i = ib + e;
         const float si = (i < P.n) ? P.stdv[i] : 1.f;
-        v[e] = rdm_value(acc[i8][j4][e], i, j, P, si, sj);
+        v[e] = rdm_value_t<ONE>(acc[i8][j4][e], i, j, P, si, sj);
       }
       if (diag) {
 #pragma unroll
@@ -1410,7 +1490,7 @@ __device__ inline void e_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool DIAG, bool ODD>
+template <bool DIAG, bool ODD, bool ONE>
 __device__ inline void e_stage(const GramParams& P, char* lds, int64_t row0, int64_t col0, int t, int ns,
                                const ELane& o, const uint32_t (&io)[2], EFragA& AX, EFragA& AY,
                                EFragB& BP, EFragB& BQ, f32x4 (&acc)[8][4]) {
@@ -1427,12 +1507,12 @@ __device__ inline void e_stage(const GramParams& P, char* lds, int64_t row0, int
   e_barrier();
   if (more1) e_issue(P, nxt, 1, row0, col0, t + 1, io);
   e_read_b(cur + hb * E_HALF, rb + 32, o, B1);
-  e_mfma<0, 0>(AX, B0, acc);
+  e_mfma<0, 0, ONE>(AX, B0, acc);
   // P1: MFMA a0 b1; read a1(t); stage B-right(t+1)
   e_barrier();
   if (!DIAG && more1) e_issue(P, nxt, 3, row0, col0, t + 1, io);
   e_read_a(cur + ha * E_HALF, 64, o, AY);
-  e_mfma<0, 1>(AX, B1, acc);
+  e_mfma<0, 1, ONE>(AX, B1, acc);
   // P2: MFMA a1 b1; read a0(t+1) (wait for the A halves of t+1); stage B-left(t+2)
   if (more1) {
     if (DIAG)
@@ -1443,7 +1523,7 @@ __device__ inline void e_stage(const GramParams& P, char* lds, int64_t row0, int
   e_barrier();
   if (!DIAG && more2) e_issue(P, cur, 2, row0, col0, t + 2, io);
   if (more1) e_read_a(nxt + ha * E_HALF, 0, o, AX);
-  e_mfma<1, 1>(AY, B1, acc);
+  e_mfma<1, 1, ONE>(AY, B1, acc);
   // P3: MFMA a1 b0; read b0(t+1) into B1's registers (wait for the B halves of t+1);
   // stage A-top(t+2)
   if (!DIAG && more1) {
@@ -1455,11 +1535,11 @@ __device__ inline void e_stage(const GramParams& P, char* lds, int64_t row0, int
   e_barrier();
   if (more2) e_issue(P, cur, 0, row0, col0, t + 2, io);
   if (more1) e_read_b(nxt + hb * E_HALF, rb, o, B1);
-  e_mfma<1, 0>(AY, B0, acc);
+  e_mfma<1, 0, ONE>(AY, B0, acc);
   if (P.flush && more1 && (t + 1) % P.flush == 0) e_flush(acc, P.fbuf + (size_t)blockIdx.x * WT * WT, t + 1 == P.flush);
 }
 
-template <bool DIAG>
+template <bool DIAG, bool ONE>
 __device__ inline void e_loop(const GramParams& P, char* lds, int64_t row0, int64_t col0, int ns,
                               f32x4 (&acc)[8][4]) {
   const int wid = threadIdx.x >> 6;
@@ -1491,8 +1571,8 @@ __device__ inline void e_loop(const GramParams& P, char* lds, int64_t row0, int6
   e_read_a(lds + ha * E_HALF, 0, o, AX);
   e_read_b(lds + hb * E_HALF, rb, o, BP);
   for (int t = 0; t < ns; t += 2) {
-    e_stage<DIAG, false>(P, lds, row0, col0, t, ns, o, io, AX, AY, BP, BQ, acc);
-    if (t + 1 < ns) e_stage<DIAG, true>(P, lds, row0, col0, t + 1, ns, o, io, AX, AY, BP, BQ, acc);
+    e_stage<DIAG, false, ONE>(P, lds, row0, col0, t, ns, o, io, AX, AY, BP, BQ, acc);
+    if (t + 1 < ns) e_stage<DIAG, true, ONE>(P, lds, row0, col0, t + 1, ns, o, io, AX, AY, BP, BQ, acc);
   }
 }
 
@@ -1511,6 +1591,7 @@ __device__ inline void e_partial(const GramParams& P, f32x4 (&acc)[8][4], int sp
 
 // Launch position id -> (super-tile, k split) as k_gram3p: split-major; one split = the
 // whole depth (P.kslice = nstage * GK).
+template <bool ONE>
 __global__ __launch_bounds__(W_THREADS, 1) void k_gram3e(GramParams P) {
   __shared__ __attribute__((aligned(16))) char lds[2 * E_STAGE];
   const int id = P.blk0 + (int)xcd_remap(blockIdx.x, (uint32_t)gridDim.x);
@@ -1530,18 +1611,23 @@ __global__ __launch_bounds__(W_THREADS, 1) void k_gram3e(GramParams P) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (diag)
-    e_loop<true>(S, lds, row0, col0, ns, acc);
+    e_loop<true, ONE>(S, lds, row0, col0, ns, acc);
   else
-    e_loop<false>(S, lds, row0, col0, ns, acc);
+    e_loop<false, ONE>(S, lds, row0, col0, ns, acc);
   if (P.flush && ns > P.flush) e_unflush(acc, P.fbuf + (size_t)blockIdx.x * WT * WT);
   if (P.splits == 1)
-    e_store(P, acc, row0, col0, diag);
+    e_store<ONE>(P, acc, row0, col0, diag);
   else
     e_partial(P, acc, split, ltile);
 }
 
 // The full-depth wide launches run k_gram3e (measured +3.5-8.5 % over k_gram3p on whole
 // RDMs at N = 10k, profiles/r3_gram_ab.log); VISREPS_GRAM_KERNEL=p selects k_gram3p (A/B).
+static bool env_flag(const char* name, bool dflt) {
+  const char* e = getenv(name);
+  return e && *e ? strcmp(e, "0") != 0 : dflt;
+}
+
 static bool gram_phased() {
   const char* e = getenv("VISREPS_GRAM_KERNEL");
   return !(e && strcmp(e, "p") == 0);
@@ -1773,7 +1859,7 @@ static size_t gram_fbuf_floats() {
 
 static size_t gram_ws(int64_t n, int64_t d, int64_t t0, int64_t t1, bool split3, void* base, float** mean,
                       float** stdv, float** partial, uint16_t** planes, float** fbuf = nullptr,
-                      bool own_planes = true) {
+                      bool own_planes = true, uint32_t** flag = nullptr) {
   const RangePlan rp = plan_range(n, d, t0, t1, split3);
   size_t part = range_partial(n, d, rp.rem_count, rp.rem_fit);
   if (rp.r_splits > 1) part = std::max(part, (size_t)rp.r_count * rp.r_splits * WT * WT);
@@ -1786,6 +1872,8 @@ static size_t gram_ws(int64_t n, int64_t d, int64_t t0, int64_t t1, bool split3,
                                       : nullptr;
   const bool flush = gram_flush_stages() > 0 && (d + GK - 1) / GK > gram_flush_stages();
   float* fb = flush ? c.take<float>(gram_fbuf_floats()) : nullptr;
+  uint32_t* fl = c.take<uint32_t>(64);
+  if (flag) *flag = fl;
   if (fbuf) *fbuf = fb;
   if (mean) *mean = m;
   if (stdv) *stdv = s;
@@ -1895,19 +1983,39 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   }
   hipStream_t st = as_stream(stream);
   GramParams P{};
-  gram_geometry(n, d, tile_end - tile_begin, P.T, P.ntiles, P.splits, P.kslice);
   const bool split3 = bf16 || pre.planes || gram_split(n, d);
   float *mean, *stdv;
   uint16_t* planes;
+  uint32_t* one_flag;
   gram_ws(n, d, tile_begin, tile_end, split3, ws, &mean, &stdv, &P.partial, &planes, &P.fbuf,
-          pre.planes == nullptr);
+          pre.planes == nullptr, &one_flag);
   const int flush_stages = P.fbuf ? gram_flush_stages() : 0;
   P.raw = raw ? 1 : 0;
+  P.dk = d;
+  bool one = false;  // bf16 input, one product per k (the default for bf16; VISREPS_GRAM_ONE=0: split)
+  if (bf16 && !pre.planes && !raw && gram_phased() && env_flag("VISREPS_GRAM_ONE", true)) {
+    const int64_t rows = (n + WT - 1) / WT * WT, nst1 = (d + 2 * GK - 1) / (2 * GK);
+    VR_CHECK_HIP(hipMemsetAsync(one_flag, 0, sizeof(uint32_t), st));
+    k_stats_one<<<(unsigned)rows, RSTAT_BS, 0, st>>>(static_cast<const uint16_t*>(Xv), n, d, ldx, nst1, correction,
+                                                     mean, stdv, planes, one_flag);
+    VR_CHECK_LAUNCH();
+    uint32_t bad = 0;
+    VR_CHECK_HIP(hipMemcpyAsync(&bad, one_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    VR_CHECK_HIP(hipStreamSynchronize(st));
+    one = bad == 0;
+    if (one) {
+      P.one = 1;
+      P.planes = planes;
+      P.nstage = nst1;
+      P.dk = nst1 * GK;  // the split-K geometry in 32-k units of the 64-k stages
+    }
+  }
   if (pre.planes) {
     mean = const_cast<float*>(pre.mean);
     stdv = const_cast<float*>(pre.stdv);
     P.planes = pre.planes;
     P.nstage = (d + GK - 1) / GK;
+  } else if (one) {  // statistics and raw records already written
   } else if (raw) {  // zero means: the panels stage X itself
     VR_CHECK_HIP(hipMemsetAsync(mean, 0, (size_t)n * sizeof(float), st));
     VR_CHECK_HIP(hipMemsetAsync(stdv, 0, (size_t)n * sizeof(float), st));
@@ -1938,7 +2046,7 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   // tile range [t0, t0 + count): its own split-K geometry, generations, reduction
   auto run_range = [&](int64_t t0, int64_t count, bool fit) -> int {
     if (count <= 0) return VR_OK;
-    gram_geometry(n, d, count, P.T, P.ntiles, P.splits, P.kslice, fit);
+    gram_geometry(n, P.dk, count, P.T, P.ntiles, P.splits, P.kslice, fit);
     P.tile0 = (int)t0;
     P.tile_count = (int)count;
     const int nblk = P.tile_count * P.splits;
@@ -1949,8 +2057,10 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
       P.blk0 = b0;
       const unsigned nb = (unsigned)std::min(gen, nblk - b0);
       KtScope kt(KT_GRAM_TILE, 2.0 * (double)nb / P.splits * GT * GT * (double)d, st);  // tile FLOPs
-      if (split3)
-        k_gram3<<<nb, G_THREADS, 0, st>>>(P);
+      if (split3 && P.one)
+        k_gram3<true><<<nb, G_THREADS, 0, st>>>(P);
+      else if (split3)
+        k_gram3<false><<<nb, G_THREADS, 0, st>>>(P);
       else
         k_gram<<<nb, G_THREADS, 0, st>>>(P);
       VR_CHECK_LAUNCH();
@@ -1985,8 +2095,10 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
   for (int b0 = 0; b0 < W.tile_count; b0 += gen) {
     W.blk0 = b0;
     KtScope kt(KT_GRAM_WIDE, 2.0 * (double)std::min(gen, W.tile_count - b0) * WT * WT * (double)d, st);
-    if (phased)
-      k_gram3e<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
+    if (phased && W.one)
+      k_gram3e<true><<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
+    else if (phased)
+      k_gram3e<false><<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
     else if (pipe)
       k_gram3p<<<(unsigned)std::min(gen, W.tile_count - b0), W_THREADS, 0, st>>>(W);
     else
@@ -2004,8 +2116,10 @@ static int rdm_launch(const void* Xv, int64_t n, int64_t d, int64_t ldx, float* 
       Rm.blk0 = b0;
       const int nb = std::min(gen, nblk - b0);
       KtScope kt(KT_GRAM_WIDE, 2.0 * (double)nb / Rm.splits * WT * WT * (double)d, st);
-      if (phased)
-        k_gram3e<<<(unsigned)nb, W_THREADS, 0, st>>>(Rm);
+      if (phased && Rm.one)
+        k_gram3e<true><<<(unsigned)nb, W_THREADS, 0, st>>>(Rm);
+      else if (phased)
+        k_gram3e<false><<<(unsigned)nb, W_THREADS, 0, st>>>(Rm);
       else
         k_gram3p<<<(unsigned)nb, W_THREADS, 0, st>>>(Rm);
       VR_CHECK_LAUNCH();

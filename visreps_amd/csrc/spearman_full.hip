@@ -34,6 +34,24 @@ __global__ void k_full_keys(const float* __restrict__ rdm, int64_t n, int64_t ld
   }
 }
 
+// the sub-RDM A[idx][:, idx]'s strict upper triangle (evals.py:362-364's `A[idx][:, idx]`, never
+// materialised): pair (a, b), a < b of the k subset rows, value rdm[idx[a] * ld + idx[b]], at
+// its triangle index in the k x k sub-RDM
+__global__ void k_full_keys_sub(const float* __restrict__ rdm, const int32_t* __restrict__ idx, int64_t k,
+                                int64_t ld, uint32_t* __restrict__ keys, uint32_t* __restrict__ tidx,
+                                uint32_t* __restrict__ nan_flag) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= k) return;
+  const int64_t cb = idx[b];
+  for (int64_t a = blockIdx.y; a < b; a += gridDim.y) {
+    const float v = rdm[(int64_t)idx[a] * ld + cb];
+    if (v != v) atomicOr(nan_flag, 1u);
+    const uint64_t t = tri_index((uint64_t)a, (uint64_t)b, (uint64_t)k);
+    keys[t] = f32_sort_key(v);
+    tidx[t] = (uint32_t)t;
+  }
+}
+
 __global__ void k_group_flags_full(const uint32_t* __restrict__ keys, int64_t M,
                                    uint32_t* __restrict__ flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -165,12 +183,16 @@ static FullWs full_layout(void* base, int64_t n, size_t* bytes) {
   return w;
 }
 
-// sort one RDM's triangle by value; flags / gidx / gstart of its tie groups
+// sort one RDM's triangle by value (idx: the sub-RDM of those n rows and columns); flags /
+// gidx / gstart of its tie groups
 static int full_sorted_groups(const float* rdm, int64_t n, int64_t ld, const FullWs& w, uint32_t* nan,
-                              hipStream_t st) {
+                              hipStream_t st, const int32_t* idx = nullptr) {
   const int64_t M = pairs_of(n);
   const dim3 grid((unsigned)((n + 255) / 256), (unsigned)std::min<int64_t>(n, 16384));
-  k_full_keys<<<grid, 256, 0, st>>>(rdm, n, ld, w.keys, w.tidx, nan);
+  if (idx)
+    k_full_keys_sub<<<grid, 256, 0, st>>>(rdm, idx, n, ld, w.keys, w.tidx, nan);
+  else
+    k_full_keys<<<grid, 256, 0, st>>>(rdm, n, ld, w.keys, w.tidx, nan);
   VR_CHECK_LAUNCH();
   VR_TRY(radix_sort_kv(w.keys, w.tidx, w.keys_alt, w.tidx_alt, M, w.radix, st));
   const unsigned gb = (unsigned)((M + 255) / 256);
@@ -186,6 +208,9 @@ static int full_sorted_groups(const float* rdm, int64_t n, int64_t ld, const Ful
 
 using namespace vr;
 
+static int spearman_full_impl(const float* A, const float* B, int64_t n, int64_t ld, const int32_t* idx,
+                              double* out, void* ws, size_t ws_bytes, hipStream_t st);
+
 extern "C" {
 
 size_t vr_spearman_full_workspace(int64_t n) {
@@ -199,9 +224,23 @@ int vr_spearman_full_f32(const float* A, const float* B, int64_t n, int64_t ld, 
                          size_t ws_bytes, void* stream) {
   VR_REQUIRE(n >= 0 && ld >= n && out, "vr_spearman_full_f32: bad shape n=%lld ld=%lld", (long long)n,
              (long long)ld);
+  return spearman_full_impl(A, B, n, ld, nullptr, out, ws, ws_bytes, as_stream(stream));
+}
+
+int vr_spearman_full_subset_f32(const float* A, const float* B, int64_t n, int64_t ld, const int32_t* idx,
+                                int64_t k, double* out, void* ws, size_t ws_bytes, void* stream) {
+  VR_REQUIRE(n >= 0 && ld >= n && k >= 0 && k <= n && out, "vr_spearman_full_subset_f32: bad shape n=%lld "
+             "ld=%lld k=%lld", (long long)n, (long long)ld, (long long)k);
+  VR_REQUIRE(idx != nullptr || k == 0, "vr_spearman_full_subset_f32: null idx");
+  return spearman_full_impl(A, B, k, ld, idx, out, ws, ws_bytes, as_stream(stream));
+}
+
+}  // extern "C"
+
+static int spearman_full_impl(const float* A, const float* B, int64_t n, int64_t ld, const int32_t* idx,
+                              double* out, void* ws, size_t ws_bytes, hipStream_t st) {
   VR_REQUIRE(pairs_of(n) < ((int64_t)1 << 32), "vr_spearman_full_f32: n=%lld has 2^32 or more pairs",
              (long long)n);
-  hipStream_t st = as_stream(stream);
   const int64_t M = pairs_of(n);
   if (M < 2) {  // scipy: NaN for fewer than two pairs
     const double nan = __builtin_nan("");
@@ -218,10 +257,10 @@ int vr_spearman_full_f32(const float* A, const float* B, int64_t n, int64_t ld, 
   }
   VR_CHECK_HIP(hipMemsetAsync(w.nan, 0, 2 * sizeof(uint32_t), st));
   const int grid = full_grid();
-  VR_TRY(full_sorted_groups(A, n, ld, w, w.nan, st));
+  VR_TRY(full_sorted_groups(A, n, ld, w, w.nan, st, idx));
   k_full_ranks<<<grid, FULL_BS, 0, st>>>(w.tidx, w.keys_alt, w.tidx_alt, w.gstart, M, w.yA, w.partA);
   VR_CHECK_LAUNCH();
-  VR_TRY(full_sorted_groups(B, n, ld, w, w.nan + 1, st));
+  VR_TRY(full_sorted_groups(B, n, ld, w, w.nan + 1, st, idx));
   k_full_dot<<<grid, FULL_BS, 0, st>>>(w.tidx, w.keys_alt, w.tidx_alt, w.gstart, M, w.yA, w.partB);
   VR_CHECK_LAUNCH();
   k_full_final<<<1, 64, 0, st>>>(w.partA, w.partB, grid, M, w.nan, out);
@@ -229,6 +268,7 @@ int vr_spearman_full_f32(const float* A, const float* B, int64_t n, int64_t ld, 
   return VR_OK;
 }
 
+extern "C" {
 
 // ---------------------------------------------------------------------------------
 // Local pieces of the distributed global rank (analysis/distributed_spearman.py)
