@@ -2492,7 +2492,11 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
     // table whose knots are the lane's counts at <= 144 boundaries, one LDS read per pair),
     // one gather per pair like EST 3; its flagged passes are re-run exact as ever. The exact
     // form from the start only with VISREPS_ENGINE_EST1_FALLBACK=0 or a point-only call.
-    if (lw == LANES && env_int("VISREPS_ENGINE_EST1_FALLBACK", 1) != 0) {
+    // (Only where the exact form reads its masks from L2 too, n > 10,176: below that the exact
+    // walks keep the masks in LDS and EST 1, whose table takes that LDS, measured slower --
+    // 79 vs 73 ms per unit on bench.structured_est_probe's RDM at N = 10k; at 20,500 EST 1
+    // won, 215 vs 234 ms, profiles/r6_large_n_probe_v2.log.)
+    if (lw == LANES && !cfg.use_lds && env_int("VISREPS_ENGINE_EST1_FALLBACK", 1) != 0) {
       EngineCfg c1 = engine_cfg(n, 1);
       c1.prejoined = cfg.prejoined;
       if (c1.nwaves == cfg.nwaves && c1.est_nsegA <= (uint32_t)cfg.nwaves * VR_SEGS_PER_WAVE) {
