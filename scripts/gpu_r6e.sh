@@ -6,7 +6,7 @@ out=gpurun_out/r6e
 mkdir -p $out
 export TMPDIR=/tmp MIOPEN_FIND_MODE=FAST
 T="python -u -m pytest -x -v --timeout 600 --timeout-method thread -p no:cacheprovider"
-timeout -k 10 600 $T tests/test_engine_est.py -m gpu -k "structured or grid" > $out/engine_est.log 2>&1 || { tail -40 $out/engine_est.log; exit 1; }
+timeout -k 10 600 $T tests/test_engine_est.py -m gpu -k "structured" > $out/engine_est.log 2>&1 || { tail -40 $out/engine_est.log; exit 1; }
 tail -3 $out/engine_est.log
 for lib in default rs32; do
   if [ $lib = default ]; then unset ALT_LIB; else export ALT_LIB=$PWD/abl/$lib.so; fi

@@ -154,12 +154,12 @@ def test_triangle_order_form_equals_exact_form(dev, n, nb, monkeypatch):
     assert np.array_equal(est, ref)
 
 
-@pytest.mark.parametrize("n", [5000, 11000])
+@pytest.mark.parametrize("n", [5000, 21000])
 def test_structured_rdm_leaves_est3_up_front(dev, monkeypatch, n):
     # the heavy per-stimulus effects: the first pass's A counts (k_countA at <= 256
     # boundaries) are already far outside the EST 3 window, so the call leaves EST 3 before
-    # spending an EST pass (vr_engine_est_predicted counts it): at n = 5000 (masks in LDS) for
-    # the exact form, at 11,000 (masks from L2) for EST 1, whose per-lane tables follow each
+    # spending an EST pass (vr_engine_est_predicted counts it): at n = 5000 (the exact walks'
+    # masks in LDS) for the exact form, at 21,000 (masks from L2) for EST 1, whose per-lane tables follow each
     # subset's own counts (vr_engine_est1_fallbacks). The scores equal the exact form, and so do
     # those of VISREPS_ENGINE_EST1_FALLBACK=0; with the check off, the first EST pass is
     # flagged and the call gives up there, same scores.
@@ -175,7 +175,7 @@ def test_structured_rdm_leaves_est3_up_front(dev, monkeypatch, n):
     p0, f0 = int(L.vr_engine_est_predicted()), int(L.vr_engine_est1_fallbacks())
     est = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
     assert int(L.vr_engine_est_predicted()) - p0 == 1
-    assert int(L.vr_engine_est1_fallbacks()) - f0 == (1 if n > 10176 else 0)
+    assert int(L.vr_engine_est1_fallbacks()) - f0 == (1 if n > 20352 else 0)
     with exact_engine():
         ref = R.bootstrap_spearman(pa, pb, idx, full_first=True).cpu().numpy()
     assert np.array_equal(est, ref)

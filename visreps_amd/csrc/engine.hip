@@ -2492,7 +2492,7 @@ static int run_engine_multi_impl(const PlanView& A, const PlanView* Bs, int64_t 
     // table whose knots are the lane's counts at <= 144 boundaries, one LDS read per pair),
     // one gather per pair like EST 3; its flagged passes are re-run exact as ever. The exact
     // form from the start only with VISREPS_ENGINE_EST1_FALLBACK=0 or a point-only call.
-    // (Only where the exact form reads its masks from L2 too, n > 10,176: below that the exact
+    // (Only where the exact form reads its masks from L2 too, n > 20,352: below that the exact
     // walks keep the masks in LDS and EST 1, whose table takes that LDS, measured slower --
     // 79 vs 73 ms per unit on bench.structured_est_probe's RDM at N = 10k; at 20,500 EST 1
     // won, 215 vs 234 ms, profiles/r6_large_n_probe_v2.log.)
