@@ -446,8 +446,8 @@ def configs2_leg(dev) -> dict:
     """BASELINE configs[2] on one GPU (the N = 1 point of its scaling curve): the NSD
     73k-stimulus full RDM -- 73,000 x 43,264 fp32 features (AlexNet conv5 width) -> split-Gram
     compute_rdm (rsa.py:59-93), a 73,000 x 2,000-voxel neural RDM, and the full-triangle
-    Spearman of the two (rsa.py:96-129 at 2.66e9 pairs, vr_spearman_full_f32: radix sort of
-    (key, triangle index) per RDM, midranks, exact integer dot). Synthetic features; HIP events
+    Spearman of the two (rsa.py:96-129 at 2.66e9 pairs, vr_spearman_full_f32: midranks from
+    per-key count tables of each triangle, exact integer dot). Synthetic features; HIP events
     after one warm call; outside the timed steps."""
     from visreps_amd.analysis import rsa as R
 
@@ -462,7 +462,7 @@ def configs2_leg(dev) -> dict:
     del y
     _free_device(dev)
     R.spearman_full(rdm_m[:4096, :4096], rdm_n[:4096, :4096])  # warm (kernels, small workspace)
-    # first full-size call: it also allocates the ~137 GB workspace (the pool keeps it), so its
+    # first full-size call: it also allocates the ~33 GB workspace (the pool keeps it), so its
     # time includes the device allocation; the second call is the kernels' steady state
     sf = []
     for _ in range(2):
@@ -487,20 +487,27 @@ def configs2_leg(dev) -> dict:
         kt.append(e0.elapsed_time(e1))
     workspace.release("kendall_full")
     M = n * (n - 1) // 2
-    # algorithmic bytes per pair of one RDM: key build (rdm read 4 + key/index write 8), LSD
-    # radix sort 4 passes x (read 8 + write 8), tie flags/scan/starts (~16), midranks of A
-    # scattered to triangle order (read 12, write 8) or B's dot (read 12 + 8-B gather) -> ~120 B
-    # per pair and RDM; two RDMs
-    bpp = 2 * 120
+    from visreps_amd._lib import lib as _vlib
+    sf_form = ["bucketed count tables", "count tables", "radix sort"][_vlib().vr_spearman_full_last_form()]
+    # algorithmic bytes per pair of the bucketed count-table form (both RDMs together): key
+    # range 8 (both triangles read), bucket histograms 8, bucket records 8 read + 12 written,
+    # per-key counts 12 read, dot 8 read + one 4-B table read of B -> 60 B per pair. Its time
+    # goes to scattered record writes and one random table read per pair (transaction-, not
+    # byte-bound), so the frac on these bytes is low; vs_sort_model restates the time on the
+    # round-5 sort pipeline's ~120 B per pair and RDM (the model VERDICT r5 #6 set its 0.45 /
+    # 180 ms target on).
+    bpp = 60
     gbs = bpp * M / (sf_ms / 1e3) / 1e9
+    sort_model = 2 * 120 * M / (sf_ms / 1e3) / 1e9 / HBM_PEAK_GBS
     out = {"n": n, "d": d, "voxels": v, "rdm_ms": round(call_ms, 2), "gram_ms": round(gram_ms, 2),
            "gram_launches": launches, "roofline_gram": _gram_roof(n, d, call_ms, gram_ms),
            "spearman_full": {"ms": round(sf_ms, 2), "first_call_ms": round(first_ms, 2), "pairs": M, "rho": rho,
-                             "pairs_per_s": round(M / (sf_ms / 1e3), 1),
+                             "form": sf_form, "pairs_per_s": round(M / (sf_ms / 1e3), 1),
                              "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                                           "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                          "algorithmic_bytes_model": "~120 B per pair and RDM (keys 12, radix "
-                                          "sort 4 x 16, tie groups ~16, midrank scatter / dot ~28), 2 RDMs"}},
+                                          "algorithmic_bytes_model": "60 B per pair, both RDMs (key range 8, bucket "
+                                          "histograms 8, records 8 + 12, counts 12, dot 8 + 4 random)",
+                                          "vs_sort_model": round(sort_model, 4)}},
            "kendall_full": {"ms": round(kt[1], 2), "first_call_ms": round(kt[0], 2), "pairs": M, "tau_a": tau,
                             "note": "vr_kendall_full_f32 (kendall_full.hip): 2 radix sorts + one inversion level per "
                                     "bit of the y dense rank"},

@@ -333,10 +333,19 @@ int vr_srp_csr_f32(const int32_t* indptr, const int32_t* indices, const float* v
 /* ------------------------------------------------------------------------------
  * Full-triangle Spearman of two RDMs with up to 2^32 - 1 pairs (n <= 92681), no rank plan:
  * the compute_rdm_correlation(.., "Spearman") path above the engine's 16-bit stimulus
- * indices (rsa.py:96-129 at configs[2]'s 73k stimuli). Radix sort of (key, triangle
- * index), average ranks, exact u128 sums; out [device] one double.
+ * indices (rsa.py:96-129 at configs[2]'s 73k stimuli). Average ranks from per-key counts
+ * of each triangle's fp32 keys (count tables over the key range, no sort) or, when the key
+ * range does not fit the workspace, a radix sort of (key, triangle index); exact u128 sums
+ * either way; out [device] one double. vr_spearman_full_workspace(n) covers every RDM whose
+ * values span at most 2^30 + 1 fp32 keys (all correlation-distance RDMs: values in [0, 2]);
+ * on a wider range the call returns VR_EWORKSPACE and vr_spearman_full_sort_workspace(n)
+ * is the size that always suffices.
  * -------------------------------------------------------------------------- */
 size_t vr_spearman_full_workspace(int64_t n);
+size_t vr_spearman_full_sort_workspace(int64_t n);
+/* Form the last vr_spearman_full_* call took: 0 bucketed count tables, 1 plain count tables,
+ * 2 radix sort (-1 before any call). */
+int vr_spearman_full_last_form(void);
 int vr_spearman_full_f32(const float* A, const float* B, int64_t n, int64_t ld, double* out,
                          void* ws, size_t ws_bytes, void* stream);
 /* ... of the sub-RDMs A[idx][:, idx], B[idx][:, idx] (k rows idx [dev] int32, never

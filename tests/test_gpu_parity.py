@@ -441,10 +441,25 @@ def test_rdm_wide_supertiles(dev, wide, kernel, d, monkeypatch):
 
 
 # --------------------------------------------------------------------------- large n
-@pytest.mark.parametrize("n,levels", [(2, None), (3, None), (700, None), (1500, 5), (3000, 40)])
-def test_spearman_full_equals_plan_path_and_oracle(dev, n, levels):
+def _key_range(v: np.ndarray) -> int:
+    """Number of fp32 sort keys between the smallest and largest value (f32_sort_key)."""
+    u = np.ascontiguousarray(v, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    u[u == 0x80000000] = 0
+    k = np.where(u & 0x80000000, (~u) & 0xFFFFFFFF, u | 0x80000000)
+    return int(k.max() - k.min() + 1)
+
+
+@pytest.mark.parametrize("n,levels", [(2, None), (3, None), (700, None), (1500, 5), (3000, 40), (2500, 2000),
+                                     (2000, 200000)])
+@pytest.mark.parametrize("form", ["bucket", "table", "sort"])
+def test_spearman_full_equals_plan_path_and_oracle(dev, n, levels, form, monkeypatch):
     # the plan-free full-triangle Spearman (used above n = 65535) against the rank-plan
-    # engine (bit for bit: both exact integer sums) and scipy (tie-heavy RDMs included)
+    # engine (bit for bit: both exact integer sums) and scipy (tie-heavy RDMs included), in
+    # each of its forms (bucketed count tables, plain count tables, radix sort)
+    monkeypatch.setenv("VISREPS_FULL_FORM", form)
+    if form != "sort":  # room for two tables of 2^30 + 1 keys (the default workspace of a small n
+        from visreps_amd._lib import workspace  # is the sort form's, and its tables may not fit)
+        workspace.get(dev, 9 << 30, "spearman_full")
     a = O.synthetic_features(n, [40], seed=n)[0]
     b = O.synthetic_features(n, [60], seed=n + 1)[0]
     ra, rb = O.compute_rdm(a), O.compute_rdm(b)
@@ -456,10 +471,56 @@ def test_spearman_full_equals_plan_path_and_oracle(dev, n, levels):
     if n < 3:
         assert np.isnan(got) and np.isnan(ref)
         return
+    from visreps_amd._lib import lib
+    iu = np.triu_indices(n, 1)
+    ranges = [_key_range(r[iu]) for r in (ra, rb)]
+    used = lib().vr_spearman_full_last_form()
+    if form == "bucket" and max(ranges) > (1 << 26):  # keys beyond the bucketed tables (e.g. 0.0 .. 2.0)
+        assert used in (1, 2)
+    else:
+        assert used == ["bucket", "table", "sort"].index(form), (used, ranges)
     assert got == ref
     iu = np.triu_indices(n, 1)
     assert abs(got - O.midrank_spearman(ra[iu], rb[iu])) <= 1e-12
     assert R.spearman_full(tb, ta) == got
+
+
+def test_spearman_full_wide_key_range_takes_the_sort_form(dev):
+    # values far outside [0, 2] (a key range beyond the count tables' 2^30 + 1): the call
+    # returns VR_EWORKSPACE on the default workspace and rsa.spearman_full re-runs it on the
+    # sort form's; the statistic still equals the rank-plan engine's and scipy's
+    n = 900
+    g = np.random.default_rng(5)
+    ra = np.exp(g.normal(0, 8, (n, n))).astype(np.float32)
+    ra = np.where(g.random((n, n)) < 0.3, -ra, ra).astype(np.float32)
+    ra = np.triu(ra, 1) + np.triu(ra, 1).T
+    rb = (ra + np.exp(g.normal(0, 6, (n, n))).astype(np.float32)).astype(np.float32)
+    rb = np.triu(rb, 1) + np.triu(rb, 1).T
+    ta, tb = torch.from_numpy(ra).to(dev), torch.from_numpy(rb).to(dev)
+    got = R.spearman_full(ta, tb)
+    assert got == R.compute_rdm_correlation(ta, tb, correlation="Spearman")
+    iu = np.triu_indices(n, 1)
+    assert abs(got - O.midrank_spearman(ra[iu], rb[iu])) <= 1e-12
+    # n = 30,000: the default workspace (count tables for 2^30 + 1 keys) is smaller than the
+    # sort form's, so this call takes the VR_EWORKSPACE retry
+    from visreps_amd._lib import lib, workspace
+    L = lib()
+    n = 30000
+    assert L.vr_spearman_full_sort_workspace(n) > L.vr_spearman_full_workspace(n)
+    gt = torch.Generator(device=dev).manual_seed(6)
+
+    def wide():
+        x = torch.exp(torch.randn(n, n, device=dev, generator=gt) * 8)
+        x = torch.where(torch.rand(n, n, device=dev, generator=gt) < 0.3, -x, x).triu(1)
+        return x + x.T
+
+    ta = wide()
+    tb = ta + wide()
+    workspace.release("spearman_full")
+    got = R.spearman_full(ta, tb)
+    assert workspace.current(dev, "spearman_full") >= L.vr_spearman_full_sort_workspace(n)
+    assert got == R.compute_rdm_correlation(ta, tb, correlation="Spearman") and 0.0 < got < 1.0
+    workspace.release("spearman_full")
 
 
 def test_spearman_full_nan_and_constant(dev):

@@ -434,14 +434,22 @@ def bootstrap_full(
     scores = torch.empty(total, dtype=torch.float64, device=dev)
     L = lib()
     spear = method == "spearman"
-    ws = workspace.get(dev, (L.vr_spearman_full_workspace if spear else L.vr_kendall_full_workspace)(n),
-                       "spearman_full" if spear else "kendall_full")
-    st = stream_of(dev)
     with torch.cuda.device(dev):
+        if spear:
+            if full_first:
+                _full_spearman_call(L.vr_spearman_full_f32, (_ptr(a), _ptr(b), n, a.stride(0), _ptr(scores)),
+                                    dev, n)
+            off = 1 if full_first else 0
+            for i in range(n_sets):
+                _full_spearman_call(L.vr_spearman_full_subset_f32, (_ptr(a), _ptr(b), n, a.stride(0),
+                                                                   _ptr(idx_t[i]), k, _ptr(scores[off + i:])), dev, k)
+            return scores
+        ws = workspace.get(dev, L.vr_kendall_full_workspace(n), "kendall_full")
+        st = stream_of(dev)
         if full_first:
-            fn = L.vr_spearman_full_f32 if spear else L.vr_kendall_full_f32
+            fn = L.vr_kendall_full_f32
             check(fn(_ptr(a), _ptr(b), n, a.stride(0), _ptr(scores), _ptr(ws), ws.numel(), st), fn.__name__)
-        sub = L.vr_spearman_full_subset_f32 if spear else L.vr_kendall_full_subset_f32
+        sub = L.vr_kendall_full_subset_f32
         off = 1 if full_first else 0
         for i in range(n_sets):
             check(sub(_ptr(a), _ptr(b), n, a.stride(0), _ptr(idx_t[i]), k, _ptr(scores[off + i:]), _ptr(ws),
@@ -568,9 +576,26 @@ def compute_rdm_correlation(
     return val
 
 
+_VR_EWORKSPACE = -3
+
+
+def _full_spearman_call(fn, args: tuple, dev: torch.device, n: int) -> None:
+    """fn(*args, ws, ws_bytes, stream) on the count-table workspace; a triangle whose key
+    range is wider than those tables (values beyond [0, 2]) returns VR_EWORKSPACE, and the
+    call runs again on the sort form's workspace."""
+    L = lib()
+    ws = workspace.get(dev, L.vr_spearman_full_workspace(n), "spearman_full")
+    rc = fn(*args, _ptr(ws), ws.numel(), stream_of(dev))
+    if rc == _VR_EWORKSPACE:
+        ws = workspace.get(dev, L.vr_spearman_full_sort_workspace(n), "spearman_full")
+        rc = fn(*args, _ptr(ws), ws.numel(), stream_of(dev))
+    check(rc, fn.__name__)
+
+
 def spearman_full(rdm1: torch.Tensor, rdm2: torch.Tensor) -> float:
     """Spearman of the strict upper triangles without a rank plan (vr_spearman_full_f32):
-    radix sort of (value, triangle index) per RDM, average ranks, exact integer sums; any
+    average ranks from per-key count tables of each triangle (a radix sort of (value,
+    triangle index) when the value range is too wide for them), exact integer sums; any
     n with n(n-1)/2 < 2^32 (n <= 92681). compute_rdm_correlation uses it above the rank
     plan's n <= 65535 (configs[2]'s 73k-stimulus RDM)."""
     dev = _device_for(rdm1, rdm2)
@@ -583,10 +608,8 @@ def spearman_full(rdm1: torch.Tensor, rdm2: torch.Tensor) -> float:
     n = a.size(0)
     out = torch.empty(1, dtype=torch.float64, device=dev)
     L = lib()
-    ws = workspace.get(dev, L.vr_spearman_full_workspace(n), "spearman_full")
     with torch.cuda.device(dev):
-        check(L.vr_spearman_full_f32(_ptr(a), _ptr(b), n, a.stride(0), _ptr(out), _ptr(ws), ws.numel(),
-                                     stream_of(dev)), "vr_spearman_full_f32")
+        _full_spearman_call(L.vr_spearman_full_f32, (_ptr(a), _ptr(b), n, a.stride(0), _ptr(out)), dev, n)
     val = float(out.item())
     if math.isnan(val):
         logger.warning("NaN returned for Spearman correlation")

@@ -26,6 +26,9 @@ constexpr int RS_TILE = RS_BS * RS_IPT;
 int radix_pass_kv(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, int64_t n,
                   int shift, uint32_t* ws, hipStream_t st);
 size_t radix_ws_elems(int64_t n);  // uint32 elements of scratch (histograms + scan)
+// The pass's offsets alone: ws[tile * 256 + d] = output position of tile `tile`'s first key
+// of digit d (tiles of RS_TILE keys), for kernels that scatter their own records.
+int radix_offsets(const uint32_t* ki, int64_t n, int shift, uint32_t* ws, hipStream_t st);
 // Sorts ascending by key, stable. keys/vals hold the result; *_alt are ping-pong
 // buffers of the same length.
 int radix_sort_kv(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,

@@ -319,8 +319,7 @@ size_t radix_ws_elems(int64_t n) {
   return (size_t)(256 * nb + 64) + (size_t)256 * rs_chunks(nb).c + 256;
 }
 
-int radix_pass_kv(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, int64_t n,
-                  int shift, uint32_t* ws, hipStream_t st) {
+int radix_offsets(const uint32_t* ki, int64_t n, int shift, uint32_t* ws, hipStream_t st) {
   if (n <= 0) return VR_OK;
   const int64_t nb = (n + RS_TILE - 1) / RS_TILE;
   const RsChunks C = rs_chunks(nb);
@@ -334,7 +333,15 @@ int radix_pass_kv(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t
   VR_CHECK_LAUNCH();
   k_rs_colapply<<<(unsigned)C.c, 256, 0, st>>>(hist, nb, C.ch, cs, cs + 256 * C.c);
   VR_CHECK_LAUNCH();
-  k_rs_scatter<<<(unsigned)nb, RS_BS, 0, st>>>(ki, vi, ko, vo, n, shift, hist, nb);
+  return VR_OK;
+}
+
+int radix_pass_kv(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, int64_t n,
+                  int shift, uint32_t* ws, hipStream_t st) {
+  if (n <= 0) return VR_OK;
+  const int64_t nb = (n + RS_TILE - 1) / RS_TILE;
+  VR_TRY(radix_offsets(ki, n, shift, ws, st));
+  k_rs_scatter<<<(unsigned)nb, RS_BS, 0, st>>>(ki, vi, ko, vo, n, shift, ws, nb);
   VR_CHECK_LAUNCH();
   return VR_OK;
 }
