@@ -219,7 +219,7 @@ POINTS = [f"{l}_{s}" for l in ["conv1", "conv2", "conv3", "conv4", "conv5", "fc1
 
 @pytest.mark.parametrize("point", POINTS)
 def test_bench_point_split_gram_parity(dev, bench, idx, point):
-    feats, neural_split, neural_64, neural_32, _ = bench
+    feats, neural_split, neural_64, neural_32 = bench[:4]
     x = feats[point]
     assert x.size(0) == N
     rdm = R.compute_rdm(x)
