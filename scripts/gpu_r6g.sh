@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 6: Kendall level kernels staged through LDS (coalesced loads / stores) -- Kendall tests,
+# then the 73k plan-free statistics with kernel stats (previous: kendall_full 906 ms, tau
+# 0.3986042363486459; level split 17.0 ms, bucket 5.2 ms per level).
+set -o pipefail
+out=gpurun_out/r6g
+mkdir -p $out
+export TMPDIR=/tmp MIOPEN_FIND_MODE=FAST
+T="python -u -m pytest -x -v --timeout 600 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 600 $T tests/test_kendall.py -m gpu > $out/kendall.log 2>&1 || { tail -40 $out/kendall.log; exit 1; }
+tail -3 $out/kendall.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o p --output-format csv -- python scripts/probe_full73k.py > $out/full73k.log 2>&1 || { tail -20 $out/full73k.log; exit 1; }
+grep -v "amdgpu.ids\|rocprofv3\|output_stream\|HSA version\|simple_timer\|tool.cpp" $out/full73k.log
+python3 scripts/kstats_summary.py $out/prof/p_kernel_stats.csv 24 1 || true
+rm -f $out/prof/p_kernel_trace.csv
