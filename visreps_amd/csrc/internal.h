@@ -29,6 +29,8 @@ size_t radix_ws_elems(int64_t n);  // uint32 elements of scratch (histograms + s
 // The pass's offsets alone: ws[tile * 256 + d] = output position of tile `tile`'s first key
 // of digit d (tiles of RS_TILE keys), for kernels that scatter their own records.
 int radix_offsets(const uint32_t* ki, int64_t n, int shift, uint32_t* ws, hipStream_t st);
+// One pass on keys alone (no values).
+int radix_pass_k(const uint32_t* ki, uint32_t* ko, int64_t n, int shift, uint32_t* ws, hipStream_t st);
 // Sorts ascending by key, stable. keys/vals hold the result; *_alt are ping-pong
 // buffers of the same length.
 int radix_sort_kv(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,

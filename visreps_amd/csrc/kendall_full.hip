@@ -204,19 +204,36 @@ __global__ __launch_bounds__(KF_BS) void k_kf_lvl_count(const uint32_t* __restri
   if (threadIdx.x == 0) tile[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-// this thread's KF_IPT consecutive elements of the tile and the ones of bit b before each
-// (tile prefix + block scan); returns the count of valid elements
+// The tile in LDS: loaded striped (each load instruction one coalesced 256-element row), read
+// back blocked (KF_IPT consecutive elements per thread) through the padded index, which keeps
+// both patterns free of bank conflicts.
+constexpr int KF_PAD = KF_TILE + KF_TILE / 32;
+__device__ inline void kf_stage(const uint32_t* __restrict__ cur, int64_t m, uint32_t* sv, uint32_t (&v)[KF_IPT],
+                                int64_t& i0) {
+  const int64_t base = (int64_t)blockIdx.x * KF_TILE;
+#pragma unroll
+  for (int j = 0; j < KF_IPT; ++j) {
+    const int q = j * KF_BS + (int)threadIdx.x;
+    sv[lds_pad(q)] = base + q < m ? cur[base + q] : 0u;
+  }
+  __syncthreads();
+  i0 = base + (int64_t)threadIdx.x * KF_IPT;
+#pragma unroll
+  for (int j = 0; j < KF_IPT; ++j) v[j] = sv[lds_pad((int)threadIdx.x * KF_IPT + j)];
+}
+
+// this thread's KF_IPT consecutive elements of the tile (staged) and the ones of bit b before
+// each (tile prefix + block scan); tot <- the tile's ones
 __device__ inline void kf_tile_scan(const uint32_t* __restrict__ cur, int64_t m, int b, uint32_t tile_pre,
-                                    uint32_t (&v)[KF_IPT], uint32_t (&p)[KF_IPT], int64_t& i0, uint32_t* lds) {
-  i0 = (int64_t)blockIdx.x * KF_TILE + (int64_t)threadIdx.x * KF_IPT;
+                                    uint32_t (&v)[KF_IPT], uint32_t (&p)[KF_IPT], int64_t& i0, uint32_t* lds,
+                                    uint32_t* sv, uint32_t& tot) {
+  kf_stage(cur, m, sv, v, i0);
   uint32_t s = 0;
 #pragma unroll
   for (int j = 0; j < KF_IPT; ++j) {
-    v[j] = i0 + j < m ? cur[i0 + j] : 0u;
     p[j] = s;
-    s += (v[j] >> b) & 1u;
+    s += i0 + j < m ? (v[j] >> b) & 1u : 0u;
   }
-  uint32_t tot;
   const uint32_t run = block_exclusive_scan<KF_BS>(s, lds, tot) + tile_pre;
 #pragma unroll
   for (int j = 0; j < KF_IPT; ++j) p[j] += run;
@@ -227,21 +244,28 @@ __global__ __launch_bounds__(KF_BS) void k_kf_lvl_bucket(const uint32_t* __restr
                                                          const uint32_t* __restrict__ tile,
                                                          uint32_t* __restrict__ bP) {
   __shared__ uint32_t lds[KF_BS / 64 + 1];
-  uint32_t v[KF_IPT], p[KF_IPT];
+  __shared__ uint32_t sv[KF_PAD];
+  uint32_t v[KF_IPT], p[KF_IPT], tot;
   int64_t i0;
-  kf_tile_scan(cur, m, b, tile[blockIdx.x], v, p, i0, lds);
+  kf_tile_scan(cur, m, b, tile[blockIdx.x], v, p, i0, lds, sv, tot);
+  // the element before this thread's first: the previous thread's last (LDS) or the tile's
+  // predecessor (global)
+  const uint32_t prev = threadIdx.x > 0 ? sv[lds_pad((int)threadIdx.x * KF_IPT - 1)] : (i0 > 0 ? cur[i0 - 1] : 0u);
 #pragma unroll
   for (int j = 0; j < KF_IPT; ++j) {
     const int64_t i = i0 + j;
     if (i >= m) break;
     const uint32_t g = kf_bucket(v[j], b);
-    const uint32_t gp = j > 0 ? kf_bucket(v[j - 1], b) : (i > 0 ? kf_bucket(cur[i - 1], b) : ~0u);
+    const uint32_t gp = j > 0 ? kf_bucket(v[j - 1], b) : (i > 0 ? kf_bucket(prev, b) : ~0u);
     if (i == 0 || gp != g) bP[g] = p[j];
   }
 }
 
 // inversions of this level (ones before each zero inside its bucket) into dpart[tile]; the
-// next level's stream (per bucket: zeros, then ones, each in order) unless last
+// next level's stream (per bucket: zeros, then ones, each in order) unless last. The tile's
+// elements are first put in their output order inside the tile (per bucket segment of the
+// tile: its zeros, then its ones) with their destinations, then written out striped: each
+// store instruction covers runs of consecutive destinations.
 __global__ __launch_bounds__(KF_BS) void k_kf_lvl_split(const uint32_t* __restrict__ cur, int64_t m, int b,
                                                         const uint32_t* __restrict__ tile,
                                                         const uint32_t* __restrict__ bstart,
@@ -250,30 +274,63 @@ __global__ __launch_bounds__(KF_BS) void k_kf_lvl_split(const uint32_t* __restri
                                                         uint32_t* __restrict__ next, uint64_t* __restrict__ dpart) {
   __shared__ uint32_t lds[KF_BS / 64 + 1];
   __shared__ uint64_t red[KF_BS / 64];
-  uint32_t v[KF_IPT], p[KF_IPT];
+  __shared__ uint32_t sv[KF_PAD], sb[KF_PAD], sp[KF_TILE + 2];
+  uint32_t* sd = sb;  // the destinations, once the bucket table is read
+  uint32_t v[KF_IPT], p[KF_IPT], tot;
   int64_t i0;
-  kf_tile_scan(cur, m, b, tile[blockIdx.x], v, p, i0, lds);
+  const uint32_t tpre = tile[blockIdx.x];
+  kf_tile_scan(cur, m, b, tpre, v, p, i0, lds, sv, tot);
   const uint32_t P_all = *ones_total;
+  const int64_t tb = (int64_t)blockIdx.x * KF_TILE;
+  const int64_t te = tb + KF_TILE < m ? tb + KF_TILE : m;
+  // the tile's buckets are one contiguous range [gf, gl] (the stream is ordered by bucket):
+  // their starts and ones-before, and the next bucket's, staged into LDS with striped loads
+  const uint32_t gf = kf_bucket(sv[lds_pad(0)], b), gl = kf_bucket(sv[lds_pad((int)(te - tb) - 1)], b);
+  const int nt = (int)(gl - gf) + 2;
+  for (int x = (int)threadIdx.x; x < nt; x += KF_BS) {
+    const uint32_t g = gf + (uint32_t)x;
+    sb[x] = g < nbk ? bstart[g] : (uint32_t)m;
+    sp[x] = g < nbk ? bP[g] : P_all;
+  }
+  __syncthreads();
   uint64_t dis = 0;
+  uint32_t q[KF_IPT], dst[KF_IPT];
 #pragma unroll
   for (int j = 0; j < KF_IPT; ++j) {
     const int64_t i = i0 + j;
     if (i >= m) break;
     const uint32_t g = kf_bucket(v[j], b);
-    const uint32_t s = bstart[g], Ps = bP[g];
+    const uint32_t s = sb[g - gf], Ps = sp[g - gf];
     const uint32_t before = p[j] - Ps;  // ones of bit b before i in its bucket
     const bool one = (v[j] >> b) & 1u;
     if (!one) dis += before;
     if (next != nullptr) {
-      uint32_t pos;
-      if (!one) {
-        pos = (uint32_t)i - before;  // bucket start + zeros before
-      } else {
-        const uint32_t e = g + 1 < nbk ? bstart[g + 1] : (uint32_t)m;
-        const uint32_t Pe = g + 1 < nbk ? bP[g + 1] : P_all;
-        pos = s + ((e - s) - (Pe - Ps)) + before;  // after the bucket's zeros
-      }
-      next[pos] = v[j];
+      const uint32_t e = sb[g + 1 - gf];
+      const uint32_t Pe = sp[g + 1 - gf];
+      dst[j] = !one ? (uint32_t)i - before                           // bucket start + zeros before
+                    : s + ((e - s) - (Pe - Ps)) + before;           // after the bucket's zeros
+      // the bucket's segment [seg0, seg1) of this tile, its ones, and i's place in it
+      const int64_t seg0 = (int64_t)s > tb ? (int64_t)s : tb, seg1 = (int64_t)e < te ? (int64_t)e : te;
+      const uint32_t P0 = (int64_t)s >= tb ? Ps : tpre;
+      const uint32_t P1 = (int64_t)e < te ? Pe : tpre + tot;
+      const uint32_t ob = p[j] - P0;  // ones before i in the segment
+      const uint32_t zs = (uint32_t)(seg1 - seg0) - (P1 - P0);
+      q[j] = (uint32_t)(seg0 - tb) + (one ? zs + ob : (uint32_t)(i - seg0) - ob);
+    }
+  }
+  if (next != nullptr) {
+    __syncthreads();  // every thread has read its staged elements
+#pragma unroll
+    for (int j = 0; j < KF_IPT; ++j) {
+      if (i0 + j >= m) break;
+      sv[lds_pad((int)q[j])] = v[j];
+      sd[lds_pad((int)q[j])] = dst[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < KF_IPT; ++j) {
+      const int r = j * KF_BS + (int)threadIdx.x;
+      if (tb + r < m) next[sd[lds_pad(r)]] = sv[lds_pad(r)];
     }
   }
   for (int o = 32; o > 0; o >>= 1) dis += __shfl_xor(dis, o, 64);

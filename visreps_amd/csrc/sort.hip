@@ -148,6 +148,8 @@ __global__ __launch_bounds__(256) void k_rs_colapply(uint32_t* __restrict__ h, i
 // ballots, plus the wave's running count of that digit (wave-private LDS counters). The
 // block then needs two barriers: the per-wave digit totals give every key its slot in the
 // digit-ordered tile (digit start + same-digit keys of the waves before + wave rank).
+// KV false: keys only (vin / vout unused).
+template <bool KV = true>
 __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
@@ -176,7 +178,7 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     vv[j] = 0;
     if (p < nvalid) {
       kk[j] = kin[base + p];
-      vv[j] = vin[base + p];
+      if constexpr (KV) vv[j] = vin[base + p];
     }
   }
 #pragma unroll
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     if (w * WT + j * 64 + lane < nvalid) {
       const uint32_t pos = wcnt[w][(kk[j] >> shift) & 255u] + rk[j];
       sk[pos] = kk[j];
-      sv[pos] = vv[j];
+      if constexpr (KV) sv[pos] = vv[j];
     }
   }
   __syncthreads();
@@ -230,11 +232,12 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
       const uint32_t d = (k >> shift) & 255u;
       const int64_t g = (int64_t)offs[tile * 256 + d] + (uint32_t)s - start[d];
       kout[g] = k;
-      vout[g] = sv[s];
+      if constexpr (KV) vout[g] = sv[s];
     }
   }
 }
 #else
+template <bool KV = true>
 __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     uint32_t k = 0xFFFFFFFFu, v = 0;
     if (i < n) {
       k = kin[i];
-      v = vin[i];
+      if constexpr (KV) v = vin[i];
       atomicAdd(&cnt[(k >> shift) & 255u], 1u);
     }
     sk[lds_pad(p)] = k;
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(
     if (r < cnt[d]) {
       int64_t g = (int64_t)offs[tile * 256 + d] + r;
       kout[g] = k;
-      vout[g] = sv[lds_pad(s)];
+      if constexpr (KV) vout[g] = sv[lds_pad(s)];
     }
   }
 }
@@ -341,7 +344,16 @@ int radix_pass_kv(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t
   if (n <= 0) return VR_OK;
   const int64_t nb = (n + RS_TILE - 1) / RS_TILE;
   VR_TRY(radix_offsets(ki, n, shift, ws, st));
-  k_rs_scatter<<<(unsigned)nb, RS_BS, 0, st>>>(ki, vi, ko, vo, n, shift, ws, nb);
+  k_rs_scatter<true><<<(unsigned)nb, RS_BS, 0, st>>>(ki, vi, ko, vo, n, shift, ws, nb);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+int radix_pass_k(const uint32_t* ki, uint32_t* ko, int64_t n, int shift, uint32_t* ws, hipStream_t st) {
+  if (n <= 0) return VR_OK;
+  const int64_t nb = (n + RS_TILE - 1) / RS_TILE;
+  VR_TRY(radix_offsets(ki, n, shift, ws, st));
+  k_rs_scatter<false><<<(unsigned)nb, RS_BS, 0, st>>>(ki, nullptr, ko, nullptr, n, shift, ws, nb);
   VR_CHECK_LAUNCH();
   return VR_OK;
 }

@@ -465,107 +465,45 @@ __global__ __launch_bounds__(256) void k_tab_dot(const float* __restrict__ A, co
 // ---------------------------------------------------------------------------------
 // Bucketed count-table form (the default when both key ranges are at most 2^26 keys): the
 // key offsets k - kmin split into at most 4096 coarse buckets of W = 2^sh <= 16384 keys.
-//   k_cb_hist   per block (a fixed slice of the triangle): LDS histograms of A's and B's
-//               coarse buckets -> one row of hrow
-//   k_cb_colsum bucket sizes (column sums of hrow); k_cb_starts: bucket starts
-//   k_cb_part   each block reserves its runs in every bucket (one global atomic per
-//               nonzero bucket), then writes A's records (kA offset, kB offset) and B's
-//               kB offsets into them (LDS cursors)
+//   k_cb_keys   both triangles' key offsets in triangle order (kA[t], kB[t])
+//   radix       B's offsets ordered by bucket (keys only), then A's (kA, kB) pairs by A's
+//               bucket: one or two 8-bit LSD passes each (sort.hip: coalesced digit runs)
+//   k_cb_bstart bucket starts of each ordered array
 //   k_cb_fine   counts per key: runs of one bucket counted in LDS (W counters) and added to
 //               the table once per block; short runs count in global memory
-//   k_cb_dot    sum yA * yB over A's records: A's table reads stay inside one bucket's
+//   k_cb_dot    sum yA * yB over A's ordered pairs: A's table reads stay inside one bucket's
 //               window (cached), B's are one random 8-B read per pair
 // ---------------------------------------------------------------------------------
-constexpr int CB_MAXB = 4096;  // coarse buckets per RDM
+constexpr int CB_MAXB = 4096;  // coarse buckets per RDM (cb_geom: 12 bits)
+static_assert(CB_MAXB == 1 << 12, "cb_geom splits the key range into 2^12 buckets at most");
 constexpr int CB_MAXSH = 14;   // keys per bucket <= 2^14 (64 KB of LDS counters)
-constexpr int CB_BLOCKS = 8192;
 
+// grid (column blocks, row slots) as k_full_keys
 template <bool SUB>
-__global__ __launch_bounds__(256) void k_cb_hist(const float* __restrict__ A, const float* __restrict__ B,
-                                                 const int32_t* __restrict__ idx, int64_t n, int64_t ld,
-                                                 const uint32_t* __restrict__ mm, int shA, int nbA, int shB,
-                                                 int nbB, uint32_t* __restrict__ hrow) {
-  __shared__ uint32_t hA[CB_MAXB], hB[CB_MAXB];
-  for (int i = threadIdx.x; i < nbA; i += 256) hA[i] = 0;
-  for (int i = threadIdx.x; i < nbB; i += 256) hB[i] = 0;
-  __syncthreads();
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t a0 = mm[0], b0 = mm[2];
-  if (b < n) {
-    for (int64_t a = blockIdx.y; a < b; a += gridDim.y) {
-      atomicAdd(&hA[(f32_sort_key(tri_value<SUB>(A, idx, ld, a, b)) - a0) >> shA], 1u);
-      atomicAdd(&hB[(f32_sort_key(tri_value<SUB>(B, idx, ld, a, b)) - b0) >> shB], 1u);
-    }
-  }
-  __syncthreads();
-  uint32_t* row = hrow + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (nbA + nbB);
-  for (int i = threadIdx.x; i < nbA; i += 256) row[i] = hA[i];
-  for (int i = threadIdx.x; i < nbB; i += 256) row[nbA + i] = hB[i];
-}
-
-// gsz[c] = sum over blocks of hrow[.][c]; grid (columns / 256, chunks of rows)
-__global__ __launch_bounds__(256) void k_cb_colsum(const uint32_t* __restrict__ hrow, int64_t nblk, int ncol,
-                                                   int64_t per, uint32_t* __restrict__ gsz) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= ncol) return;
-  const int64_t r0 = (int64_t)blockIdx.y * per, r1 = r0 + per < nblk ? r0 + per : nblk;
-  uint32_t s = 0;
-  for (int64_t r = r0; r < r1; ++r) s += hrow[r * ncol + c];
-  if (s) atomicAdd(&gsz[c], s);
-}
-
-// one block: bstart[0..nb] = exclusive scan of gsz[0..nb) (bstart[nb] = M), cur = bstart
-__global__ __launch_bounds__(1024) void k_cb_starts(const uint32_t* __restrict__ gsz, int nb,
-                                                    uint32_t* __restrict__ bstart, uint32_t* __restrict__ cur) {
-  __shared__ uint32_t scan_lds[1024 / 64 + 1];
-  const int t = threadIdx.x;
-  uint32_t x[4], s = 0;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    x[u] = 4 * t + u < nb ? gsz[4 * t + u] : 0u;
-    s += x[u];
-  }
-  uint32_t tot;
-  uint32_t acc = block_exclusive_scan<1024>(s, scan_lds, tot);
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    if (4 * t + u < nb) {
-      bstart[4 * t + u] = acc;
-      cur[4 * t + u] = acc;
-    }
-    acc += x[u];
-  }
-  if (t == 0) bstart[nb] = tot;
-}
-
-template <bool SUB>
-__global__ __launch_bounds__(256) void k_cb_part(const float* __restrict__ A, const float* __restrict__ B,
-                                                 const int32_t* __restrict__ idx, int64_t n, int64_t ld,
-                                                 const uint32_t* __restrict__ mm, int shA, int nbA, int shB,
-                                                 int nbB, const uint32_t* __restrict__ hrow,
-                                                 uint32_t* __restrict__ curA, uint32_t* __restrict__ curB,
-                                                 uint64_t* __restrict__ recA, uint32_t* __restrict__ recB) {
-  __shared__ uint32_t lA[CB_MAXB], lB[CB_MAXB];
-  const uint32_t* row = hrow + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (nbA + nbB);
-  for (int i = threadIdx.x; i < nbA; i += 256) {
-    const uint32_t c = row[i];
-    lA[i] = c ? atomicAdd(&curA[i], c) : 0u;
-  }
-  for (int i = threadIdx.x; i < nbB; i += 256) {
-    const uint32_t c = row[nbA + i];
-    lB[i] = c ? atomicAdd(&curB[i], c) : 0u;
-  }
-  __syncthreads();
+__global__ void k_cb_keys(const float* __restrict__ A, const float* __restrict__ B, const int32_t* __restrict__ idx,
+                          int64_t n, int64_t ld, const uint32_t* __restrict__ mm, uint32_t* __restrict__ kA,
+                          uint32_t* __restrict__ kB) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
   const uint32_t a0 = mm[0], b0 = mm[2];
   for (int64_t a = blockIdx.y; a < b; a += gridDim.y) {
-    const uint32_t ka = f32_sort_key(tri_value<SUB>(A, idx, ld, a, b)) - a0;
-    const uint32_t kb = f32_sort_key(tri_value<SUB>(B, idx, ld, a, b)) - b0;
-    const uint32_t pa = atomicAdd(&lA[ka >> shA], 1u), pb = atomicAdd(&lB[kb >> shB], 1u);
-    recA[pa] = (uint64_t)ka | ((uint64_t)kb << 32);
-    recB[pb] = kb;
+    const uint64_t t = tri_index((uint64_t)a, (uint64_t)b, (uint64_t)n);
+    kA[t] = f32_sort_key(tri_value<SUB>(A, idx, ld, a, b)) - a0;
+    kB[t] = f32_sort_key(tri_value<SUB>(B, idx, ld, a, b)) - b0;
   }
+}
+
+// bstart[g] = first position of bucket g in keys ordered by bucket (empty buckets: the next
+// bucket's start), bstart[nb] = M
+__global__ void k_cb_bstart(const uint32_t* __restrict__ keys, int64_t M, int sh, int nb,
+                            uint32_t* __restrict__ bstart) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const int g = (int)(keys[i] >> sh);
+  const int gp = i > 0 ? (int)(keys[i - 1] >> sh) : -1;
+  for (int x = gp + 1; x <= g; ++x) bstart[x] = (uint32_t)i;
+  if (i == M - 1)
+    for (int x = g + 1; x <= nb; ++x) bstart[x] = (uint32_t)M;
 }
 
 constexpr int CB_FINE_BS = 1024;
@@ -605,13 +543,12 @@ __global__ __launch_bounds__(CB_FINE_BS) void k_cb_fine(const uint32_t* __restri
   }
 }
 
-__global__ __launch_bounds__(FULL_BS) void k_cb_dot(const uint64_t* __restrict__ recA, int64_t M,
-                                                    const uint32_t* __restrict__ sA,
+__global__ __launch_bounds__(FULL_BS) void k_cb_dot(const uint32_t* __restrict__ kA, const uint32_t* __restrict__ kB,
+                                                    int64_t M, const uint32_t* __restrict__ sA,
                                                     const uint32_t* __restrict__ sB, uint64_t* __restrict__ part) {
   u128 ab = 0;
   for (int64_t p = (int64_t)blockIdx.x * FULL_BS + threadIdx.x; p < M; p += (int64_t)gridDim.x * FULL_BS) {
-    const uint64_t r = recA[p];
-    const uint32_t ka = (uint32_t)r, kb = (uint32_t)(r >> 32);
+    const uint32_t ka = kA[p], kb = kB[p];
     const uint64_t ya = (uint64_t)sA[ka] + sA[ka + 1] + 1u, yb = (uint64_t)sB[kb] + sB[kb + 1] + 1u;
     ab += (u128)ya * yb;
   }
@@ -735,31 +672,21 @@ static CbGeom cb_geom(uint64_t R) {
 }
 constexpr uint64_t CB_CAP = (uint64_t)1 << (12 + CB_MAXSH);  // 2^26 keys
 
-static dim3 cb_grid(int64_t n) {
-  const int64_t gx = (n + 255) / 256;
-  const int64_t gy = std::max<int64_t>(1, std::min<int64_t>(n, (CB_BLOCKS + gx - 1) / gx));
-  return dim3((unsigned)gx, (unsigned)gy);
-}
-
 struct CbWs {
-  uint32_t *sw, *cA, *cB, *hrow, *gsz, *bsA, *bsB, *cur, *recB;
-  uint64_t* recA;
+  uint32_t *sw, *cA, *cB, *bsA, *bsB, *radix;
+  uint32_t* k[5];  // key arrays (triangle order, then the radix passes' outputs)
 };
 
 static CbWs cb_layout(Carver& c, int64_t n, const CbGeom& ga, const CbGeom& gb) {
   const int64_t M = pairs_of(n);
-  const dim3 g = cb_grid(n);
   CbWs w;
   w.sw = c.take<uint32_t>(scan_ws_elems((int64_t)std::max(ga.tab, gb.tab) + 1));
   w.cA = c.take<uint32_t>((size_t)ga.tab + 1);
   w.cB = c.take<uint32_t>((size_t)gb.tab + 1);
-  w.hrow = c.take<uint32_t>((size_t)g.x * g.y * (ga.nb + gb.nb));
-  w.gsz = c.take<uint32_t>((size_t)(ga.nb + gb.nb));
   w.bsA = c.take<uint32_t>((size_t)ga.nb + 1);
   w.bsB = c.take<uint32_t>((size_t)gb.nb + 1);
-  w.cur = c.take<uint32_t>((size_t)(ga.nb + gb.nb));
-  w.recA = c.take<uint64_t>((size_t)M);
-  w.recB = c.take<uint32_t>((size_t)M);
+  w.radix = c.take<uint32_t>(radix_ws_elems(M));
+  for (int i = 0; i < 5; ++i) w.k[i] = c.take<uint32_t>((size_t)M);
   return w;
 }
 
@@ -847,39 +774,38 @@ static int full_cb_form(const float* A, const float* B, int64_t n, int64_t ld, c
   const int64_t M = pairs_of(n);
   const CbGeom ga = cb_geom(RA), gb = cb_geom(RB);
   const CbWs w = cb_layout(c, n, ga, gb);
-  const int ncol = ga.nb + gb.nb;
   VR_CHECK_HIP(hipMemsetAsync(w.cA, 0, (ga.tab + 1) * sizeof(uint32_t), st));
   VR_CHECK_HIP(hipMemsetAsync(w.cB, 0, (gb.tab + 1) * sizeof(uint32_t), st));
-  VR_CHECK_HIP(hipMemsetAsync(w.gsz, 0, (size_t)ncol * sizeof(uint32_t), st));
-  const dim3 g = cb_grid(n);
-  const int64_t nblk = (int64_t)g.x * g.y;
-  k_cb_hist<SUB><<<g, 256, 0, st>>>(A, B, idx, n, ld, h.mm, ga.sh, ga.nb, gb.sh, gb.nb, w.hrow);
+  uint32_t *ka = w.k[0], *kb = w.k[1];
+  const dim3 kg((unsigned)((n + 255) / 256), (unsigned)std::min<int64_t>(n, 16384));
+  k_cb_keys<SUB><<<kg, 256, 0, st>>>(A, B, idx, n, ld, h.mm, ka, kb);
   VR_CHECK_LAUNCH();
-  const int64_t per = (nblk + 63) / 64;
-  k_cb_colsum<<<dim3((unsigned)((ncol + 255) / 256), (unsigned)((nblk + per - 1) / per)), 256, 0, st>>>(
-      w.hrow, nblk, ncol, per, w.gsz);
+  // B's offsets by bucket (8-bit digits of the bucket, low first), then A's pairs
+  uint32_t* bo = w.k[2];
+  VR_TRY(radix_pass_k(kb, bo, M, gb.sh, w.radix, st));
+  uint32_t* spare = w.k[4];
+  if (gb.nb > 256) {
+    VR_TRY(radix_pass_k(bo, w.k[4], M, gb.sh + 8, w.radix, st));
+    spare = bo;
+    bo = w.k[4];
+  }
+  uint32_t *oa = w.k[3], *ob = spare;
+  VR_TRY(radix_pass_kv(ka, kb, oa, ob, M, ga.sh, w.radix, st));
+  if (ga.nb > 256) {
+    VR_TRY(radix_pass_kv(oa, ob, ka, kb, M, ga.sh + 8, w.radix, st));
+    oa = ka;
+    ob = kb;
+  }
+  const unsigned gm = (unsigned)((M + 255) / 256);
+  k_cb_bstart<<<gm, 256, 0, st>>>(oa, M, ga.sh, ga.nb, w.bsA);
   VR_CHECK_LAUNCH();
-  k_cb_starts<<<1, 1024, 0, st>>>(w.gsz, ga.nb, w.bsA, w.cur);
-  VR_CHECK_LAUNCH();
-  k_cb_starts<<<1, 1024, 0, st>>>(w.gsz + ga.nb, gb.nb, w.bsB, w.cur + ga.nb);
-  VR_CHECK_LAUNCH();
-  k_cb_part<SUB><<<g, 256, 0, st>>>(A, B, idx, n, ld, h.mm, ga.sh, ga.nb, gb.sh, gb.nb, w.hrow, w.cur,
-                                     w.cur + ga.nb, w.recA, w.recB);
+  k_cb_bstart<<<gm, 256, 0, st>>>(bo, M, gb.sh, gb.nb, w.bsB);
   VR_CHECK_LAUNCH();
   const unsigned fb = (unsigned)((M + CB_SEG - 1) / CB_SEG);
-  if (ga.sh == 0) {  // one key per bucket: the counts are the bucket sizes
-    VR_CHECK_HIP(hipMemcpyAsync(w.cA, w.gsz, ga.nb * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-  } else {
-    k_cb_fine<2><<<fb, CB_FINE_BS, 0, st>>>(reinterpret_cast<const uint32_t*>(w.recA), M, w.bsA, ga.nb, ga.sh,
-                                             w.cA);
-    VR_CHECK_LAUNCH();
-  }
-  if (gb.sh == 0) {
-    VR_CHECK_HIP(hipMemcpyAsync(w.cB, w.gsz + ga.nb, gb.nb * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-  } else {
-    k_cb_fine<1><<<fb, CB_FINE_BS, 0, st>>>(w.recB, M, w.bsB, gb.nb, gb.sh, w.cB);
-    VR_CHECK_LAUNCH();
-  }
+  k_cb_fine<1><<<fb, CB_FINE_BS, 0, st>>>(oa, M, w.bsA, ga.nb, ga.sh, w.cA);
+  VR_CHECK_LAUNCH();
+  k_cb_fine<1><<<fb, CB_FINE_BS, 0, st>>>(bo, M, w.bsB, gb.nb, gb.sh, w.cB);
+  VR_CHECK_LAUNCH();
   const int fg = full_grid();
   k_tab_ties<<<fg, FULL_BS, 0, st>>>(w.cA, (int64_t)ga.tab, h.part);
   VR_CHECK_LAUNCH();
@@ -891,7 +817,7 @@ static int full_cb_form(const float* A, const float* B, int64_t n, int64_t ld, c
   VR_CHECK_LAUNCH();
   VR_TRY(scan_exclusive_u32(w.cA, w.cA, (int64_t)ga.tab + 1, nullptr, w.sw, st));
   VR_TRY(scan_exclusive_u32(w.cB, w.cB, (int64_t)gb.tab + 1, nullptr, w.sw, st));
-  k_cb_dot<<<fg, FULL_BS, 0, st>>>(w.recA, M, w.cA, w.cB, h.part);
+  k_cb_dot<<<fg, FULL_BS, 0, st>>>(oa, ob, M, w.cA, w.cB, h.part);
   VR_CHECK_LAUNCH();
   k_reduce_u128<<<1, FULL_BS, 0, st>>>(h.part, fg, h.sums + 4);
   VR_CHECK_LAUNCH();
