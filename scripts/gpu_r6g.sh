@@ -15,3 +15,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o p --output-fo
 grep -v "amdgpu.ids\|rocprofv3\|output_stream\|HSA version\|simple_timer\|tool.cpp" $out/full73k.log
 python3 scripts/kstats_summary.py $out/prof/p_kernel_stats.csv 24 1 || true
 rm -f $out/prof/p_kernel_trace.csv
+# A/B: the level kernels with 256-thread blocks (abl/kf256.so) against the default 512
+ALT_LIB=$PWD/abl/kf256.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof256 -o p --output-format csv -- python scripts/probe_full73k.py > $out/full73k_256.log 2>&1 || { tail -20 $out/full73k_256.log; exit 1; }
+grep "kendall" $out/full73k_256.log
+python3 scripts/kstats_summary.py $out/prof256/p_kernel_stats.csv 40 1 | grep k_kf_lvl || true
+rm -f $out/prof256/p_kernel_trace.csv

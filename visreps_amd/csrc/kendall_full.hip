@@ -204,55 +204,63 @@ __global__ __launch_bounds__(KF_BS) void k_kf_lvl_count(const uint32_t* __restri
   if (threadIdx.x == 0) tile[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+#ifndef VR_KF_LV_BS
+#define VR_KF_LV_BS 512
+#endif
+// the level kernels' blocks: LV_BS threads x LV_IPT consecutive elements = one KF_TILE
+constexpr int LV_BS = VR_KF_LV_BS;
+constexpr int LV_IPT = KF_TILE / LV_BS;
+static_assert(LV_BS * LV_IPT == KF_TILE, "level tile");
+
 // The tile in LDS: loaded striped (each load instruction one coalesced 256-element row), read
-// back blocked (KF_IPT consecutive elements per thread) through the padded index, which keeps
+// back blocked (LV_IPT consecutive elements per thread) through the padded index, which keeps
 // both patterns free of bank conflicts.
 constexpr int KF_PAD = KF_TILE + KF_TILE / 32;
-__device__ inline void kf_stage(const uint32_t* __restrict__ cur, int64_t m, uint32_t* sv, uint32_t (&v)[KF_IPT],
+__device__ inline void kf_stage(const uint32_t* __restrict__ cur, int64_t m, uint32_t* sv, uint32_t (&v)[LV_IPT],
                                 int64_t& i0) {
   const int64_t base = (int64_t)blockIdx.x * KF_TILE;
 #pragma unroll
-  for (int j = 0; j < KF_IPT; ++j) {
-    const int q = j * KF_BS + (int)threadIdx.x;
+  for (int j = 0; j < LV_IPT; ++j) {
+    const int q = j * LV_BS + (int)threadIdx.x;
     sv[lds_pad(q)] = base + q < m ? cur[base + q] : 0u;
   }
   __syncthreads();
-  i0 = base + (int64_t)threadIdx.x * KF_IPT;
+  i0 = base + (int64_t)threadIdx.x * LV_IPT;
 #pragma unroll
-  for (int j = 0; j < KF_IPT; ++j) v[j] = sv[lds_pad((int)threadIdx.x * KF_IPT + j)];
+  for (int j = 0; j < LV_IPT; ++j) v[j] = sv[lds_pad((int)threadIdx.x * LV_IPT + j)];
 }
 
-// this thread's KF_IPT consecutive elements of the tile (staged) and the ones of bit b before
+// this thread's LV_IPT consecutive elements of the tile (staged) and the ones of bit b before
 // each (tile prefix + block scan); tot <- the tile's ones
 __device__ inline void kf_tile_scan(const uint32_t* __restrict__ cur, int64_t m, int b, uint32_t tile_pre,
-                                    uint32_t (&v)[KF_IPT], uint32_t (&p)[KF_IPT], int64_t& i0, uint32_t* lds,
+                                    uint32_t (&v)[LV_IPT], uint32_t (&p)[LV_IPT], int64_t& i0, uint32_t* lds,
                                     uint32_t* sv, uint32_t& tot) {
   kf_stage(cur, m, sv, v, i0);
   uint32_t s = 0;
 #pragma unroll
-  for (int j = 0; j < KF_IPT; ++j) {
+  for (int j = 0; j < LV_IPT; ++j) {
     p[j] = s;
     s += i0 + j < m ? (v[j] >> b) & 1u : 0u;
   }
-  const uint32_t run = block_exclusive_scan<KF_BS>(s, lds, tot) + tile_pre;
+  const uint32_t run = block_exclusive_scan<LV_BS>(s, lds, tot) + tile_pre;
 #pragma unroll
-  for (int j = 0; j < KF_IPT; ++j) p[j] += run;
+  for (int j = 0; j < LV_IPT; ++j) p[j] += run;
 }
 
 // ones before every bucket start: bP[g]
-__global__ __launch_bounds__(KF_BS) void k_kf_lvl_bucket(const uint32_t* __restrict__ cur, int64_t m, int b,
+__global__ __launch_bounds__(LV_BS) void k_kf_lvl_bucket(const uint32_t* __restrict__ cur, int64_t m, int b,
                                                          const uint32_t* __restrict__ tile,
                                                          uint32_t* __restrict__ bP) {
-  __shared__ uint32_t lds[KF_BS / 64 + 1];
+  __shared__ uint32_t lds[LV_BS / 64 + 1];
   __shared__ uint32_t sv[KF_PAD];
-  uint32_t v[KF_IPT], p[KF_IPT], tot;
+  uint32_t v[LV_IPT], p[LV_IPT], tot;
   int64_t i0;
   kf_tile_scan(cur, m, b, tile[blockIdx.x], v, p, i0, lds, sv, tot);
   // the element before this thread's first: the previous thread's last (LDS) or the tile's
   // predecessor (global)
-  const uint32_t prev = threadIdx.x > 0 ? sv[lds_pad((int)threadIdx.x * KF_IPT - 1)] : (i0 > 0 ? cur[i0 - 1] : 0u);
+  const uint32_t prev = threadIdx.x > 0 ? sv[lds_pad((int)threadIdx.x * LV_IPT - 1)] : (i0 > 0 ? cur[i0 - 1] : 0u);
 #pragma unroll
-  for (int j = 0; j < KF_IPT; ++j) {
+  for (int j = 0; j < LV_IPT; ++j) {
     const int64_t i = i0 + j;
     if (i >= m) break;
     const uint32_t g = kf_bucket(v[j], b);
@@ -266,17 +274,17 @@ __global__ __launch_bounds__(KF_BS) void k_kf_lvl_bucket(const uint32_t* __restr
 // elements are first put in their output order inside the tile (per bucket segment of the
 // tile: its zeros, then its ones) with their destinations, then written out striped: each
 // store instruction covers runs of consecutive destinations.
-__global__ __launch_bounds__(KF_BS) void k_kf_lvl_split(const uint32_t* __restrict__ cur, int64_t m, int b,
+__global__ __launch_bounds__(LV_BS) void k_kf_lvl_split(const uint32_t* __restrict__ cur, int64_t m, int b,
                                                         const uint32_t* __restrict__ tile,
                                                         const uint32_t* __restrict__ bstart,
                                                         const uint32_t* __restrict__ bP, uint32_t nbk,
                                                         const uint32_t* __restrict__ ones_total,
                                                         uint32_t* __restrict__ next, uint64_t* __restrict__ dpart) {
-  __shared__ uint32_t lds[KF_BS / 64 + 1];
-  __shared__ uint64_t red[KF_BS / 64];
+  __shared__ uint32_t lds[LV_BS / 64 + 1];
+  __shared__ uint64_t red[LV_BS / 64];
   __shared__ uint32_t sv[KF_PAD], sb[KF_PAD], sp[KF_TILE + 2];
   uint32_t* sd = sb;  // the destinations, once the bucket table is read
-  uint32_t v[KF_IPT], p[KF_IPT], tot;
+  uint32_t v[LV_IPT], p[LV_IPT], tot;
   int64_t i0;
   const uint32_t tpre = tile[blockIdx.x];
   kf_tile_scan(cur, m, b, tpre, v, p, i0, lds, sv, tot);
@@ -287,16 +295,16 @@ __global__ __launch_bounds__(KF_BS) void k_kf_lvl_split(const uint32_t* __restri
   // their starts and ones-before, and the next bucket's, staged into LDS with striped loads
   const uint32_t gf = kf_bucket(sv[lds_pad(0)], b), gl = kf_bucket(sv[lds_pad((int)(te - tb) - 1)], b);
   const int nt = (int)(gl - gf) + 2;
-  for (int x = (int)threadIdx.x; x < nt; x += KF_BS) {
+  for (int x = (int)threadIdx.x; x < nt; x += LV_BS) {
     const uint32_t g = gf + (uint32_t)x;
     sb[x] = g < nbk ? bstart[g] : (uint32_t)m;
     sp[x] = g < nbk ? bP[g] : P_all;
   }
   __syncthreads();
   uint64_t dis = 0;
-  uint32_t q[KF_IPT], dst[KF_IPT];
+  uint32_t q[LV_IPT], dst[LV_IPT];
 #pragma unroll
-  for (int j = 0; j < KF_IPT; ++j) {
+  for (int j = 0; j < LV_IPT; ++j) {
     const int64_t i = i0 + j;
     if (i >= m) break;
     const uint32_t g = kf_bucket(v[j], b);
@@ -321,22 +329,27 @@ __global__ __launch_bounds__(KF_BS) void k_kf_lvl_split(const uint32_t* __restri
   if (next != nullptr) {
     __syncthreads();  // every thread has read its staged elements
 #pragma unroll
-    for (int j = 0; j < KF_IPT; ++j) {
+    for (int j = 0; j < LV_IPT; ++j) {
       if (i0 + j >= m) break;
       sv[lds_pad((int)q[j])] = v[j];
       sd[lds_pad((int)q[j])] = dst[j];
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < KF_IPT; ++j) {
-      const int r = j * KF_BS + (int)threadIdx.x;
+    for (int j = 0; j < LV_IPT; ++j) {
+      const int r = j * LV_BS + (int)threadIdx.x;
       if (tb + r < m) next[sd[lds_pad(r)]] = sv[lds_pad(r)];
     }
   }
   for (int o = 32; o > 0; o >>= 1) dis += __shfl_xor(dis, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dis;
   __syncthreads();
-  if (threadIdx.x == 0) dpart[blockIdx.x] += red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+#pragma unroll
+    for (int w = 0; w < LV_BS / 64; ++w) t += red[w];
+    dpart[blockIdx.x] += t;
+  }
 }
 
 // tau-a from the exact counts: k_kfinal's fp64 order (kendall.hip) for one set of m elements
@@ -421,9 +434,9 @@ static int kf_run(int64_t m, const KfWs& w, double* out, hipStream_t st) {
     k_kf_lvl_count<<<(unsigned)nt, KF_BS, 0, st>>>(cur, m, b, w.tile, bstart);
     VR_CHECK_LAUNCH();
     VR_TRY(scan_exclusive_u32(w.tile, w.tile, nt, w.tot + 2, w.scan, st));
-    k_kf_lvl_bucket<<<(unsigned)nt, KF_BS, 0, st>>>(cur, m, b, w.tile, bP);
+    k_kf_lvl_bucket<<<(unsigned)nt, LV_BS, 0, st>>>(cur, m, b, w.tile, bP);
     VR_CHECK_LAUNCH();
-    k_kf_lvl_split<<<(unsigned)nt, KF_BS, 0, st>>>(cur, m, b, w.tile, bstart, bP, nbk, w.tot + 2,
+    k_kf_lvl_split<<<(unsigned)nt, LV_BS, 0, st>>>(cur, m, b, w.tile, bstart, bP, nbk, w.tot + 2,
                                                    b > 0 ? next : nullptr, w.dpart);
     VR_CHECK_LAUNCH();
     std::swap(cur, next);
