@@ -7,8 +7,9 @@
 // reference's tau-a conversion, in k_kfinal's fp64 operation order (kendall.hip):
 //   1  sort (y key, index) by y               radix_sort_kv (sort.hip)
 //      dense y rank r of every sorted position, y tie pairs (sum over groups of C(k, 2))
-//   2  gather the x key of each y-sorted element, stable sort by it: the (x, y)-lexicographic
-//      order with the sequence of y ranks r; x tie pairs and joint (x, y) tie pairs
+//      (the x keys ride along as the sort's payload)
+//   2  stable sort of those dense y ranks by their x keys: the (x, y)-lexicographic order
+//      with the sequence of y ranks r; x tie pairs and joint (x, y) tie pairs
 //   3  discordant pairs = inversions of that r sequence, counted bit by bit of r from the top
 //      (an MSD binary radix split: at level b the sequence is stably ordered by r >> (b+1);
 //      a pair i < j with r_i > r_j has its highest differing bit at exactly one level, where
@@ -162,14 +163,11 @@ __global__ __launch_bounds__(KF_BS) void k_kf_tie_pairs(const uint32_t* __restri
   if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-// y-sorted position i -> (x key of its element, its dense y rank): the sort payload of step 2
-__global__ void k_kf_xkeys(const uint32_t* __restrict__ kx, const uint32_t* __restrict__ order,
-                           const uint32_t* __restrict__ flags, const uint32_t* __restrict__ gidx, int64_t m,
-                           uint32_t* __restrict__ xs, uint32_t* __restrict__ r) {
+// dense y rank of every y-sorted position: the sort payload of step 2
+__global__ void k_kf_yrank(const uint32_t* __restrict__ flags, const uint32_t* __restrict__ gidx, int64_t m,
+                           uint32_t* __restrict__ r) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  xs[i] = kx[order[i]];
-  r[i] = kf_rank(flags, gidx, i);
+  if (i < m) r[i] = kf_rank(flags, gidx, i);
 }
 
 // dense ranks back to element order: rank[order[i]] = rank of sorted position i
@@ -404,22 +402,21 @@ static int kf_groups(const uint32_t* k1, const uint32_t* k2, int64_t m, const Kf
   return VR_OK;
 }
 
-// the u32 pipeline on w.kx / w.ky (m >= 2): tau-a into out
+// the u32 pipeline on w.kx / w.ky (m >= 2, both overwritten): tau-a into out
 static int kf_run(int64_t m, const KfWs& w, double* out, hipStream_t st) {
   const int64_t nt = kf_tiles(m);
   VR_CHECK_HIP(hipMemsetAsync(w.dpart, 0, (size_t)nt * sizeof(uint64_t), st));
-  // 1  y order, dense y ranks, y ties
-  VR_CHECK_HIP(hipMemcpyAsync(w.a, w.ky, (size_t)m * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-  k_kf_iota<<<kf_blocks(m), 256, 0, st>>>(w.b, m);
+  // 1  y order with the x keys as the payload (no element order, no gather), dense y ranks,
+  //    y ties
+  //    (in place: kx / ky are not read again)
+  VR_TRY(radix_sort_kv(w.ky, w.kx, w.c, w.d, m, w.radix, st));  // ky: sorted y keys, kx: x keys in y order
+  VR_TRY(kf_groups(w.ky, nullptr, m, w, w.tot, KFP_YT, st));     // tot[0]: distinct y values G
+  // 2  (x, y)-lexicographic order: the dense y ranks, stably sorted by the x keys
+  k_kf_yrank<<<kf_blocks(m), 256, 0, st>>>(w.flags, w.gidx, m, w.d);
   VR_CHECK_LAUNCH();
-  VR_TRY(radix_sort_kv(w.a, w.b, w.c, w.d, m, w.radix, st));  // a: sorted y keys, b: element order
-  VR_TRY(kf_groups(w.a, nullptr, m, w, w.tot, KFP_YT, st));    // tot[0]: distinct y values G
-  // 2  (x, y)-lexicographic order: x keys of the y-sorted elements, stable sort by them
-  k_kf_xkeys<<<kf_blocks(m), 256, 0, st>>>(w.kx, w.b, w.flags, w.gidx, m, w.c, w.d);
-  VR_CHECK_LAUNCH();
-  VR_TRY(radix_sort_kv(w.c, w.d, w.a, w.b, m, w.radix, st));  // c: sorted x keys, d: y ranks
-  VR_TRY(kf_groups(w.c, nullptr, m, w, w.tot + 1, KFP_XT, st));
-  VR_TRY(kf_groups(w.c, w.d, m, w, w.tot + 1, KFP_NT, st));
+  VR_TRY(radix_sort_kv(w.kx, w.d, w.a, w.c, m, w.radix, st));  // kx: sorted x keys, d: y ranks
+  VR_TRY(kf_groups(w.kx, nullptr, m, w, w.tot + 1, KFP_XT, st));
+  VR_TRY(kf_groups(w.kx, w.d, m, w, w.tot + 1, KFP_NT, st));
   // 3  inversions of the y ranks d, most significant level first (levels: bits of G - 1)
   uint32_t G = 0;
   VR_CHECK_HIP(hipMemcpyAsync(&G, w.tot, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
