@@ -490,13 +490,13 @@ def configs2_leg(dev) -> dict:
     from visreps_amd._lib import lib as _vlib
     sf_form = ["bucketed count tables", "count tables", "radix sort"][_vlib().vr_spearman_full_last_form()]
     # algorithmic bytes per pair of the bucketed count-table form (both RDMs together): key
-    # range 8 (both triangles read), bucket histograms 8, bucket records 8 read + 12 written,
-    # per-key counts 12 read, dot 8 read + one 4-B table read of B -> 60 B per pair. Its time
-    # goes to scattered record writes and one random table read per pair (transaction-, not
-    # byte-bound), so the frac on these bytes is low; vs_sort_model restates the time on the
-    # round-5 sort pipeline's ~120 B per pair and RDM (the model VERDICT r5 #6 set its 0.45 /
-    # 180 ms target on).
-    bpp = 60
+    # range 8 (both triangles read), key offsets 8 read + 8 written, B's two keys-only LSD
+    # passes 2 x 12, A's two (kA, kB) passes 2 x 20, bucket starts 8, per-key counts 8, dot 8
+    # read + one 4-B random read of B's table + A's (cached) 4 -> 120 B per pair. The dot's
+    # random table read costs a line each (transaction-, not byte-bound); vs_sort_model
+    # restates the time on the round-5 sort pipeline's ~120 B per pair and RDM (the model
+    # VERDICT r5 #6 set its 0.45 / 180 ms target on).
+    bpp = 120
     gbs = bpp * M / (sf_ms / 1e3) / 1e9
     sort_model = 2 * 120 * M / (sf_ms / 1e3) / 1e9 / HBM_PEAK_GBS
     out = {"n": n, "d": d, "voxels": v, "rdm_ms": round(call_ms, 2), "gram_ms": round(gram_ms, 2),
@@ -505,8 +505,9 @@ def configs2_leg(dev) -> dict:
                              "form": sf_form, "pairs_per_s": round(M / (sf_ms / 1e3), 1),
                              "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                                           "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                          "algorithmic_bytes_model": "60 B per pair, both RDMs (key range 8, bucket "
-                                          "histograms 8, records 8 + 12, counts 12, dot 8 + 4 random)",
+                                          "algorithmic_bytes_model": "120 B per pair, both RDMs (key range 8, key "
+                                          "offsets 16, B radix 2 x 12, A radix 2 x 20, bucket starts 8, counts 8, "
+                                          "dot 16 incl. one 4-B random read)",
                                           "vs_sort_model": round(sort_model, 4)}},
            "kendall_full": {"ms": round(kt[1], 2), "first_call_ms": round(kt[0], 2), "pairs": M, "tau_a": tau,
                             "note": "vr_kendall_full_f32 (kendall_full.hip): 2 radix sorts + one inversion level per "
