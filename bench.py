@@ -122,7 +122,7 @@ def split_mode(n: int, dims: dict) -> bool:
     return mode == "split" or all(float(n) * n * d >= 1e10 for d in dims.values())
 
 
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r5_pmc_engine_grid.json")
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r6_pmc_engine_grid.json")
 
 
 def pmc_traffic(n: int, est: bool):

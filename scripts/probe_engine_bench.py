@@ -64,7 +64,8 @@ if os.environ.get("CHECK_EXACT", "1") == "1" and os.environ.get("VISREPS_ENGINE_
     os.environ["VISREPS_ENGINE_EST"] = "0"  # the same RDMs in the exact form, same process
     ref = R.bootstrap_spearman_multi(neural, models, idx)
     os.environ["VISREPS_ENGINE_EST"] = "1"
-    ref_note = f" exact_equal={bool(torch.equal(ref, s))} max_diff={float((ref - s).abs().max()):.3g}"
+    s0 = s[: len(models)]  # JOINED: the first region's units (V1, the reference's neural plan)
+    ref_note = f" exact_equal={bool(torch.equal(ref, s0))} max_diff={float((ref - s0).abs().max()):.3g}"
 print(f"engine bench-RDMs NB={len(models)}: {min(ts) / len(models):.2f} ms/unit  "
       f"checksum={float(s.double().sum()):.15g} est_reruns={int(_lib.lib().vr_engine_est_reruns())}{ref_note}",
       flush=True)
