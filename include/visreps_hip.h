@@ -358,6 +358,15 @@ int vr_spearman_full_subset_f32(const float* A, const float* B, int64_t n, int64
  * visreps_amd/analysis/distributed_spearman.py): sortable keys of fp32 values, an in-place
  * (key, value) radix sort, doubled midranks (+ 2 base) of a sorted key run with its tie
  * term sum (k^3 - k) as a u128 {lo, hi}, and an exact u64 dot product (u128 {lo, hi}). */
+/* Count-table form of the same global rank (no sort, no key exchange): per-key counts of a
+ * rank's sortable keys in [kmin, kmin + bins) into cnt[bins + 1] (zeroed by the caller;
+ * atomics), which the caller sums over ranks; then, on the summed table, the tie term sum
+ * (c^3 - c) as a u128 {lo, hi}, the table turned into exclusive starts in place, and the
+ * doubled midranks cnt[k] + cnt[k + 1] + 1 of this rank's keys. */
+int vr_key_counts_u32(const uint32_t* keys, int64_t m, uint32_t kmin, int64_t bins, uint32_t* cnt, void* stream);
+size_t vr_key_table_workspace(int64_t bins);
+int vr_key_table_midranks(const uint32_t* keys, int64_t m, uint32_t kmin, uint32_t* cnt, int64_t bins, uint64_t* y,
+                          uint64_t* tie, void* ws, size_t ws_bytes, void* stream);
 int vr_f32_sort_keys(const float* v, int64_t m, uint32_t* keys, void* stream);
 size_t vr_sort_pairs_workspace(int64_t m);
 int vr_sort_pairs_u32(uint32_t* keys, uint32_t* vals, int64_t m, void* ws, size_t ws_bytes,

@@ -1,8 +1,9 @@
-"""Distributed full-triangle Spearman by sample sort (analysis/distributed_spearman.py,
-SURVEY.md §8(f4)). CPU: gloo world 2 and 3, pairs spread over ranks at random, the device
-pieces (sort keys, radix sort, midranks, exact dot) emulated in numpy; the collectives,
-splitters, bucket exchange, global offsets and owner routing are the product code; the
-score must equal the oracle's midrank Spearman. GPU: world 1 through the HIP pieces equals
+"""Distributed full-triangle Spearman (analysis/distributed_spearman.py),
+in its count-table form and its sample-sort form. CPU: gloo world 2 and 3, pairs spread over
+ranks at random, the device pieces (sort keys, radix sort, midranks, per-key counts, table
+midranks, exact dot) emulated in numpy; the collectives, key range, table all-reduce,
+splitters, bucket exchange, global offsets and owner routing are the product code; the score
+must equal the oracle's midrank Spearman. GPU: world 1 through the HIP pieces equals
 spearman_full bit for bit."""
 import os
 import socket
@@ -46,6 +47,20 @@ class NumpyRankKernels(DS.RankKernels):
         return torch.from_numpy(y.astype(np.int64)), tie
 
     @staticmethod
+    def counts(keys, kmin, bins):
+        k = keys.numpy().view(np.uint32).astype(np.int64) - int(kmin)
+        return torch.from_numpy(np.bincount(k, minlength=bins + 1).astype(np.int64))
+
+    @staticmethod
+    def table_midranks(keys, kmin, counts):
+        c = counts.numpy().astype(np.int64)
+        start = np.concatenate([[0], np.cumsum(c)])[:-1]  # exclusive, bins + 1 entries
+        k = keys.numpy().view(np.uint32).astype(np.int64) - int(kmin)
+        y = start[k] + start[k + 1] + 1
+        tie = sum(int(v) ** 3 - int(v) for v in c[c > 1])
+        return torch.from_numpy(y.astype(np.int64)), tie
+
+    @staticmethod
     def dot(a, b):
         return int(np.dot(a.numpy().astype(object), b.numpy().astype(object)))
 
@@ -67,8 +82,10 @@ def _tri(n, seed, levels=None, nan=False):
     return r[np.triu_indices(n, 1)]
 
 
-def _worker(rank, world, port, n, seed, levels, nan, out_dir):
+def _worker(rank, world, port, n, seed, levels, nan, out_dir, method="tables", cap=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if cap:  # a key range beyond the table cap: the count-table form falls back to the sample sort
+        DS.TABLE_CAP = cap
     dist.init_process_group("gloo", rank=rank, world_size=world)
     a, b = _tri(n, seed, levels), _tri(n, seed + 1, None, nan)
     M = len(a)
@@ -78,17 +95,19 @@ def _worker(rank, world, port, n, seed, levels, nan, out_dir):
     ownb = np.random.RandomState(seed + 8).randint(0, world, size=M)
     mineb = np.flatnonzero(ownb == rank)
     r = DS.distributed_spearman(torch.from_numpy(a[mine]), torch.from_numpy(mine), torch.from_numpy(b[mineb]),
-                                torch.from_numpy(mineb), M, dist.group.WORLD, NumpyRankKernels())
+                                torch.from_numpy(mineb), M, dist.group.WORLD, NumpyRankKernels(), method=method)
     with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
         f.write(repr(r))
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("method", ["tables", "sort"])
 @pytest.mark.parametrize("n,world,levels,nan", [(60, 2, None, False), (150, 3, 6, False), (90, 2, 4, True),
                                                 (33, 3, None, False)])
-def test_gloo_distributed_spearman_matches_oracle(tmp_path, n, world, levels, nan):
+def test_gloo_distributed_spearman_matches_oracle(tmp_path, n, world, levels, nan, method):
     seed = n + world
-    mp.spawn(_worker, args=(world, _free_port(), n, seed, levels, nan, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, seed, levels, nan, str(tmp_path), method), nprocs=world,
+             join=True)
     got = [float((tmp_path / f"r{r}.txt").read_text()) for r in range(world)]
     a, b = _tri(n, seed, levels), _tri(n, seed + 1, None, nan)
     if nan:
@@ -99,15 +118,26 @@ def test_gloo_distributed_spearman_matches_oracle(tmp_path, n, world, levels, na
     assert abs(got[0] - ref) <= 1e-12
 
 
+def test_gloo_tables_fall_back_to_sample_sort_beyond_the_cap(tmp_path):
+    n, world = 70, 2
+    seed = 11
+    mp.spawn(_worker, args=(world, _free_port(), n, seed, None, False, str(tmp_path), "tables", 16), nprocs=world,
+             join=True)
+    got = [float((tmp_path / f"r{r}.txt").read_text()) for r in range(world)]
+    ref = O.midrank_spearman(_tri(n, seed), _tri(n, seed + 1))
+    assert got[0] == got[1] and abs(got[0] - ref) <= 1e-12
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("method", ["tables", "sort"])
 @pytest.mark.parametrize("n,levels", [(500, None), (2000, 7)])
-def test_world1_hip_pieces_equal_spearman_full(dev, n, levels):
+def test_world1_hip_pieces_equal_spearman_full(dev, n, levels, method):
     from visreps_amd.analysis import rsa as R
 
     a, b = _tri(n, 3, levels), _tri(n, 4)
     M = len(a)
     got = DS.distributed_spearman(torch.from_numpy(a).to(dev), torch.arange(M, device=dev),
-                                  torch.from_numpy(b).to(dev), torch.arange(M, device=dev), M)
+                                  torch.from_numpy(b).to(dev), torch.arange(M, device=dev), M, method=method)
     full = np.zeros((n, n), np.float32)
     iu = np.triu_indices(n, 1)
     full[iu] = a

@@ -164,6 +164,9 @@ _PROTOTYPES = {
     "vr_spearman_full_workspace": (_c_sz, [_c_i64]),
     "vr_spearman_full_sort_workspace": (_c_sz, [_c_i64]),
     "vr_spearman_full_last_form": (ctypes.c_int, []),
+    "vr_key_counts_u32": (ctypes.c_int, [_vp, _c_i64, ctypes.c_uint32, _c_i64, _vp, _vp]),
+    "vr_key_table_workspace": (_c_sz, [_c_i64]),
+    "vr_key_table_midranks": (ctypes.c_int, [_vp, _c_i64, ctypes.c_uint32, _vp, _c_i64, _vp, _vp, _vp, _c_sz, _vp]),
     "vr_spearman_full_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _vp, _c_sz, _vp]),
     "vr_spearman_full_subset_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _c_sz, _vp]),
     "vr_kendall_full_subset_f32": (ctypes.c_int, [_vp, _vp, _c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _c_sz, _vp]),

@@ -19,6 +19,12 @@ Per RDM, every rank holds an arbitrary subset of the M pairs: (fp32 value, trian
 Then sum yA yB over each rank's t range (vr_dot_u64), and the u128 sums and tie terms are
 all-reduced as 16-bit limbs (exact in int64 for any world size), and rho follows the
 engine's exact formula. Results equal spearman_full / the rank-plan engine bit for bit.
+
+The default count-table form (global_midranks_tables, spearman_full's idea) replaces steps
+1-4: the global key range by all-reduce, each rank's per-key counts (vr_key_counts_u32)
+summed by one all-reduce, then every rank's doubled midranks and the tie term from the
+summed table (vr_key_table_midranks) -- no sort and no key exchange; step 5 routes (t, y)
+as before.
 """
 from __future__ import annotations
 
@@ -31,7 +37,7 @@ import torch.distributed as dist
 
 from .._lib import check, lib, stream_of, workspace
 
-__all__ = ["RankKernels", "distributed_spearman", "global_midranks"]
+__all__ = ["RankKernels", "distributed_spearman", "global_midranks", "global_midranks_tables"]
 
 
 def _u32(x: torch.Tensor) -> torch.Tensor:
@@ -71,6 +77,31 @@ class RankKernels:
         ws = workspace.get(dev, L.vr_midranks_workspace(m), "dist_midranks")
         check(L.vr_midranks_sorted(keys_sorted.data_ptr(), m, int(base), y.data_ptr(), tie.data_ptr(),
                                    ws.data_ptr(), ws.numel(), stream_of(dev)), "vr_midranks_sorted")
+        lo, hi = (int(v) & 0xFFFFFFFFFFFFFFFF for v in tie.cpu().tolist())
+        return y, lo | (hi << 64)
+
+    @staticmethod
+    def counts(keys: torch.Tensor, kmin: int, bins: int) -> torch.Tensor:
+        """Per-key counts of keys in [kmin, kmin + bins) as int64[bins + 1] (last entry 0)."""
+        dev = keys.device
+        cnt = torch.zeros(bins + 1, dtype=torch.int32, device=dev)
+        check(lib().vr_key_counts_u32(keys.data_ptr(), keys.numel(), int(kmin), int(bins), cnt.data_ptr(),
+                                      stream_of(dev)), "vr_key_counts_u32")
+        return cnt.to(torch.int64) & 0xFFFFFFFF
+
+    @staticmethod
+    def table_midranks(keys: torch.Tensor, kmin: int, counts: torch.Tensor) -> Tuple[torch.Tensor, int]:
+        """Doubled midranks of keys from the global per-key counts, and the tie term."""
+        dev = keys.device
+        bins = counts.numel() - 1
+        cnt = counts.to(torch.int32).contiguous()  # < 2^32 each: the u32 bit pattern
+        y = torch.empty(keys.numel(), dtype=torch.int64, device=dev)
+        tie = torch.zeros(2, dtype=torch.int64, device=dev)
+        L = lib()
+        ws = workspace.get(dev, L.vr_key_table_workspace(bins), "dist_table")
+        check(L.vr_key_table_midranks(keys.data_ptr(), keys.numel(), int(kmin), cnt.data_ptr(), bins, y.data_ptr(),
+                                      tie.data_ptr(), ws.data_ptr(), ws.numel(), stream_of(dev)),
+              "vr_key_table_midranks")
         lo, hi = (int(v) & 0xFFFFFFFFFFFFFFFF for v in tie.cpu().tolist())
         return y, lo | (hi << 64)
 
@@ -164,9 +195,15 @@ def global_midranks(values: torch.Tensor, tidx: torch.Tensor, M: int, pg=None,
     y, tie = K.midranks(rk, offset)
     tie = _allreduce_int(tie, dev, pg)
     # 5. (t, y) to the owner of t
+    return _to_owners(_u32(rt), y, M, pg), tie
+
+
+def _to_owners(tt: torch.Tensor, y: torch.Tensor, M: int, pg) -> torch.Tensor:
+    """Route (t, y) to the rank owning t ([M r / W, M (r+1) / W)); that rank's dense y."""
+    rank, world = _world(pg)
+    dev = y.device
     lo = M * rank // world
     hi = M * (rank + 1) // world
-    tt = _u32(rt)
     owner = ((tt + 1) * world - 1) // M  # the r with M r // W <= t < M (r + 1) // W
     order = torch.argsort(owner, stable=True)
     oc = torch.bincount(owner, minlength=world).cpu().tolist() if owner.numel() else [0] * world
@@ -174,21 +211,63 @@ def global_midranks(values: torch.Tensor, tidx: torch.Tensor, M: int, pg=None,
     gy = _a2a(y[order], oc, pg)
     dense = torch.empty(hi - lo, dtype=torch.int64, device=dev)
     dense[gt - lo] = gy
-    return dense, tie
+    return dense
+
+
+# the count-table form while the key range has at most this many keys (2^27: two 1-GB int64
+# tables per RDM in the all-reduce); the sample sort beyond
+TABLE_CAP = 1 << 27
+
+
+def global_midranks_tables(values: torch.Tensor, tidx: torch.Tensor, M: int, pg=None,
+                           kernels: RankKernels = None) -> Tuple[torch.Tensor, int]:
+    """global_midranks without a sort: the key range [kmin, kmax] by two all-reduces, every
+    rank's per-key counts summed by one all-reduce, then each rank's doubled midranks from
+    the summed table (start + end + 1 of its key's group) and the (t, y) routing of step 5.
+    Falls back to the sample sort when the key range exceeds TABLE_CAP (e.g. values far
+    outside a correlation distance's [0, 2]). NaN-free values (the caller checks)."""
+    K = kernels or KERNELS
+    rank, world = _world(pg)
+    dev = values.device
+    keys = K.keys(values.float().contiguous())
+    ku = _u32(keys)
+    ext = torch.tensor([int(ku.min()) if ku.numel() else 1 << 32, -int(ku.max()) if ku.numel() else 0],
+                       dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(ext, op=dist.ReduceOp.MIN, group=pg)
+    kmin, kmax = int(ext[0]), -int(ext[1])
+    if kmax < kmin:  # no pairs anywhere
+        return torch.empty(0, dtype=torch.int64, device=dev), 0
+    bins = kmax - kmin + 1
+    if bins > TABLE_CAP:
+        return global_midranks(values, tidx, M, pg, K)
+    cnt = K.counts(keys, kmin, bins)
+    if world > 1:
+        dist.all_reduce(cnt, group=pg)
+    y, tie = K.table_midranks(keys, kmin, cnt)
+    return _to_owners(_u32(tidx.to(torch.int64)), y, M, pg), tie
 
 
 def distributed_spearman(a_values: torch.Tensor, a_tidx: torch.Tensor, b_values: torch.Tensor,
-                         b_tidx: torch.Tensor, M: int, pg=None, kernels: RankKernels = None) -> float:
-    """Spearman of two triangles of M pairs, each spread over the ranks as (values, t)."""
+                         b_tidx: torch.Tensor, M: int, pg=None, kernels: RankKernels = None,
+                         method: str = "tables") -> float:
+    """Spearman of two triangles of M pairs, each spread over the ranks as (values, t).
+    method "tables": per-key count tables summed over ranks (global_midranks_tables; the
+    sample sort when a key range is too wide); "sort": the sample sort (global_midranks)."""
+    if method not in ("tables", "sort"):
+        raise ValueError(f"method={method!r}: tables or sort")
     K = kernels or KERNELS
     dev = a_values.device
-    ya, ta = global_midranks(a_values, a_tidx, M, pg, K)
-    yb, tb = global_midranks(b_values, b_tidx, M, pg, K)
-    ab = _allreduce_int(K.dot(ya, yb), dev, pg)
     nan = torch.tensor([int(torch.isnan(a_values).any()) + int(torch.isnan(b_values).any())],
                        dtype=torch.int64, device=dev)
     if _world(pg)[1] > 1:
         dist.all_reduce(nan, group=pg)
+    if int(nan.item()) or M < 2:  # scipy: NaN in either triangle or fewer than two pairs
+        return float("nan")
+    ranks = global_midranks_tables if method == "tables" else global_midranks
+    ya, ta = ranks(a_values, a_tidx, M, pg, K)
+    yb, tb = ranks(b_values, b_tidx, M, pg, K)
+    ab = _allreduce_int(K.dot(ya, yb), dev, pg)
     mu = M * (M + 1) ** 2
     sq = 4 * (M * (M + 1) * (2 * M + 1) // 6)
     va = sq - ta // 3 - mu

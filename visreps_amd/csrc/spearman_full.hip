@@ -1038,6 +1038,62 @@ int vr_midranks_sorted(const uint32_t* keys, int64_t m, uint64_t base, uint64_t*
   return VR_OK;
 }
 
+// ---- count-table form of the distributed global rank: per-key counts of a rank's keys,
+// all-reduced by the caller, then starts, tie terms and the doubled midranks of its keys
+__global__ void k_key_counts(const uint32_t* __restrict__ keys, int64_t m, uint32_t kmin,
+                             uint32_t* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) atomicAdd(&cnt[keys[i] - kmin], 1u);
+}
+
+__global__ void k_key_midranks(const uint32_t* __restrict__ keys, int64_t m, uint32_t kmin,
+                               const uint32_t* __restrict__ start, uint64_t* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) {
+    const uint32_t k = keys[i] - kmin;
+    y[i] = (uint64_t)start[k] + start[k + 1] + 1u;
+  }
+}
+
+int vr_key_counts_u32(const uint32_t* keys, int64_t m, uint32_t kmin, int64_t bins, uint32_t* cnt, void* stream) {
+  VR_REQUIRE(m >= 0 && bins >= 1 && bins < ((int64_t)1 << 32), "vr_key_counts_u32: m=%lld bins=%lld",
+             (long long)m, (long long)bins);
+  if (m == 0) return VR_OK;
+  VR_REQUIRE(keys && cnt, "vr_key_counts_u32: null pointer");
+  k_key_counts<<<(unsigned)((m + 255) / 256), 256, 0, as_stream(stream)>>>(keys, m, kmin, cnt);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+size_t vr_key_table_workspace(int64_t bins) {
+  Carver c(nullptr);
+  c.take<uint32_t>(scan_ws_elems(std::max<int64_t>(bins, 1) + 1));
+  c.take<uint64_t>((size_t)full_grid() * 2);
+  return c.bytes();
+}
+
+int vr_key_table_midranks(const uint32_t* keys, int64_t m, uint32_t kmin, uint32_t* cnt, int64_t bins, uint64_t* y,
+                          uint64_t* tie, void* ws, size_t ws_bytes, void* stream) {
+  VR_REQUIRE(m >= 0 && bins >= 1 && bins < ((int64_t)1 << 32) && cnt && tie,
+             "vr_key_table_midranks: m=%lld bins=%lld", (long long)m, (long long)bins);
+  VR_REQUIRE(ws && ws_bytes >= vr_key_table_workspace(bins), "vr_key_table_midranks: workspace");
+  hipStream_t st = as_stream(stream);
+  Carver c(ws);
+  uint32_t* sw = c.take<uint32_t>(scan_ws_elems(bins + 1));
+  uint64_t* part = c.take<uint64_t>((size_t)full_grid() * 2);
+  k_tab_ties<<<full_grid(), FULL_BS, 0, st>>>(cnt, bins, part);
+  VR_CHECK_LAUNCH();
+  k_reduce_u128<<<1, FULL_BS, 0, st>>>(part, full_grid(), tie);
+  VR_CHECK_LAUNCH();
+  VR_TRY(scan_exclusive_u32(cnt, cnt, bins + 1, nullptr, sw, st));
+  if (m > 0) {
+    VR_REQUIRE(keys && y, "vr_key_table_midranks: null pointer");
+    k_key_midranks<<<(unsigned)((m + 255) / 256), 256, 0, st>>>(keys, m, kmin, cnt, y);
+    VR_CHECK_LAUNCH();
+  }
+  return VR_OK;
+}
+
 size_t vr_dot_u64_workspace(void) { return (size_t)full_grid() * 2 * sizeof(uint64_t) + 256; }
 
 int vr_dot_u64(const uint64_t* a, const uint64_t* b, int64_t m, uint64_t* out, void* ws, size_t ws_bytes,
