@@ -146,3 +146,26 @@ def test_world1_hip_pieces_equal_spearman_full(dev, n, levels, method):
     fb = np.triu(full, 1) + np.triu(full, 1).T
     ref = R.spearman_full(torch.from_numpy(fa).to(dev), torch.from_numpy(fb).to(dev))
     assert got == ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nkeys", [3, 3000])
+def test_world1_tables_few_keys(dev, nkeys):
+    # a small key range: per-block LDS counts (vr_key_counts_u32 at <= 16384 keys)
+    from visreps_amd.analysis import rsa as R
+
+    n = 1500
+    g = np.random.default_rng(nkeys)
+    tri = lambda k: (0x3F800000 + g.integers(0, k, n * (n - 1) // 2)).astype(np.uint32).view(np.float32)
+    a, b = tri(nkeys), tri(nkeys + 5)
+    M = len(a)
+    got = DS.distributed_spearman(torch.from_numpy(a).to(dev), torch.arange(M, device=dev),
+                                  torch.from_numpy(b).to(dev), torch.arange(M, device=dev), M)
+    assert abs(got - O.midrank_spearman(a, b)) <= 1e-12
+    full = np.zeros((n, n), np.float32)
+    iu = np.triu_indices(n, 1)
+    full[iu] = a
+    fa = full + full.T
+    full[iu] = b
+    fb = np.triu(full, 1) + np.triu(full, 1).T
+    assert got == R.spearman_full(torch.from_numpy(fa).to(dev), torch.from_numpy(fb).to(dev))

@@ -523,6 +523,32 @@ def test_spearman_full_wide_key_range_takes_the_sort_form(dev):
     workspace.release("spearman_full")
 
 
+@pytest.mark.parametrize("nkeys", [1, 2, 200, 5000])
+def test_spearman_full_few_adjacent_keys(dev, nkeys):
+    # values on nkeys consecutive fp32 keys (1.0 + k ulp): a key range of <= 4096 keys puts one
+    # key in each bucket (counts = bucket sizes); 5000 keys: W = 2 keys per bucket
+    n = 900
+    g = np.random.default_rng(nkeys)
+    u = (0x3F800000 + g.integers(0, nkeys, (n, n))).astype(np.uint32)
+    ra = np.triu(u.view(np.float32), 1)
+    ra = (ra + ra.T).astype(np.float32)
+    ub = (0x3F800000 + g.integers(0, max(2, nkeys // 3), (n, n))).astype(np.uint32)
+    rb = np.triu(ub.view(np.float32), 1)
+    rb = (rb + rb.T).astype(np.float32)
+    from visreps_amd._lib import lib, workspace
+    workspace.get(dev, 1 << 30, "spearman_full")
+    ta, tb = torch.from_numpy(ra).to(dev), torch.from_numpy(rb).to(dev)
+    got = R.spearman_full(ta, tb)
+    assert lib().vr_spearman_full_last_form() == 0
+    ref = R.compute_rdm_correlation(ta, tb, correlation="Spearman")
+    if nkeys == 1:  # a constant triangle
+        assert np.isnan(got) and np.isnan(ref)
+        return
+    assert got == ref
+    iu = np.triu_indices(n, 1)
+    assert abs(got - O.midrank_spearman(ra[iu], rb[iu])) <= 1e-12
+
+
 def test_spearman_full_nan_and_constant(dev):
     a = torch.rand(50, 50, device=dev)
     a = (a + a.T) / 2

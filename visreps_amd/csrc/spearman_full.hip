@@ -14,10 +14,10 @@
 // bucketed count tables (default; both ranges <= 2^26 keys): see k_cb_* below -- block
 //   histograms of coarse key buckets, records written bucket by bucket, per-key counts in
 //   LDS, one random 8-B table read per pair in the dot
-// plain count tables (ranges up to the workspace, VISREPS_FULL_FORM=table):
+// plain count tables (only when VISREPS_FULL_FORM=table names them):
 //            k_tab_count    global-atomic counts of both triangles' keys
 //            k_tab_ties + scan, k_tab_dot (two random table reads per pair)
-// sort form (key range beyond the workspace, or VISREPS_FULL_FORM=sort):
+// sort form (key ranges beyond 2^26 keys or the workspace, or VISREPS_FULL_FORM=sort):
 //   per RDM  k_full_keys    (sortable fp32 key, triangle index t) of every pair
 //            radix_sort_kv  by key (sort.hip; u32 offsets, M < 2^32)
 //            k_tile_bounds  first / last tie-group start of every 4096-position tile
@@ -506,6 +506,12 @@ __global__ void k_cb_bstart(const uint32_t* __restrict__ keys, int64_t M, int sh
     for (int x = g + 1; x <= nb; ++x) bstart[x] = (uint32_t)M;
 }
 
+// one key per bucket (sh = 0): the counts are the bucket sizes
+__global__ void k_cb_sizes(const uint32_t* __restrict__ bstart, int nb, uint32_t* __restrict__ cnt) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < nb) cnt[g] = bstart[g + 1] - bstart[g];
+}
+
 constexpr int CB_FINE_BS = 1024;
 constexpr int64_t CB_SEG = (int64_t)1 << 21;  // records per k_cb_fine block
 constexpr int64_t CB_LDS_RUN = 2048;          // shorter runs count in global memory
@@ -802,9 +808,15 @@ static int full_cb_form(const float* A, const float* B, int64_t n, int64_t ld, c
   k_cb_bstart<<<gm, 256, 0, st>>>(bo, M, gb.sh, gb.nb, w.bsB);
   VR_CHECK_LAUNCH();
   const unsigned fb = (unsigned)((M + CB_SEG - 1) / CB_SEG);
-  k_cb_fine<1><<<fb, CB_FINE_BS, 0, st>>>(oa, M, w.bsA, ga.nb, ga.sh, w.cA);
+  if (ga.sh == 0)
+    k_cb_sizes<<<(unsigned)((ga.nb + 255) / 256), 256, 0, st>>>(w.bsA, ga.nb, w.cA);
+  else
+    k_cb_fine<1><<<fb, CB_FINE_BS, 0, st>>>(oa, M, w.bsA, ga.nb, ga.sh, w.cA);
   VR_CHECK_LAUNCH();
-  k_cb_fine<1><<<fb, CB_FINE_BS, 0, st>>>(bo, M, w.bsB, gb.nb, gb.sh, w.cB);
+  if (gb.sh == 0)
+    k_cb_sizes<<<(unsigned)((gb.nb + 255) / 256), 256, 0, st>>>(w.bsB, gb.nb, w.cB);
+  else
+    k_cb_fine<1><<<fb, CB_FINE_BS, 0, st>>>(bo, M, w.bsB, gb.nb, gb.sh, w.cB);
   VR_CHECK_LAUNCH();
   const int fg = full_grid();
   k_tab_ties<<<fg, FULL_BS, 0, st>>>(w.cA, (int64_t)ga.tab, h.part);
@@ -831,7 +843,7 @@ extern "C" {
 
 size_t vr_spearman_full_workspace(int64_t n) {
   if (n < 2) return 256;
-  return std::min(sort_bytes(n), std::max(tab_bytes(n, TAB_CAP, TAB_CAP), cb_bytes(n, CB_CAP, CB_CAP)));
+  return std::min(sort_bytes(n), cb_bytes(n, CB_CAP, CB_CAP));
 }
 
 int vr_spearman_full_last_form(void) { return g_full_form.load(); }
@@ -895,13 +907,15 @@ static int spearman_full_impl(const float* A, const float* B, int64_t n, int64_t
     return VR_OK;
   }
   const uint64_t binsA = (uint64_t)hv[1] - hv[0] + 1, binsB = (uint64_t)hv[3] - hv[2] + 1;
-  // forms in order of preference: bucketed count tables, plain count tables, sort; a form
+  // forms in order of preference: bucketed count tables, then the sort (any key range, any
+  // tie structure); the plain count tables only when VISREPS_FULL_FORM=table names them (their
+  // global atomics serialise on the few hot keys of quantized RDMs whose range is wide); a form
   // named in VISREPS_FULL_FORM (bucket / table / sort) runs when it applies and fits
   const size_t need_tab = tab_bytes(n, binsA, binsB), need_sort = sort_bytes(n);
   const bool cb_fits = binsA <= CB_CAP && binsB <= CB_CAP && cb_bytes(n, binsA, binsB) <= ws_bytes;
   const char* fe = getenv("VISREPS_FULL_FORM");
   const std::string forced = fe ? fe : "";
-  int form = cb_fits ? 0 : (need_tab <= ws_bytes ? 1 : (need_sort <= ws_bytes ? 2 : -1));
+  int form = cb_fits ? 0 : (need_sort <= ws_bytes ? 2 : -1);
   if (forced == "table" && need_tab <= ws_bytes) form = 1;
   if (forced == "sort" && need_sort <= ws_bytes) form = 2;
   g_full_form = form;
@@ -1046,6 +1060,21 @@ __global__ void k_key_counts(const uint32_t* __restrict__ keys, int64_t m, uint3
   if (i < m) atomicAdd(&cnt[keys[i] - kmin], 1u);
 }
 
+// tables of <= 16384 keys: per-block counts in LDS (a few hot keys would serialise global
+// atomics), added to the table once per block
+constexpr int KC_LDS_BINS = 16384;
+__global__ __launch_bounds__(1024) void k_key_counts_lds(const uint32_t* __restrict__ keys, int64_t m, uint32_t kmin,
+                                                         int bins, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t h[KC_LDS_BINS];
+  for (int i = threadIdx.x; i < bins; i += 1024) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < m; i += (int64_t)gridDim.x * 1024)
+    atomicAdd(&h[keys[i] - kmin], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < bins; i += 1024)
+    if (h[i]) atomicAdd(&cnt[i], h[i]);
+}
+
 __global__ void k_key_midranks(const uint32_t* __restrict__ keys, int64_t m, uint32_t kmin,
                                const uint32_t* __restrict__ start, uint64_t* __restrict__ y) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1060,7 +1089,11 @@ int vr_key_counts_u32(const uint32_t* keys, int64_t m, uint32_t kmin, int64_t bi
              (long long)m, (long long)bins);
   if (m == 0) return VR_OK;
   VR_REQUIRE(keys && cnt, "vr_key_counts_u32: null pointer");
-  k_key_counts<<<(unsigned)((m + 255) / 256), 256, 0, as_stream(stream)>>>(keys, m, kmin, cnt);
+  if (bins <= KC_LDS_BINS)
+    k_key_counts_lds<<<(unsigned)std::min<int64_t>((m + 1023) / 1024, full_grid()), 1024, 0, as_stream(stream)>>>(
+        keys, m, kmin, (int)bins, cnt);
+  else
+    k_key_counts<<<(unsigned)((m + 255) / 256), 256, 0, as_stream(stream)>>>(keys, m, kmin, cnt);
   VR_CHECK_LAUNCH();
   return VR_OK;
 }
