@@ -15,7 +15,9 @@
  *    torch.Tensor.data_ptr()); [host] pointers are host memory.
  *  - Scratch memory comes from a caller-provided workspace whose size is given by the
  *    matching *_workspace() query. The library never allocates caller-visible memory.
- *  - `stream` is a hipStream_t passed as void*; device work is asynchronous on it.
+ *  - `stream` is a hipStream_t passed as void*; device work is enqueued on it. Calls whose
+ *    launch geometry depends on device data (plan headers, key ranges, level counts)
+ *    synchronise it once before returning; INTEGRATION.md lists them.
  *    Functions are reentrant across distinct streams and workspaces.
  *  - A statistic that is undefined (constant input, NaN input, fewer than two pairs)
  *    is returned as NaN in the output value, never as an error status — the same
