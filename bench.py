@@ -473,6 +473,19 @@ def configs2_leg(dev) -> dict:
         torch.cuda.synchronize()
         sf.append(e0.elapsed_time(e1))
     first_ms, sf_ms = sf
+    # the bootstrap beyond the rank plans (rsa.bootstrap_full: evals.py:355-373 at n = 73k, one
+    # plan-free sub-RDM Spearman per draw of 0.9 n): a few RandomState(42) draws, timed
+    from visreps_amd.analysis._random import bootstrap_indices
+    nd = 8
+    bidx = torch.from_numpy(bootstrap_indices(42, n, int(0.9 * n), nd).copy()).to(dev)
+    R.bootstrap_full(rdm_m, rdm_n, bidx[:1], full_first=False)  # warm (the subset workspace)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    bscores = R.bootstrap_full(rdm_m, rdm_n, bidx, full_first=False)
+    e1.record()
+    torch.cuda.synchronize()
+    boot_ms = e0.elapsed_time(e1) / nd
+    del bidx
     from visreps_amd._lib import workspace
     workspace.release("spearman_full")
     # compare_method=kendall on the same pair (rsa.py:22-40 at 2.66e9 elements, beyond the rank
@@ -509,6 +522,12 @@ def configs2_leg(dev) -> dict:
                                           "offsets 16, B radix 2 x 12, A radix 2 x 20, bucket starts 8, counts 8, "
                                           "dot 16 incl. one 4-B random read)",
                                           "vs_sort_model": round(sort_model, 4)}},
+           "bootstrap_full": {"ms_per_draw": round(boot_ms, 2), "draws_timed": nd, "subset": int(0.9 * n),
+                              "est_1000_draws_s": round(boot_ms, 2),
+                              "first_scores": [round(float(v), 8) for v in bscores[:3].tolist()],
+                              "note": "rsa.bootstrap_full (n > 65,535: no rank plans): one vr_spearman_full_subset_f32 "
+                                      "per RandomState(42) draw on the sub-RDMs read in place; est_1000_draws_s = "
+                                      "ms_per_draw x 1000 / 1000"},
            "kendall_full": {"ms": round(kt[1], 2), "first_call_ms": round(kt[0], 2), "pairs": M, "tau_a": tau,
                             "note": "vr_kendall_full_f32 (kendall_full.hip): 2 radix sorts + one inversion level per "
                                     "bit of the y dense rank"},

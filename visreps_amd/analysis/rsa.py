@@ -430,6 +430,11 @@ def bootstrap_full(
     n = a.size(0)
     idx_t = _idx_tensor(idx, dev)
     n_sets, k = (int(idx_t.size(0)), int(idx_t.size(1))) if idx_t.numel() else (0, 0)
+    # a draw's statistic depends on its set of stimuli only (the same pairs, values and ties in
+    # any order): read each sub-RDM in ascending stimulus order, whose rows and columns are
+    # then nearly contiguous in memory (coalesced) instead of gathered at random
+    if idx_t.numel():
+        idx_t = torch.sort(idx_t, dim=1).values
     total = n_sets + (1 if full_first else 0)
     scores = torch.empty(total, dtype=torch.float64, device=dev)
     L = lib()
