@@ -2,7 +2,8 @@
 the bench's synthetic RDM shapes, HIP events around the point-only call and the full
 1001-subset call, per-kernel times from vr_ktimer where available.
 
-  python scripts/probe_kendall.py [n] [n_boot]      (CASES=unit,point ... to run a subset)
+  python scripts/probe_kendall.py [n] [n_boot]      (CASES=unit,point ... to run a subset;
+                                                     ALT_LIB=path: another library build)
 """
 import json
 import os
@@ -13,6 +14,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+if os.environ.get("ALT_LIB"):  # another library build (A/B)
+    import visreps_amd._lib as _L  # noqa: E402
+
+    _L.LIB_PATH = os.environ["ALT_LIB"]
 from visreps_amd.analysis import rsa as R  # noqa: E402
 from visreps_amd.analysis._random import bootstrap_indices  # noqa: E402
 

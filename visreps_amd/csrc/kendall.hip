@@ -37,7 +37,9 @@ namespace vr {
 constexpr int KW_THREADS = 1024;
 constexpr int KW_WAVES = KW_THREADS / 64;
 constexpr int KFIX_GROUPS = KW_THREADS / 64;
-// k_kwalk's static LDS: the per-wave partials it composes into its block summary
+// the per-wave partials a walk composes into its block summary; they live in the walk's
+// dynamic LDS, over the masks once the walk is done (kw_parts), so at n = 10k two 16-wave
+// blocks fit a CU (80 KB of masks each) instead of one
 constexpr size_t KW_STATIC_LDS = (size_t)KW_WAVES * 64 * (8 + 8 + 4 + 4 + 4);
 
 enum KField { KF_DIS = 0, KF_XTIE, KF_NTIE, KF_YTIE, KF_INCL, KF_N };
@@ -52,13 +54,13 @@ struct KCfg {
 static KCfg kendall_cfg(int64_t n) {
   KCfg c;
   const size_t need = (size_t)n * sizeof(uint64_t);
-  const size_t cap = 160 * 1024 - 1024 - KW_STATIC_LDS;
+  const size_t cap = 160 * 1024 - 1024;
   c.use_lds = need <= cap;
-  const size_t per_block = (c.use_lds ? need : 0) + KW_STATIC_LDS;
-  const int per_cu = std::max<int>(1, std::min<int>(2, (int)((160 * 1024 - 1024) / per_block)));
+  const size_t per_block = std::max(c.use_lds ? need : (size_t)0, KW_STATIC_LDS);
+  const int per_cu = std::max<int>(1, std::min<int>(2, (int)(cap / per_block)));
   c.grid = num_cus() * per_cu;
   c.nwaves = c.grid * KW_WAVES;
-  c.lds = c.use_lds ? need : 0;
+  c.lds = per_block;  // masks (LDS) and, after the walk, the partials
   return c;
 }
 
@@ -303,6 +305,55 @@ __device__ inline void ksum_push(KSum& S, uint64_t s, uint64_t g, uint64_t a, ui
   S.b = S.b & b;
 }
 
+// where a walk writes its block summaries (per pass: [block][lane])
+struct KOut {
+  uint64_t *acc, *g, *a;
+  uint32_t *b, *incl;
+};
+// the partials' arrays in the dynamic LDS (over the masks: kw_block_summary's first barrier
+// orders them after every wave's last mask read)
+struct KParts {
+  uint64_t *acc, *zl;
+  uint32_t *c, *inc, *seen;
+};
+__device__ inline KParts kw_parts(uint64_t* smem) {
+  KParts p;
+  p.acc = smem;
+  p.zl = smem + KW_WAVES * LANES;
+  uint32_t* u = reinterpret_cast<uint32_t*>(smem + 2 * KW_WAVES * LANES);
+  p.c = u;
+  p.inc = u + KW_WAVES * LANES;
+  p.seen = u + 2 * KW_WAVES * LANES;
+  return p;
+}
+
+__device__ inline void kw_block_summary(const KSeg& a, bool seen, uint32_t incl, const KOut& o, uint64_t* s_acc,
+                                        uint64_t* s_zl, uint32_t* s_c, uint32_t* s_inc, uint32_t* s_seen) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();  // the arrays' previous use is done
+  s_acc[wv * LANES + lane] = a.acc;
+  s_zl[wv * LANES + lane] = a.zlead;
+  s_c[wv * LANES + lane] = a.c;
+  s_seen[wv * LANES + lane] = seen ? 1u : 0u;
+  s_inc[wv * LANES + lane] = incl;
+  __syncthreads();
+  if (wv == 0) {
+    KSum S = ksum_identity();
+    uint32_t inc = 0;
+    for (int w = 0; w < KW_WAVES; ++w) {
+      ksum_push(S, s_acc[w * LANES + lane], s_zl[w * LANES + lane], s_c[w * LANES + lane],
+                s_seen[w * LANES + lane] == 0u);
+      inc += s_inc[w * LANES + lane];
+    }
+    const size_t off = (size_t)blockIdx.x * LANES + lane;
+    o.acc[off] = S.s;
+    o.g[off] = S.g;
+    o.a[off] = S.a;
+    o.b[off] = S.b;
+    o.incl[off] = inc;
+  }
+}
+
 template <bool LDS, bool TIE>
 __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ sflag,
@@ -376,64 +427,13 @@ __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
   // The block's 16 wave ranges are consecutive: compose them here (affine carry maps, see
   // k_kfix) and write one summary per block, so the fix-up reads grid x 64 entries instead
   // of nwaves x 64 (16x less: the single-block fix-up was bound by reading them).
-  __shared__ uint64_t s_acc[KW_WAVES][LANES], s_zl[KW_WAVES][LANES];
-  __shared__ uint32_t s_c[KW_WAVES][LANES], s_inc[KW_WAVES][LANES], s_seen[KW_WAVES][LANES];
-  const int wv = threadIdx.x >> 6;
-  s_acc[wv][lane] = a.acc;
-  s_zl[wv][lane] = a.zlead;
-  s_c[wv][lane] = a.c;
-  s_seen[wv][lane] = seen ? 1u : 0u;
-  s_inc[wv][lane] = incl;
-  __syncthreads();
-  if (wv != 0) return;
-  KSum S = ksum_identity();
-  uint32_t inc = 0;
-  for (int w = 0; w < KW_WAVES; ++w) {
-    ksum_push(S, s_acc[w][lane], s_zl[w][lane], s_c[w][lane], s_seen[w][lane] == 0u);
-    inc += s_inc[w][lane];
-  }
-  const size_t o = (size_t)blockIdx.x * LANES + lane;
-  w_acc[o] = S.s;
-  w_g[o] = S.g;
-  w_a[o] = S.a;
-  w_b[o] = S.b;
-  w_incl[o] = inc;
+  const KParts pt = kw_parts(smask);
+  kw_block_summary(a, seen, incl, KOut{w_acc, w_g, w_a, w_b, w_incl}, pt.acc, pt.zl, pt.c, pt.inc, pt.seen);
 }
 
 // The top inversion level fused with the two x-lex tie streams (A ties, joint ties): the same
 // pair codes (the x-lex order), so one walk shares the code loads, mask lookups and
 // transposes; three segment states, three block summaries (one k_kfix each).
-struct KOut {
-  uint64_t *acc, *g, *a;
-  uint32_t *b, *incl;
-};
-__device__ inline void kw_block_summary(const KSeg& a, bool seen, uint32_t incl, const KOut& o, uint64_t* s_acc,
-                                        uint64_t* s_zl, uint32_t* s_c, uint32_t* s_inc, uint32_t* s_seen) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  __syncthreads();  // the arrays' previous use is done
-  s_acc[wv * LANES + lane] = a.acc;
-  s_zl[wv * LANES + lane] = a.zlead;
-  s_c[wv * LANES + lane] = a.c;
-  s_seen[wv * LANES + lane] = seen ? 1u : 0u;
-  s_inc[wv * LANES + lane] = incl;
-  __syncthreads();
-  if (wv == 0) {
-    KSum S = ksum_identity();
-    uint32_t inc = 0;
-    for (int w = 0; w < KW_WAVES; ++w) {
-      ksum_push(S, s_acc[w * LANES + lane], s_zl[w * LANES + lane], s_c[w * LANES + lane],
-                s_seen[w * LANES + lane] == 0u);
-      inc += s_inc[w * LANES + lane];
-    }
-    const size_t off = (size_t)blockIdx.x * LANES + lane;
-    o.acc[off] = S.s;
-    o.g[off] = S.g;
-    o.a[off] = S.a;
-    o.b[off] = S.b;
-    o.incl[off] = inc;
-  }
-}
-
 template <bool LDS>
 __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk_top3(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ s0, const uint32_t* __restrict__ x0p,
@@ -481,11 +481,10 @@ __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk_top3(
       kseg_window<true>(t2, t2, plane(s2, win), a2, seen2);
     }
   }
-  __shared__ uint64_t s_acc[KW_WAVES * LANES], s_zl[KW_WAVES * LANES];
-  __shared__ uint32_t s_c[KW_WAVES * LANES], s_inc[KW_WAVES * LANES], s_seen[KW_WAVES * LANES];
-  kw_block_summary(a0, seen0, incl, o0, s_acc, s_zl, s_c, s_inc, s_seen);
-  kw_block_summary(a1, seen1, incl, o1, s_acc, s_zl, s_c, s_inc, s_seen);
-  kw_block_summary(a2, seen2, incl, o2, s_acc, s_zl, s_c, s_inc, s_seen);
+  const KParts pt = kw_parts(smask);
+  kw_block_summary(a0, seen0, incl, o0, pt.acc, pt.zl, pt.c, pt.inc, pt.seen);
+  kw_block_summary(a1, seen1, incl, o1, pt.acc, pt.zl, pt.c, pt.inc, pt.seen);
+  kw_block_summary(a2, seen2, incl, o2, pt.acc, pt.zl, pt.c, pt.inc, pt.seen);
 }
 
 // Stream total per lane: the block summaries (k_kwalk) composed in block order with carry 0
@@ -571,7 +570,7 @@ template <bool LDS>
 static int set_kwalk_attr() {
   if (!LDS) return VR_OK;
   VR_ONCE({
-    const int mx = 160 * 1024 - (int)KW_STATIC_LDS;
+    const int mx = 160 * 1024 - 1024;
     VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk<LDS, false>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, mx));
     VR_CHECK_HIP(hipFuncSetAttribute((const void*)k_kwalk<LDS, true>,
@@ -588,7 +587,7 @@ static int walk_stream(bool tie, const uint32_t* codes, const uint32_t* sflag, c
                        bool add_incl, int64_t cap, const KCfg& cfg, hipStream_t st) {
   if (cfg.use_lds) VR_TRY(set_kwalk_attr<true>());
   auto walk = [&](const uint64_t* mk, int nl, size_t o) {
-    const size_t lds = cfg.use_lds ? cfg.lds : 0;
+    const size_t lds = cfg.lds;  // the masks (LDS form) and the block-summary partials
     auto* k = cfg.use_lds ? (tie ? k_kwalk<true, true> : k_kwalk<true, false>)
                           : (tie ? k_kwalk<false, true> : k_kwalk<false, false>);
     k<<<cfg.grid, KW_THREADS, lds, st>>>(codes, sflag, aux, M, mk, n, nl, (uint32_t)cfg.nwaves, W.w_acc + o,
@@ -628,7 +627,7 @@ static int walk_top3(const uint32_t* codes, const uint32_t* lvs, const uint32_t*
                                                                W.xj_mem, M, mk, n, nl, (uint32_t)cfg.nwaves,
                                                                shift(o0, d), shift(o1, d), shift(o2, d));
     else
-      k_kwalk_top3<false><<<cfg.grid, KW_THREADS, 0, st>>>(codes, lvs, lvb, W.xa_start, W.xa_mem, W.xj_start,
+      k_kwalk_top3<false><<<cfg.grid, KW_THREADS, cfg.lds, st>>>(codes, lvs, lvb, W.xa_start, W.xa_mem, W.xj_start,
                                                           W.xj_mem, M, mk, n, nl, (uint32_t)cfg.nwaves,
                                                           shift(o0, d), shift(o1, d), shift(o2, d));
     VR_CHECK_LAUNCH();
