@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 
 #include "kcount.h"
@@ -51,13 +52,17 @@ struct KCfg {
   bool use_lds;
 };
 
+#ifndef VR_KW_MINB
+#define VR_KW_MINB 2  // walk blocks per CU the walks are compiled for (launch bounds)
+#endif
 static KCfg kendall_cfg(int64_t n) {
   KCfg c;
   const size_t need = (size_t)n * sizeof(uint64_t);
   const size_t cap = 160 * 1024 - 1024;
-  c.use_lds = need <= cap;
+  const char* e = getenv("VISREPS_KENDALL_MASKS");  // "global": masks from L2 (A/B timing)
+  c.use_lds = need <= cap && !(e && strcmp(e, "global") == 0);
   const size_t per_block = std::max(c.use_lds ? need : (size_t)0, KW_STATIC_LDS);
-  const int per_cu = std::max<int>(1, std::min<int>(2, (int)(cap / per_block)));
+  const int per_cu = std::max<int>(1, std::min<int>(VR_KW_MINB, (int)(cap / per_block)));
   c.grid = num_cus() * per_cu;
   c.nwaves = c.grid * KW_WAVES;
   c.lds = per_block;  // masks (LDS) and, after the walk, the partials
@@ -355,7 +360,7 @@ __device__ inline void kw_block_summary(const KSeg& a, bool seen, uint32_t incl,
 }
 
 template <bool LDS, bool TIE>
-__global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
+__global__ __launch_bounds__(KW_THREADS, VR_KW_MINB) void k_kwalk(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ sflag,
     const uint32_t* __restrict__ aux, int64_t M, const uint64_t* __restrict__ gmask, int64_t n,
     int nl, uint32_t nwaves, uint64_t* __restrict__ w_acc, uint64_t* __restrict__ w_g,
@@ -435,7 +440,7 @@ __global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk(
 // pair codes (the x-lex order), so one walk shares the code loads, mask lookups and
 // transposes; three segment states, three block summaries (one k_kfix each).
 template <bool LDS>
-__global__ __launch_bounds__(KW_THREADS, 2) void k_kwalk_top3(
+__global__ __launch_bounds__(KW_THREADS, VR_KW_MINB) void k_kwalk_top3(
     const uint32_t* __restrict__ codes, const uint32_t* __restrict__ s0, const uint32_t* __restrict__ x0p,
     const uint32_t* __restrict__ s1, const uint32_t* __restrict__ x1p, const uint32_t* __restrict__ s2,
     const uint32_t* __restrict__ x2p, int64_t M, const uint64_t* __restrict__ gmask, int64_t n, int nl,
