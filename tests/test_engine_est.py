@@ -314,6 +314,13 @@ def test_grid_equals_per_region_calls(dev, na):
     with exact_engine():  # the exact form runs the per-region calls
         ex = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
     assert np.array_equal(ex, got)
+    ktimer_enable(True)
+    with exact_engine(), _exact_grid():  # or region-fused (opt-in, k_rankB_gridx)
+        ex = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    gridx_launches = ktimer_read("k_rankB_gridx")[1]
+    ktimer_enable(False)
+    assert gridx_launches == 3 * len(models), "the exact grid walk: one launch per model plan and pass"
+    assert np.array_equal(ex, got)
 
 
 def test_grid_falls_back_on_a_structured_region(dev):
@@ -419,6 +426,91 @@ def test_grid_structured_region_leaves_the_others_fused(dev):
     for a, pn in enumerate(neurals):
         ref = R.bootstrap_spearman_multi(pn, models, idx, full_first=True).cpu().numpy()
         assert np.array_equal(got[a], ref)
+
+
+class _exact_grid:
+    """Context: the region-fused exact walk (VISREPS_ENGINE_GRIDX=1, opt-in)."""
+
+    def __enter__(self):
+        os.environ["VISREPS_ENGINE_GRIDX"] = "1"
+
+    def __exit__(self, *a):
+        os.environ.pop("VISREPS_ENGINE_GRIDX", None)
+
+
+def _structured_rdm(dev, n, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    u = torch.empty(n, device=dev).exponential_(1.0, generator=g) ** 2
+    s = u[:, None] + u[None, :] + 0.05 * torch.rand(n, n, device=dev, generator=g)
+    s = torch.triu(s, 1)
+    return s + s.T
+
+
+def test_grid_structured_regions_walk_the_exact_grid(dev):
+    # VERDICT r5 #3: regions whose estimate fails the up-front check go to the exact form; with
+    # the exact grid on, two or more of them walk it region-fused (k_rankB_gridx), the
+    # continuous ones stay in the EST grid, and every score equals the per-region calls (and
+    # the default, the structured regions' own exact calls)
+    from visreps_amd._lib import ktimer_enable, ktimer_read
+
+    n = 5000
+    neurals = [R.RankPlan(_structured_rdm(dev, n, 7)), R.RankPlan(_rdm(dev, n, 80, 121)),
+               R.RankPlan(_structured_rdm(dev, n, 8)), R.RankPlan(_rdm(dev, n, 90, 122))]
+    models = [R.RankPlan(_rdm(dev, n, 60, 123)), R.RankPlan(_rdm(dev, n, 60, 124, relu=True))]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 100)  # 101 subsets: 2 passes
+    sj = R.SharedJoins(neurals)
+    joins = [sj.join(pm) for pm in models]
+    p0, r0 = int(lib().vr_engine_est_predicted()), int(lib().vr_engine_est_reruns())
+    ktimer_enable(True)
+    with _exact_grid():
+        got = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    est_launches = ktimer_read("k_rankB_grid")[1]
+    gridx_launches = ktimer_read("k_rankB_gridx")[1]
+    ktimer_enable(False)
+    assert int(lib().vr_engine_est_predicted()) - p0 == 2, "both structured regions go exact up front"
+    assert est_launches == 1 * len(models), "the two continuous regions stay in the EST grid (pass 1)"
+    # (region 0 is off the estimate: the fused walk takes its window parameters from a fused
+    # region's workspace, so no pass of the continuous regions is flagged)
+    assert int(lib().vr_engine_est_reruns()) - r0 == 0
+    assert gridx_launches == 2 * len(models), "the two structured regions walk the exact grid"
+    for a, pn in enumerate(neurals):
+        ref = R.bootstrap_spearman_multi(pn, models, idx, full_first=True).cpu().numpy()
+        assert np.array_equal(got[a], ref), a
+    p1, r1 = int(lib().vr_engine_est_predicted()), int(lib().vr_engine_est_reruns())
+    off = R.bootstrap_spearman_grid(neurals, models, idx, joins, full_first=True).cpu().numpy()
+    assert int(lib().vr_engine_est_predicted()) - p1 == 2 and int(lib().vr_engine_est_reruns()) - r1 == 0
+    assert np.array_equal(off, got)
+
+
+def test_exact_grid_ties_and_l2_masks(dev, monkeypatch):
+    # the exact grid walk with tied A plans (chunks that start after c L, the chunk lookup's
+    # step back), tied and quantised B plans, 4 and 2 regions, masks from L2 too
+    from visreps_amd._lib import ktimer_enable, ktimer_read
+
+    n = 1800
+    neurals = [R.RankPlan((_rdm(dev, n, 40 + 10 * i, 130 + i) * 1024).floor() / 1024) for i in range(3)]
+    neurals.append(R.RankPlan(_rdm(dev, n, 70, 134, relu=True)))
+    q = (_rdm(dev, n, 40, 135) * 64).floor() / 64
+    models = [R.RankPlan(_rdm(dev, n, 70, 136, relu=True)), R.RankPlan(q)]
+    idx = bootstrap_indices(42, n, int(0.9 * n), 130)
+    sj = R.SharedJoins(neurals)
+    joins = [sj.join(pm) for pm in models]
+    monkeypatch.setenv("VISREPS_ENGINE_GRIDX", "1")
+    with exact_engine():
+        refs = [R.bootstrap_spearman_multi(pn, models, idx, full_first=True,
+                                           joined=[joins[m][a] for m in range(len(models))]).cpu().numpy()
+                for a, pn in enumerate(neurals)]
+        for lds in ("1", "0"):
+            monkeypatch.setenv("VISREPS_ENGINE_GRID_LDS", lds)
+            for na in (4, 2):
+                ktimer_enable(True)
+                got = R.bootstrap_spearman_grid(neurals[:na], models, idx, [js[:na] for js in joins],
+                                                full_first=True).cpu().numpy()
+                launches = ktimer_read("k_rankB_gridx")[1]
+                ktimer_enable(False)
+                assert launches == 3 * len(models), (lds, na)
+                for a in range(na):
+                    assert np.array_equal(got[a], refs[a]), (lds, na, a)
 
 
 @pytest.mark.parametrize("n", [12000, 20500])

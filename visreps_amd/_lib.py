@@ -309,7 +309,7 @@ workspace = _WorkspacePool()
 KTIMER_KERNELS = {"k_rankB_est": 0, "k_rankB_exact": 1, "k_rankA": 2, "k_join": 3,
                   "k_gram_wide": 4, "k_gram_tile": 5, "k_countA": 6, "k_rankB_full": 7,
                   "k_kwalk": 8, "k_cov": 9, "k_join4": 10,
-                  "k_full_corr": 11, "k_rankB_grid": 12}
+                  "k_full_corr": 11, "k_rankB_grid": 12, "k_rankB_gridx": 13}
 
 
 def ktimer_enable(on: bool = True) -> None:

@@ -1888,6 +1888,169 @@ __global__ __launch_bounds__(ENG_THREADS, VR_GRID_MINW) void k_rankB_grid(
 }
 
 // ---------------------------------------------------------------------------------
+// Exact grid B walk: k_rankB_grid's region fusion in the exact chunk-base form (every pass
+// with VISREPS_ENGINE_EST=0, and the regions of a grid call whose estimate fails its up-front
+// check). Per pair and region yA = 2 baseA[chunk] + TB[posA] (u16 chunk-relative ranks:
+// narrow A plans), as in k_rankB's exact form; the A chunk of a position is found here from
+// the region's chunk starts (cst: the last c <= pos / L whose start is <= pos, k_join's rule),
+// so the shared joins' A positions serve the exact form too (no per-unit chunk joins). Same
+// integer sums as the per-region exact walks: scores bit-identical to them.
+// ---------------------------------------------------------------------------------
+struct GridX {
+  const uint16_t* TB[4];     // each region's chunk-relative doubled ranks (u16)
+  const uint32_t* posA[4];   // B position -> A position, per region
+  const uint32_t* base[4];   // [nch][64] absolute included count at each A chunk start
+  const uint32_t* cst[4];    // [nch] A chunk start positions
+  uint32_t* seg_tot[4];
+  uint64_t* seg_part[4];
+};
+#ifndef VR_GRIDX_NB
+#define VR_GRIDX_NB 2  // pairs per gather batch (x R regions x 2 loads in flight, two batches);
+#endif                 // 1 at R = 4, whose 2-pair batches do not fit 128 VGPRs
+// chunk of A position pa: q = pa / L from the reciprocal Lm = floor(2^32 / L) (q is exact or
+// one low), then back over chunk starts above pa (group-aligned chunks start at or after c L)
+__device__ inline uint32_t a_chunk(uint32_t pa, const uint32_t* __restrict__ cst, uint32_t L, uint32_t Lm,
+                                   uint32_t nch) {
+  uint32_t q = __umulhi(pa, Lm);
+  if ((q + 1u) * L <= pa) ++q;
+  q = min(q, nch - 1u);
+  while (q > 0u && cst[q] > pa) --q;
+  return q;
+}
+template <int R, bool LDS>
+__global__ __launch_bounds__(ENG_THREADS, VR_GRID_MINW) void k_rankB_gridx(
+    const uint32_t* __restrict__ codes, const uint32_t* __restrict__ gflag, const uint64_t* __restrict__ gmask,
+    int64_t n, GridX g, uint32_t nseg, uint32_t L, uint32_t Lm, uint32_t nch, const uint32_t* __restrict__ segpos,
+    uint32_t* __restrict__ queue) {
+  constexpr int NB = R >= 4 ? 1 : VR_GRIDX_NB;
+  static_assert(64 % NB == 0, "batch");
+  extern __shared__ uint64_t smask[];
+  const uint64_t* m = stage_masks<LDS>(gmask, n, smask);
+  const int lane = threadIdx.x & 63;
+  const uint32_t lane_off = (uint32_t)lane;
+  for (;;) {
+    const uint32_t sidx = next_segment(queue);
+    if (sidx >= nseg) break;
+    const uint32_t P0 = segpos[sidx], P1 = segpos[sidx + 1];
+    u128 acc[R];
+    uint64_t St[R], S[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0, St[r] = 0, S[r] = 0;
+    uint64_t tie = 0;
+    u128 tie_unused = 0;
+    uint32_t cw = 0, cgs = 0;
+    if (P0 < P1) {
+      auto close = [&](uint32_t ce) {
+        const uint32_t y = cgs + ce + 1u;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          acc[r] += (u128)S[r] * y;
+          St[r] += S[r];
+          S[r] = 0;
+        }
+        tie_add<false>(tie, tie_unused, ce - cgs);
+        cgs = ce;
+      };
+      for (uint32_t w0 = P0 & ~63u; w0 < P1; w0 += 64) {
+        const uint32_t pos = w0 + (uint32_t)lane;
+        const bool valid = pos >= P0 && pos < P1;
+        const uint32_t cd = valid ? codes[pos] : 0u;
+        uint32_t pa[R], ca[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          pa[r] = valid ? g.posA[r][pos] : 0u;
+          ca[r] = a_chunk(pa[r], g.cst[r], L, Lm, nch);
+        }
+        const uint64_t x = window_bits<VR_XPOSE_B>(m, cd, w0, P0, P1, lane, true);
+        const uint64_t F =
+            restrict_flags(((uint64_t)sload(gflag + (w0 >> 5) + 1) << 32) | sload(gflag + (w0 >> 5)), w0, P0, P1);
+        // batch h's rows, t / b[r][q] = region r's TB entry / chunk base of pair h NB + q
+        auto issue = [&](int h, uint32_t (&t)[R][NB], uint32_t (&b)[R][NB]) {
+#pragma unroll
+          for (int q = 0; q < NB; ++q)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              t[r][q] = __builtin_nontemporal_load(g.TB[r] + (size_t)readlane_u32(pa[r], h * NB + q) * LANES + lane_off);
+              b[r][q] = g.base[r][(size_t)readlane_u32(ca[r], h * NB + q) * LANES + lane_off];
+            }
+        };
+        uint32_t tb[2][R][NB], bb[2][R][NB];
+        if (F == ~0ull) {  // every position starts a group (k_rankB's per-window form explains)
+          close(cw);
+          uint64_t a64[R];
+#pragma unroll
+          for (int r = 0; r < R; ++r) a64[r] = 0;
+          uint32_t c1 = cw + 1u;
+          issue(0, tb[0], bb[0]);
+#pragma unroll
+          for (int h = 0; h < 64 / NB; ++h) {
+            if (h + 1 < 64 / NB) issue(h + 1, tb[(h + 1) & 1], bb[(h + 1) & 1]);
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+              const uint32_t j = h * NB + q;
+              const uint32_t mk = (uint32_t)((int32_t)((uint32_t)(x >> (j & 32u)) << (31u - (j & 31u))) >> 31);
+#pragma unroll
+              for (int r = 0; r < R; ++r) {
+                const uint32_t y = 2u * bb[h & 1][r][q] + tb[h & 1][r][q];
+                if (j < 63) {
+                  const uint32_t yb = y & mk;
+                  a64[r] += (uint64_t)yb * c1;
+                  St[r] += yb;
+                } else {
+                  S[r] = y & mk;
+                }
+              }
+              if (j < 63)
+                c1 -= mk;
+              else
+                cgs = c1 - 1u;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < R; ++r) acc[r] += (u128)a64[r] * 2u;
+        } else {
+          issue(0, tb[0], bb[0]);
+#pragma unroll
+          for (int h = 0; h < 64 / NB; ++h) {
+            if (h + 1 < 64 / NB) issue(h + 1, tb[(h + 1) & 1], bb[(h + 1) & 1]);
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+              const uint32_t j = h * NB + q;
+              if ((F >> j) & 1ull) close(cw + popc64(x & lowmask(j)));
+              const bool in = (x >> j) & 1ull;
+#pragma unroll
+              for (int r = 0; r < R; ++r) {
+                const uint32_t y = 2u * bb[h & 1][r][q] + tb[h & 1][r][q];
+                S[r] += in ? (uint64_t)y : 0ull;
+              }
+            }
+          }
+        }
+        cw += popc64(x);
+      }
+      if ((P1 & 63u) == 0) close(cw);  // a 64-aligned segment end is in no window
+    }
+    const size_t o = (size_t)sidx * LANES + lane, fs = (size_t)nseg * LANES;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      g.seg_tot[r][o] = cw;
+      g.seg_part[r][PB_ACCL * fs + o] = (uint64_t)acc[r];
+      g.seg_part[r][PB_ACCH * fs + o] = (uint64_t)(acc[r] >> 64);
+      g.seg_part[r][PB_ST * fs + o] = St[r];
+      g.seg_part[r][PB_TIEL * fs + o] = tie;
+      g.seg_part[r][PB_TIEH * fs + o] = 0;
+    }
+  }
+}
+
+// chunk start positions of an A plan: cst[c] = gstart[chunk_g[c]]
+__global__ void k_chunk_starts(const uint32_t* __restrict__ gstart, const uint32_t* __restrict__ chunk_g,
+                               uint32_t nch, uint32_t* __restrict__ cst) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < nch) cst[c] = gstart[chunk_g[c]];
+}
+
+// ---------------------------------------------------------------------------------
 // final combination
 // ---------------------------------------------------------------------------------
 __device__ inline double i128_to_f64(i128 x) {
@@ -2647,6 +2810,114 @@ static bool grid_masks_lds(int64_t n) {
   return (size_t)n * sizeof(uint64_t) <= 160 * 1024 - 1024 && env_int("VISREPS_ENGINE_GRID_LDS", 1) != 0;
 }
 
+template <bool LDS>
+static int launch_gridx(int R, unsigned grid, size_t lds, const PlanView& B, const uint64_t* masks, int64_t n,
+                        const GridX& g, uint32_t ns, uint32_t L, uint32_t Lm, uint32_t nch, const uint32_t* segpos,
+                        uint32_t* q, hipStream_t st) {
+  VR_ONCE(VR_TRY(allow_big_lds(k_rankB_gridx<2, LDS>)); VR_TRY(allow_big_lds(k_rankB_gridx<3, LDS>));
+          VR_TRY(allow_big_lds(k_rankB_gridx<4, LDS>)));
+  if (R == 2)
+    k_rankB_gridx<2, LDS><<<grid, ENG_THREADS, lds, st>>>(B.codes, B.gflag, masks, n, g, ns, L, Lm, nch, segpos, q);
+  else if (R == 3)
+    k_rankB_gridx<3, LDS><<<grid, ENG_THREADS, lds, st>>>(B.codes, B.gflag, masks, n, g, ns, L, Lm, nch, segpos, q);
+  else
+    k_rankB_gridx<4, LDS><<<grid, ENG_THREADS, lds, st>>>(B.codes, B.gflag, masks, n, g, ns, L, Lm, nch, segpos, q);
+  VR_CHECK_LAUNCH();
+  return VR_OK;
+}
+
+// A region a grid call can walk in the exact grid form: u16 chunk-relative ranks (every A
+// chunk span, < L + its largest tie group, <= 32767) and 64-bit tie sums (groups < 2^16)
+static bool gridx_region_ok(const PlanHeader& h) {
+  return (uint64_t)PLAN_L + h.max_group <= 32767u && h.max_group < 65536u;
+}
+
+// Every pass of regions rs (2..4 of them, gridx_region_ok; B tie groups < 2^16) in the exact
+// chunk-base form, region-fused: per pass the masks once, each region's exact A walk
+// (pass_a: TB, chunk bases), then one k_rankB_gridx launch per B plan for all of them, then
+// each region's tail. B segments: cfg.nwaves per plan (the exact A side's count, so the tail
+// pairs them as the per-region exact calls do). E: the grid's workspaces (E[r].masks = the
+// shared masks); region 0's B segment tables and queue counters are rewritten.
+static int grid_exact(const PlanView* As, const std::vector<int>& rs, const PlanView* Bs, int64_t nb, int64_t n,
+                      const int32_t* idx, int64_t k, int64_t n_sets, int full_first, double* scores,
+                      int64_t score_ld, uint32_t* const* const* joins, const std::vector<EngineWs>& E,
+                      const std::vector<PlanHeader>& hA, const std::vector<char>& nan_b, const EngineCfg& cfg,
+                      hipStream_t st) {
+  const int64_t M = pairs_of(n);
+  const int64_t total = n_sets + (full_first ? 1 : 0);
+  const int RA = (int)rs.size();
+  VR_REQUIRE(RA >= 2 && RA <= 4, "grid_exact: %d regions", RA);
+  const uint32_t nch = plan_nchunks(M), L = plan_chunk_len(M);
+  const uint32_t Lm = (uint32_t)(((uint64_t)1 << 32) / L);
+  const uint32_t nsx = (uint32_t)cfg.nwaves;
+  VR_REQUIRE(E[0].segstride >= (size_t)nsx + 1 && E[0].useg >= (size_t)nsx * LANES, "grid_exact: segment tables");
+  for (int64_t j = 0; j < nb; ++j) {
+    k_seg_table<<<(nsx + 256) / 256, 256, 0, st>>>(Bs[j].gstart, Bs[j].hdr, M, nsx,
+                                                    E[0].segposB + E[0].segstride * (size_t)j);
+    VR_CHECK_LAUNCH();
+  }
+  for (int r : rs) VR_CHECK_HIP(hipMemsetAsync(E[(size_t)r].viol + EST_MAX_PASSES, 0, sizeof(uint32_t), st));
+  const unsigned ggrid = (unsigned)num_cus();
+  const bool glds = grid_masks_lds(n);
+  // regions per launch: all, or (VISREPS_ENGINE_GRIDX_MAXR < 4, A/B) 4 regions as 2 + 2
+  const int maxr = (RA == 4 && env_int("VISREPS_ENGINE_GRIDX_MAXR", 4) < 4) ? 2 : RA;
+  const int64_t npass = (total + LANES - 1) / LANES;
+  for (int64_t p = 0; p < npass; ++p) {
+    const int64_t set0 = p * LANES;
+    const int nl = (int)std::min<int64_t>(LANES, total - set0);
+    VR_TRY(build_pass_masks(idx, k, set0, nl, full_first, E[0].masks, n, st));
+    for (int r : rs) {
+      const EngineWs& e = E[(size_t)r];
+      VR_TRY((cfg.use_lds ? pass_a<true, true, uint16_t, false>(As[r], n, e, LANES, cfg, st)
+                          : pass_a<false, true, uint16_t, false>(As[r], n, e, LANES, cfg, st)));
+      // the chunk starts go to lpA, dead once pass_a has turned it into baseA
+      k_chunk_starts<<<(nch + 255) / 256, 256, 0, st>>>(As[r].gstart, As[r].chunk_g, nch, e.lpA);
+      VR_CHECK_LAUNCH();
+    }
+    VR_CHECK_HIP(hipMemsetAsync(E[0].queue + QS_RANKB, 0,
+                                sizeof(uint32_t) * (size_t)std::min<int64_t>(nb, QSLOTS - QS_RANKB), st));
+    for (int64_t j = 0; j < nb; ++j) {
+      const uint32_t* segpos = E[0].segposB + E[0].segstride * (size_t)j;
+      for (int i0 = 0; i0 < RA; i0 += maxr) {  // region groups of <= maxr per launch
+        const int ri = std::min(maxr, RA - i0);
+        GridX g{};
+        for (int i = 0; i < ri; ++i) {
+          const int r = rs[(size_t)(i0 + i)];
+          const EngineWs& e = E[(size_t)r];
+          const size_t us = e.useg * (size_t)j;
+          g.TB[i] = static_cast<const uint16_t*>(e.TB);
+          g.posA[i] = joins[r][2 * j];
+          g.base[i] = e.baseA;
+          g.cst[i] = e.lpA;
+          g.seg_tot[i] = e.segB_tot + us;
+          g.seg_part[i] = e.segB_part + us * PB_N;
+        }
+        uint32_t* q = E[0].queue + QS_RANKB + (size_t)(j * 2 + i0 / maxr) % (size_t)(QSLOTS - QS_RANKB);
+        VR_CHECK_HIP(hipMemsetAsync(q, 0, sizeof(uint32_t), st));
+        KtScope kt(KT_RANKB_GRIDX, (double)M * ri, st);
+        if (glds)
+          VR_TRY(launch_gridx<true>(ri, ggrid, (size_t)n * sizeof(uint64_t), Bs[j], E[0].masks, n, g, nsx, L, Lm, nch,
+                                    segpos, q, st));
+        else
+          VR_TRY(launch_gridx<false>(ri, ggrid, 0, Bs[j], E[0].masks, n, g, nsx, L, Lm, nch, segpos, q, st));
+      }
+    }
+    for (int r : rs)
+      VR_TRY(tail_units(E[(size_t)r], nb, nsx, 1u, hA[(size_t)r].has_nan != 0, nan_b, nl,
+                        scores + (size_t)r * nb * score_ld + set0, score_ld, E[(size_t)r].viol + EST_MAX_PASSES, st));
+  }
+  for (int r : rs) {  // an exact pass that breaks the invariants is an error, as in run_engine_multi
+    uint32_t bad = 0;
+    VR_CHECK_HIP(hipMemcpyAsync(&bad, E[(size_t)r].viol + EST_MAX_PASSES, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    VR_CHECK_HIP(hipStreamSynchronize(st));
+    if (bad) {
+      set_error("bootstrap engine: an exact grid pass broke the rank-sum invariants (included pairs / sum of ranks)");
+      return VR_EINTERNAL;
+    }
+  }
+  return VR_OK;
+}
+
 static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_t nb, int64_t n, const int32_t* idx,
                            int64_t k, int64_t n_sets, int full_first, double* scores, int64_t score_ld,
                            uint32_t* const* const* joins, const EngineWs* Es, const EngineCfg& cfg, hipStream_t st) {
@@ -2654,7 +2925,14 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
   const int64_t total = n_sets + (full_first ? 1 : 0);
   std::vector<int> solo;  // regions run on their own once the fused passes are done
   std::vector<std::vector<int64_t>> fix((size_t)R);  // fused regions' flagged passes (re-run exact)
+  std::vector<int> xg;  // regions walked together in the exact grid form (grid_exact), before the solos
+  std::vector<PlanHeader> hA((size_t)R), hB((size_t)nb);
+  std::vector<char> nan_b((size_t)nb);
+  std::vector<EngineWs> E(Es, Es + R);  // the masks of a pass are built once (region 0's buffer)
+  for (int r = 1; r < R; ++r) E[(size_t)r].masks = E[0].masks;
   auto finish = [&]() -> int {
+    if (!xg.empty())
+      VR_TRY(grid_exact(As, xg, Bs, nb, n, idx, k, n_sets, full_first, scores, score_ld, joins, E, hA, nan_b, cfg, st));
     for (int r : solo)
       VR_TRY(run_engine_multi(As[r], Bs, nb, n, idx, k, n_sets, full_first, scores + (size_t)r * nb * score_ld,
                               score_ld, joins[r], Es[0], LANES, cfg, st));
@@ -2666,36 +2944,57 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
   };
   auto all_solo = [&]() -> int {
     solo.clear();
-    for (int r = 0; r < R; ++r) solo.push_back(r);
+    for (int r = 0; r < R; ++r)
+      if (std::find(xg.begin(), xg.end(), r) == xg.end()) solo.push_back(r);
     return finish();
   };
   if (total == 0 || nb == 0 || M == 0) return all_solo();
-  std::vector<PlanHeader> hA((size_t)R), hB((size_t)nb);
   for (int r = 0; r < R; ++r)
     VR_CHECK_HIP(hipMemcpyAsync(&hA[(size_t)r], As[r].hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
   for (int64_t j = 0; j < nb; ++j)
     VR_CHECK_HIP(hipMemcpyAsync(&hB[(size_t)j], Bs[j].hdr, sizeof(PlanHeader), hipMemcpyDeviceToHost, st));
   VR_CHECK_HIP(hipStreamSynchronize(st));
-  bool fused = engine_est() && cfg.est_mode == 3 && R >= 2 && R <= 4 && env_int("VISREPS_ENGINE_TRI", 0) == 0 &&
+  for (int64_t j = 0; j < nb; ++j) nan_b[(size_t)j] = hB[(size_t)j].has_nan != 0;
+  bool b_small = true;  // B tie groups < 2^16 (the fused walks' 64-bit tie sums)
+  for (int64_t j = 0; j < nb; ++j) b_small = b_small && hB[(size_t)j].max_group < 65536u;
+  // the exact grid form (opt-in, VISREPS_ENGINE_GRIDX=1): measured slower than the per-region
+  // exact calls on the bench RDMs (36.2-36.9 against 33.8 ms per unit, every pass exact,
+  // profiles/r6_exact_grid_ab.log): one 16-wave workgroup per CU, which the LDS masks and
+  // 128 VGPRs allow, cannot keep the two gathers per pair and region in flight that the
+  // per-region walks' two workgroups per CU do
+  const bool gridx = b_small && R >= 2 && R <= 4 && env_int("VISREPS_ENGINE_GRID", 1) != 0 &&
+                     env_int("VISREPS_ENGINE_GRIDX", 0) != 0;
+  auto take_exact_grid = [&](const std::vector<int>& rs) -> std::vector<int> {  // -> the regions left over
+    std::vector<int> ok, rest;
+    for (int r : rs) (gridx && gridx_region_ok(hA[(size_t)r]) ? ok : rest).push_back(r);
+    if (ok.size() >= 2)
+      xg.insert(xg.end(), ok.begin(), ok.end());
+    else
+      rest.insert(rest.end(), ok.begin(), ok.end());
+    std::sort(xg.begin(), xg.end());
+    return rest;
+  };
+  if (!engine_est()) {  // every pass exact: the exact grid where it applies
+    std::vector<int> all;
+    for (int r = 0; r < R; ++r) all.push_back(r);
+    take_exact_grid(all);
+    return all_solo();
+  }
+  bool fused = cfg.est_mode == 3 && R >= 2 && R <= 4 && env_int("VISREPS_ENGINE_TRI", 0) == 0 &&
                env_int("VISREPS_ENGINE_LO_JOIN", 0) == 0 && env_int("VISREPS_ENGINE_GRID", 1) != 0;
   // test hook (vr_test_engine_inject): the first fused region's TB gets the B-side error after
   // its A walk of that pass, so the region must be flagged and re-run on its own
   const int64_t inject = g_test_inject.load(std::memory_order_relaxed);
-  for (int64_t j = 0; j < nb && fused; ++j) fused = hB[(size_t)j].max_group < 65536u;
+  fused = fused && b_small;
   if (!fused) return all_solo();
   std::vector<int> act;  // the fused regions
   for (int r = 0; r < R; ++r) (hA[(size_t)r].max_group < 65536u ? act : solo).push_back(r);
-  std::vector<char> nan_b((size_t)nb);
-  for (int64_t j = 0; j < nb; ++j) nan_b[(size_t)j] = hB[(size_t)j].has_nan != 0;
   // (a point-only call holds the full set alone: its window is the full set's, so lane 0's
   // EST 4 shift is at most 1 -- with k's window instead a group of > 3 tied pairs could
   // shift below 1 and flag the pass)
   const uint2 e3 = est3_params(n_sets > 0 ? k : n, M);
   const uint2 trip = make_uint2(0u, 0u);
   const uint32_t ns = cfg.est_nseg, nsA = cfg.est_nsegA;
-  // the masks of a pass are built once (region 0's buffer) and read by every region
-  std::vector<EngineWs> E(Es, Es + R);
-  for (int r = 1; r < R; ++r) E[(size_t)r].masks = E[0].masks;
   // A-side walks: masks in LDS when two 16-wave workgroups per CU hold them (n <= 10,176),
   // else from L2 (the per-region calls' choice, engine_cfg)
   auto est_a = [&](auto&& fn) -> int {
@@ -2713,16 +3012,25 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
   if (n_sets > 0 && env_int("VISREPS_ENGINE_EST_PREDICT", 1) != 0) {
     const int nl0 = (int)std::min<int64_t>(LANES, total);
     VR_TRY(build_pass_masks(idx, k, 0, nl0, full_first, E[0].masks, n, st));
-    std::vector<int> keep;
+    std::vector<int> keep, pbad;
     for (int r : act) {
       bool bad = false;
       VR_TRY(est_a([&](auto cl) -> int {
         return est_predict<decltype(cl)::value, true>(As[r], n, E[(size_t)r], LANES, nl0, full_first != 0, cfg, e3,
                                                       st, bad);
       }));
-      (bad ? solo : keep).push_back(r);
+      (bad ? pbad : keep).push_back(r);
     }
     act.swap(keep);
+    // Regions off the estimate go to the exact form (run_engine_multi's choice while the exact
+    // walks keep their masks in LDS; above that EST 1 serves them on their own): two or more of
+    // them walk it region-fused
+    if (cfg.use_lds || env_int("VISREPS_ENGINE_EST1_FALLBACK", 1) == 0) {
+      for (int r : take_exact_grid(pbad)) solo.push_back(r);
+      g_est_predicted.fetch_add((int64_t)xg.size());
+    } else {
+      for (int r : pbad) solo.push_back(r);
+    }
   }
   if (act.size() < 2) return all_solo();  // fusing pays with two regions or more
   const int64_t npass = (total + LANES - 1) / LANES;
@@ -2765,12 +3073,15 @@ static int run_engine_grid(const PlanView* As, int R, const PlanView* Bs, int64_
       uint32_t* q = E[0].queue + QS_RANKB + (size_t)j % (size_t)(QSLOTS - QS_RANKB);
       if (j >= QSLOTS - QS_RANKB) VR_CHECK_HIP(hipMemsetAsync(q, 0, sizeof(uint32_t), st));
       const uint32_t* segpos = E[0].segposB + E[0].segstride * (size_t)j;
+      // the window parameters of this pass (k_c0_u: the same for every region) from a fused
+      // region's workspace: region 0 may be running on its own
+      const uint2* ftab = E[(size_t)act[0]].ftab;
       KtScope kt(full0 ? KT_RANKB_FULL : KT_RANKB_GRID, (double)M * RA, st);
       if (glds)
-        VR_TRY(launch_grid<true>(RA, ggrid, (size_t)n * sizeof(uint64_t), Bs[j], E[0].masks, n, g, ns, E[0].ftab,
+        VR_TRY(launch_grid<true>(RA, ggrid, (size_t)n * sizeof(uint64_t), Bs[j], E[0].masks, n, g, ns, ftab,
                                  segpos, q, st));
       else
-        VR_TRY(launch_grid<false>(RA, ggrid, 0, Bs[j], E[0].masks, n, g, ns, E[0].ftab, segpos, q, st));
+        VR_TRY(launch_grid<false>(RA, ggrid, 0, Bs[j], E[0].masks, n, g, ns, ftab, segpos, q, st));
     }
     for (int r : act) {
       if (full0) {

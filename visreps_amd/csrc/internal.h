@@ -106,7 +106,8 @@ enum KtKernel : int {
   KT_JOIN4 = 10,      // k_join4: shared join of one B plan to up to 4 A plans (units = algorithmic bytes)
   KT_FULL_CORR = 11,  // k_full_corr: lane 0's shift sums of an EST 4 pass, per unit (4 B / pair streamed)
   KT_RANKB_GRID = 12,  // k_rankB_grid: one B plan x up to 4 regions, EST 3 (units: pairs x regions)
-  KT_N = 13
+  KT_RANKB_GRIDX = 13, // k_rankB_gridx: the same in the exact chunk-base form (units: pairs x regions)
+  KT_N = 14
 };
 bool ktimer_on();
 struct KtScope {
