@@ -841,6 +841,11 @@ def main():
                                                       "record of the 4 neural plans (random gather) + 4 B written "
                                                       "per region"),
                           "traffic": round(j4_pmc["bytes_per_launch"]) if j4_pmc else None}
+            if j4_pmc and j4["avg_us"]:
+                # each random 16-B record gather fills a whole 128-B L2 line: the kernel's own
+                # line traffic per launch time against HBM peak (profiles/r6_microbench_join.log)
+                roof_join4["traffic_rate_frac"] = round(
+                    j4_pmc["bytes_per_launch"] / (j4["avg_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
         roof_engine = {"bound": "hbm", "achieved": round(eng_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(eng_gbs / HBM_PEAK_GBS, 4),
                        "scope": ("whole engine calls (vr_bootstrap_spearman_multi[_joined]: A walks, B walks, "
