@@ -104,3 +104,16 @@ def test_checker_flags_violations():
            (8, "s_waitcnt vmcnt(0)", None), (12, "s_nop 0", None), (16, "v_add_u32_e32 v1, v10, v0", None),
            (20, "s_endpgm", None)]
     assert check_asm_gathers(bad)[1]
+
+
+def test_grid_walks_have_no_hazards_or_scratch():
+    # the region-fused walks (EST k_rankB_grid, exact k_rankB_gridx): no SGPR-base hazard on
+    # their asm loads, and the exact grid walk -- 1-pair batches at 4 regions -- uses no scratch
+    if not os.path.exists(ENGINE_O):
+        pytest.fail("visreps_amd/csrc/build/engine.o missing: run __graft_entry__.build() first")
+    res = check_object(ENGINE_O, r"k_rankB_grid")
+    assert sum("k_rankB_gridx" in k for k in res) == 6, sorted(res)
+    for name, r in res.items():
+        assert not r["problems"], (name, r["problems"][:5])
+        if "k_rankB_gridx" in name:
+            assert r["vgpr_spill_count"] == 0 and r["private_segment_fixed_size"] == 0, (name, r)
