@@ -500,8 +500,10 @@ def test_exact_grid_ties_and_l2_masks(dev, monkeypatch):
         refs = [R.bootstrap_spearman_multi(pn, models, idx, full_first=True,
                                            joined=[joins[m][a] for m in range(len(models))]).cpu().numpy()
                 for a, pn in enumerate(neurals)]
-        for lds in ("1", "0"):
-            monkeypatch.setenv("VISREPS_ENGINE_GRID_LDS", lds)
+        for lds in ("1", "0", "global"):  # grid walk masks in LDS / L2; "global": the A walks' too
+            monkeypatch.setenv("VISREPS_ENGINE_GRID_LDS", "0" if lds == "global" else lds)
+            if lds == "global":
+                monkeypatch.setenv("VISREPS_ENGINE_MASKS", "global")
             for na in (4, 2):
                 ktimer_enable(True)
                 got = R.bootstrap_spearman_grid(neurals[:na], models, idx, [js[:na] for js in joins],
